@@ -1,0 +1,221 @@
+"""bzip2_amd -- MI355X-native bzip2 compression (drop-in libbz2) -- Python host mirror.
+
+The product is the C-ABI shared library ``libbz2_amd.so`` built in this directory (SONAME
+``libbz2.so.1.0``): it exports the reference's 24 ``bzlib.h`` functions (reference
+libbz2.def:4-27) with the compression hot path on the GPU, plus the ``bzg_*`` engine entry
+points of ``include/bzg.h``.  This module binds both with ctypes so that tests and the
+benchmark call exactly what a C caller would call.
+
+There is no CPU fallback: if the library or a usable GPU is missing, compression raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+try:  # share torch's HIP runtime (its libamdhip64 carries SONAME libamdhip64.so.7)
+    import torch as _torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the C ABI
+    _torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbz2_amd.so")
+
+# bzlib.h return codes (reference bzlib.h:33-46)
+BZ_RUN, BZ_FLUSH, BZ_FINISH = 0, 1, 2
+BZ_OK, BZ_RUN_OK, BZ_FLUSH_OK, BZ_FINISH_OK, BZ_STREAM_END = 0, 1, 2, 3, 4
+BZ_SEQUENCE_ERROR, BZ_PARAM_ERROR, BZ_MEM_ERROR = -1, -2, -3
+BZ_DATA_ERROR, BZ_DATA_ERROR_MAGIC, BZ_IO_ERROR = -4, -5, -6
+BZ_UNEXPECTED_EOF, BZ_OUTBUFF_FULL, BZ_CONFIG_ERROR = -7, -8, -9
+
+BZG_FLAG_END_SEGMENT, BZG_FLAG_TAIL_MERGE, BZG_FLAG_TRAILER = 1, 2, 4
+
+EXPORTS = [
+    "BZ2_bzCompressInit", "BZ2_bzCompress", "BZ2_bzCompressEnd",
+    "BZ2_bzDecompressInit", "BZ2_bzDecompress", "BZ2_bzDecompressEnd",
+    "BZ2_bzReadOpen", "BZ2_bzReadClose", "BZ2_bzReadGetUnused", "BZ2_bzRead",
+    "BZ2_bzWriteOpen", "BZ2_bzWrite", "BZ2_bzWriteClose", "BZ2_bzWriteClose64",
+    "BZ2_bzBuffToBuffCompress", "BZ2_bzBuffToBuffDecompress", "BZ2_bzlibVersion",
+    "BZ2_bzopen", "BZ2_bzdopen", "BZ2_bzread", "BZ2_bzwrite", "BZ2_bzflush",
+    "BZ2_bzclose", "BZ2_bzerror",
+]
+ENGINE_EXPORTS = [
+    "bzg_stream_init", "bzg_compress_device", "bzg_compress_host", "bzg_compress_host_stream",
+    "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_last_stats",
+    "bzg_release", "bzg_device_ok",
+]
+
+
+class BzError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        super().__init__(f"{what}: bzlib error {code}")
+        self.code = code
+
+
+class bz_stream(ctypes.Structure):
+    """Byte-identical to the reference's bz_stream (bzlib.h:48-66)."""
+
+    _fields_ = [
+        ("next_in", ctypes.c_void_p), ("avail_in", ctypes.c_uint),
+        ("total_in_lo32", ctypes.c_uint), ("total_in_hi32", ctypes.c_uint),
+        ("next_out", ctypes.c_void_p), ("avail_out", ctypes.c_uint),
+        ("total_out_lo32", ctypes.c_uint), ("total_out_hi32", ctypes.c_uint),
+        ("state", ctypes.c_void_p),
+        ("bzalloc", ctypes.c_void_p), ("bzfree", ctypes.c_void_p), ("opaque", ctypes.c_void_p),
+    ]
+
+
+class bzg_stream_state(ctypes.Structure):
+    _fields_ = [
+        ("combined_crc", ctypes.c_uint32), ("blocks_done", ctypes.c_uint32),
+        ("carry_byte", ctypes.c_uint8), ("carry_bits", ctypes.c_uint8),
+        ("header_done", ctypes.c_uint8), ("level", ctypes.c_uint8),
+    ]
+
+
+class bzg_stats(ctypes.Structure):
+    _fields_ = [
+        ("rle1_ms", ctypes.c_float), ("bwt_ms", ctypes.c_float), ("mtf_ms", ctypes.c_float),
+        ("code_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
+        ("nblocks", ctypes.c_uint32), ("sort_iterations", ctypes.c_uint32),
+        ("rle_bytes", ctypes.c_uint64), ("sort_unsorted", ctypes.c_uint64),
+        ("mtf_symbols", ctypes.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The product library; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `make -C {HERE}` or __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        u64, u32, vp, ci = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int
+        L.BZ2_bzBuffToBuffCompress.argtypes = [vp, ctypes.POINTER(ctypes.c_uint), vp, ctypes.c_uint, ci, ci, ci]
+        L.BZ2_bzBuffToBuffDecompress.argtypes = [vp, ctypes.POINTER(ctypes.c_uint), vp, ctypes.c_uint, ci, ci]
+        L.BZ2_bzCompressInit.argtypes = [ctypes.POINTER(bz_stream), ci, ci, ci]
+        L.BZ2_bzCompress.argtypes = [ctypes.POINTER(bz_stream), ci]
+        L.BZ2_bzCompressEnd.argtypes = [ctypes.POINTER(bz_stream)]
+        L.BZ2_bzDecompressInit.argtypes = [ctypes.POINTER(bz_stream), ci, ci]
+        L.BZ2_bzDecompress.argtypes = [ctypes.POINTER(bz_stream)]
+        L.BZ2_bzDecompressEnd.argtypes = [ctypes.POINTER(bz_stream)]
+        L.BZ2_bzlibVersion.restype = ctypes.c_char_p
+        L.bzg_stream_init.argtypes = [ctypes.POINTER(bzg_stream_state), ci]
+        L.bzg_compress_device.argtypes = [vp, u64, ctypes.c_uint, ctypes.POINTER(bzg_stream_state), vp, u64,
+                                          ctypes.POINTER(u64), ctypes.POINTER(u64), vp]
+        L.bzg_compress_host.argtypes = [vp, u64, ci, vp, u64, ctypes.POINTER(u64)]
+        L.bzg_bound.argtypes = [u64]
+        L.bzg_bound.restype = u64
+        L.bzg_stage_rle1.argtypes = [vp, u64, ci, ci, vp, u64, vp, vp, ctypes.POINTER(u32), u32]
+        L.bzg_stage_bwt.argtypes = [vp, vp, u32, vp, vp]
+        L.bzg_stage_mtf.argtypes = [vp, vp, u32, vp, vp, vp, vp]
+        L.bzg_last_stats.argtypes = [ctypes.POINTER(bzg_stats)]
+        _lib = L
+    return _lib
+
+
+def device_ok() -> bool:
+    return bool(lib().bzg_device_ok())
+
+
+def version() -> str:
+    return lib().BZ2_bzlibVersion().decode()
+
+
+def bound(n: int) -> int:
+    return int(lib().bzg_bound(n))
+
+
+def buff_to_buff_compress(data: bytes, level: int = 9) -> bytes:
+    """BZ2_bzBuffToBuffCompress (reference bzlib.c:1309-1357): FINISH with all input."""
+    src = bytes(data)
+    cap = bound(len(src))
+    dst = ctypes.create_string_buffer(cap)
+    dl = ctypes.c_uint(cap)
+    rc = lib().BZ2_bzBuffToBuffCompress(dst, ctypes.byref(dl), src, len(src), level, 0, 30)
+    if rc != BZ_OK:
+        raise BzError(rc, "BZ2_bzBuffToBuffCompress")
+    return dst.raw[: dl.value]
+
+
+def buff_to_buff_decompress(data: bytes, out_cap: int) -> bytes:
+    dst = ctypes.create_string_buffer(max(out_cap, 1))
+    dl = ctypes.c_uint(out_cap)
+    rc = lib().BZ2_bzBuffToBuffDecompress(dst, ctypes.byref(dl), bytes(data), len(data), 0, 0)
+    if rc != BZ_OK:
+        raise BzError(rc, "BZ2_bzBuffToBuffDecompress")
+    return dst.raw[: dl.value]
+
+
+def stream_compress(chunks, level: int = 9, finish_with_last: bool = False, out_chunk: int = 1 << 16,
+                    flush_after=()) -> bytes:
+    """Drive BZ2_bzCompress like a streaming caller: every chunk with BZ_RUN (or, for the last
+    chunk when finish_with_last, with BZ_FINISH directly), then BZ_FINISH until
+    BZ_STREAM_END.  Chunk indices listed in flush_after are followed by BZ_FLUSH."""
+    L = lib()
+    strm = bz_stream()
+    rc = L.BZ2_bzCompressInit(ctypes.byref(strm), level, 0, 30)
+    if rc != BZ_OK:
+        raise BzError(rc, "BZ2_bzCompressInit")
+    out = bytearray()
+    obuf = ctypes.create_string_buffer(out_chunk)
+    keep = []
+
+    def pump(action, expect):
+        while True:
+            strm.next_out = ctypes.cast(obuf, ctypes.c_void_p)
+            strm.avail_out = out_chunk
+            r = L.BZ2_bzCompress(ctypes.byref(strm), action)
+            out.extend(obuf.raw[: out_chunk - strm.avail_out])
+            if r not in expect:
+                raise BzError(r, f"BZ2_bzCompress({action})")
+            return r
+
+    try:
+        chunks = list(chunks)
+        for i, c in enumerate(chunks):
+            buf = ctypes.create_string_buffer(bytes(c), len(c))
+            keep.append(buf)
+            strm.next_in = ctypes.cast(buf, ctypes.c_void_p)
+            strm.avail_in = len(c)
+            if finish_with_last and i == len(chunks) - 1:
+                break
+            while strm.avail_in > 0:
+                pump(BZ_RUN, (BZ_RUN_OK,))
+            if i in flush_after:
+                while pump(BZ_FLUSH, (BZ_FLUSH_OK, BZ_RUN_OK)) != BZ_RUN_OK:
+                    pass
+        if not (finish_with_last and chunks):
+            strm.avail_in = 0
+        while pump(BZ_FINISH, (BZ_FINISH_OK, BZ_STREAM_END)) != BZ_STREAM_END:
+            pass
+    finally:
+        L.BZ2_bzCompressEnd(ctypes.byref(strm))
+    return bytes(out)
+
+
+def compress_device(d_in_ptr: int, n: int, level: int, d_out_ptr: int, out_cap: int, *, flags=None,
+                    state: bzg_stream_state | None = None, stream_ptr: int = 0):
+    """bzg_compress_device on device-resident buffers.  Returns (out_bytes, consumed, state)."""
+    L = lib()
+    st = state if state is not None else bzg_stream_state()
+    if state is None:
+        L.bzg_stream_init(ctypes.byref(st), level)
+    if flags is None:
+        flags = BZG_FLAG_END_SEGMENT | BZG_FLAG_TRAILER | (BZG_FLAG_TAIL_MERGE if n else 0)
+    ob = ctypes.c_uint64(0)
+    cons = ctypes.c_uint64(0)
+    rc = L.bzg_compress_device(ctypes.c_void_p(d_in_ptr), n, flags, ctypes.byref(st), ctypes.c_void_p(d_out_ptr),
+                               out_cap, ctypes.byref(ob), ctypes.byref(cons), ctypes.c_void_p(stream_ptr or None))
+    if rc != BZ_OK:
+        raise BzError(rc, "bzg_compress_device")
+    return ob.value, cons.value, st
+
+
+def last_stats() -> dict:
+    s = bzg_stats()
+    lib().bzg_last_stats(ctypes.byref(s))
+    return {k: getattr(s, k) for k, _ in bzg_stats._fields_}

@@ -1,0 +1,508 @@
+// code.hip -- stages A7/A8/A3: coding-table optimisation, Huffman code lengths, canonical
+// codes, bit accounting and bit packing of every block, plus stream framing.
+//
+// Reference: sendMTFValues (compress.c:250-818), BZ2_hbMakeCodeLengths / BZ2_hbAssignCodes
+// (huffman.c:63-166), BZ2_compressBlock framing (compress.c:822-881).  One workgroup owns one
+// block for the table passes; selector groups of 50 symbols are costed in parallel and their
+// per-table symbol frequencies gathered with LDS atomics; each table's heap Huffman runs on
+// one lane with the reference's exact tie order.  Packing computes every field's bit offset
+// with block-level scans and ORs 32-bit big-endian words into the (zeroed) output.
+#include "stages.h"
+#include "scan.h"
+
+namespace bzg {
+
+namespace {
+constexpr int kT = 256;
+
+struct CodeLds {
+  uint32_t rfreq[kNGroups][kMaxAlpha];
+  uint32_t code[kNGroups][kMaxAlpha];
+  int32_t hweight[kNGroups][kMaxAlpha * 2];
+  int32_t hparent[kNGroups][kMaxAlpha * 2];
+  int32_t hheap[kNGroups][kMaxAlpha + 4];
+  uint8_t len[kNGroups][kMaxAlpha + 2];
+  uint8_t sel[kMaxSelectors + 4];
+  uint32_t freq[kMaxAlpha];
+  uint32_t sh[8];
+  uint32_t misc[16];
+};
+
+// BZ2_hbMakeCodeLengths (huffman.c:63-148) on one lane: leaf weight = max(freq,1) << 8 | 0,
+// merge = sum of weights | (1 + max depth); heap moves use strict '<'; rescale with
+// w = 1 + w/2 while any length exceeds max_len.
+__device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, int max_len, int32_t* heap,
+                                int32_t* weight, int32_t* parent) {
+  for (int i = 0; i < alpha; i++) weight[i + 1] = (int32_t)((freq[i] == 0 ? 1u : freq[i]) << 8);
+  for (int round = 0; round < 64; round++) {  // converges in a few rounds for valid tables
+    int nodes = alpha, nheap = 0;
+    heap[0] = 0;
+    weight[0] = 0;
+    parent[0] = -2;
+    for (int i = 1; i <= alpha; i++) {
+      parent[i] = -1;
+      heap[++nheap] = i;
+      int z = nheap, item = heap[z];
+      while (weight[item] < weight[heap[z >> 1]]) {
+        heap[z] = heap[z >> 1];
+        z >>= 1;
+      }
+      heap[z] = item;
+    }
+    while (nheap > 1) {
+      int pick[2];
+      for (int k = 0; k < 2; k++) {
+        pick[k] = heap[1];
+        heap[1] = heap[nheap--];
+        int z = 1, item = heap[1];
+        for (;;) {
+          int y = z << 1;
+          if (y > nheap) break;
+          if (y < nheap && weight[heap[y + 1]] < weight[heap[y]]) y++;
+          if (weight[item] < weight[heap[y]]) break;
+          heap[z] = heap[y];
+          z = y;
+        }
+        heap[z] = item;
+      }
+      nodes++;
+      parent[pick[0]] = parent[pick[1]] = nodes;
+      const int32_t w0 = weight[pick[0]], w1 = weight[pick[1]];
+      const int32_t d0 = w0 & 0xff, d1 = w1 & 0xff;
+      weight[nodes] = (int32_t)(((uint32_t)w0 & 0xffffff00u) + ((uint32_t)w1 & 0xffffff00u)) | (1 + (d0 > d1 ? d0 : d1));
+      parent[nodes] = -1;
+      heap[++nheap] = nodes;
+      int z = nheap, item = heap[z];
+      while (weight[item] < weight[heap[z >> 1]]) {
+        heap[z] = heap[z >> 1];
+        z >>= 1;
+      }
+      heap[z] = item;
+    }
+    bool too_long = false;
+    for (int i = 1; i <= alpha; i++) {
+      int d = 0, k = i;
+      while (parent[k] >= 0) {
+        k = parent[k];
+        d++;
+      }
+      len[i - 1] = (uint8_t)d;
+      if (d > max_len) too_long = true;
+    }
+    if (!too_long) return;
+    for (int i = 1; i <= alpha; i++) weight[i] = (1 + ((weight[i] >> 8) / 2)) << 8;
+  }
+}
+
+// Per-block table optimisation.  Outputs (global, per block b):
+//   lens[b][6][258], codes[b][6][258], sel[b][nsel] (table ids), selmtf[b][nsel],
+//   gbits[b][nsel] (payload bits per 50-group), info[b] = {nGroups, nSel, alpha, bits}
+__global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv, const uint32_t* __restrict__ mtf_off,
+                                               const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ freq_g,
+                                               const uint32_t* __restrict__ ninuse, const uint32_t* __restrict__ inuse,
+                                               uint8_t* __restrict__ lens_g, uint32_t* __restrict__ codes_g,
+                                               uint8_t* __restrict__ sel_g, uint8_t* __restrict__ selmtf_g,
+                                               uint16_t* __restrict__ gbits_g, uint32_t* __restrict__ info_g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  CodeLds& S = *reinterpret_cast<CodeLds*>(smem);
+  const uint32_t b = blockIdx.x;
+  const uint32_t nmtf = nmtf_g[b];
+  const uint16_t* mv = mtfv + mtf_off[b];
+  const int alpha = (int)ninuse[b] + 2;
+  const int ng = nmtf < 200 ? 2 : nmtf < 600 ? 3 : nmtf < 1200 ? 4 : nmtf < 2400 ? 5 : 6;
+  const uint32_t nsel = ceil_div(nmtf, kGroupSize);
+  for (int i = threadIdx.x; i < kMaxAlpha; i += kT) S.freq[i] = freq_g[(size_t)b * kMaxAlpha + i];
+  __syncthreads();
+  // initial tables (compress.c:276-319)
+  if (threadIdx.x == 0) {
+    for (int t = 0; t < ng; t++)
+      for (int v = 0; v < alpha; v++) S.len[t][v] = 15;
+    int part = ng, rem = (int)nmtf, gs = 0;
+    while (part > 0) {
+      const int target = rem / part;
+      int ge = gs - 1, acc = 0;
+      while (acc < target && ge < alpha - 1) acc += (int)S.freq[++ge];
+      if (ge > gs && part != ng && part != 1 && ((ng - part) % 2 == 1)) acc -= (int)S.freq[ge--];
+      for (int v = gs; v <= ge; v++) S.len[part - 1][v] = 0;
+      part--;
+      gs = ge + 1;
+      rem -= acc;
+    }
+  }
+  __syncthreads();
+  for (int it = 0; it < kIters; it++) {
+    for (int i = threadIdx.x; i < kNGroups * kMaxAlpha; i += kT) (&S.rfreq[0][0])[i] = 0;
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < nsel; g += kT) {
+      const uint32_t gs = g * kGroupSize, ge = min(gs + kGroupSize, nmtf);
+      uint32_t cost[kNGroups] = {0, 0, 0, 0, 0, 0};
+      for (uint32_t i = gs; i < ge; i++) {
+        const uint32_t v = mv[i];
+#pragma unroll
+        for (int t = 0; t < kNGroups; t++) cost[t] += S.len[t][v];
+      }
+      int bt = 0;
+      uint32_t bc = cost[0];
+      for (int t = 1; t < ng; t++)
+        if (cost[t] < bc) {
+          bc = cost[t];
+          bt = t;
+        }
+      S.sel[g] = (uint8_t)bt;
+      for (uint32_t i = gs; i < ge; i++) atomicAdd(&S.rfreq[bt][mv[i]], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)ng) {
+      const int t = threadIdx.x;
+      hb_code_lengths(S.len[t], S.rfreq[t], alpha, kMaxCodeLen, S.hheap[t], S.hweight[t], S.hparent[t]);
+    }
+    __syncthreads();
+  }
+  // selector table ids out
+  uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
+  for (uint32_t g = threadIdx.x; g < nsel; g += kT) selo[g] = S.sel[g];
+  // canonical codes (huffman.c:152-166)
+  if (threadIdx.x < (unsigned)ng) {
+    const int t = threadIdx.x;
+    int mn = 32, mx = 0;
+    for (int v = 0; v < alpha; v++) {
+      mn = min(mn, (int)S.len[t][v]);
+      mx = max(mx, (int)S.len[t][v]);
+    }
+    uint32_t c = 0;
+    for (int l = mn; l <= mx; l++) {
+      for (int v = 0; v < alpha; v++)
+        if (S.len[t][v] == l) S.code[t][v] = c++;
+      c <<= 1;
+    }
+  }
+  __syncthreads();
+  // payload bits per group
+  uint32_t mybits = 0;
+  uint16_t* gb = gbits_g + (size_t)b * kMaxSelectors;
+  for (uint32_t g = threadIdx.x; g < nsel; g += kT) {
+    const uint32_t gs = g * kGroupSize, ge = min(gs + kGroupSize, nmtf);
+    const int t = S.sel[g];
+    uint32_t bits = 0;
+    for (uint32_t i = gs; i < ge; i++) bits += S.len[t][mv[i]];
+    gb[g] = (uint16_t)bits;
+    mybits += bits;
+  }
+  uint32_t data_bits;
+  block_incl_sum(mybits, S.sh, &data_bits);
+  // selector MTF (compress.c:573-631): lane 0, sequential
+  uint8_t* smo = selmtf_g + (size_t)b * kMaxSelectors;
+  if (threadIdx.x == 0) {
+    uint8_t order[kNGroups] = {0, 1, 2, 3, 4, 5};
+    uint32_t sbits = 0;
+    for (uint32_t g = 0; g < nsel; g++) {
+      const uint8_t s = S.sel[g];
+      int j = 0;
+      while (order[j] != s) j++;
+      for (int k = j; k > 0; k--) order[k] = order[k - 1];
+      order[0] = s;
+      smo[g] = (uint8_t)j;
+      sbits += (uint32_t)j + 1;
+    }
+    S.misc[0] = sbits;
+  }
+  // code-length table bits (compress.c:694-706)
+  if (threadIdx.x < (unsigned)ng) {
+    const int t = threadIdx.x;
+    int cur = S.len[t][0];
+    uint32_t bits = 5;
+    for (int v = 0; v < alpha; v++) {
+      const int l = S.len[t][v];
+      bits += 1 + 2 * (uint32_t)(l > cur ? l - cur : cur - l);
+      cur = l;
+    }
+    S.misc[8 + t] = bits;
+  }
+  __syncthreads();
+  uint8_t* lo = lens_g + (size_t)b * kNGroups * kMaxAlpha;
+  uint32_t* co = codes_g + (size_t)b * kNGroups * kMaxAlpha;
+  for (int i = threadIdx.x; i < ng * kMaxAlpha; i += kT) {
+    const int t = i / kMaxAlpha, v = i % kMaxAlpha;
+    lo[i] = v < alpha ? S.len[t][v] : 0;
+    co[i] = v < alpha ? S.code[t][v] : 0;
+  }
+  if (threadIdx.x == 0) {
+    uint32_t used16 = 0;
+    for (int i = 0; i < 16; i++) {
+      const uint32_t w = inuse[b * 8 + (i >> 1)];
+      const uint32_t half = (i & 1) ? (w >> 16) : (w & 0xffffu);
+      if (half) used16++;
+    }
+    uint32_t tbits = 0;
+    for (int t = 0; t < ng; t++) tbits += S.misc[8 + t];
+    const uint32_t total = 48 + 32 + 1 + 24 + 16 + 16 * used16 + 3 + 15 + S.misc[0] + tbits + data_bits;
+    uint32_t* info = info_g + (size_t)b * 8;
+    info[0] = (uint32_t)ng;
+    info[1] = nsel;
+    info[2] = (uint32_t)alpha;
+    info[3] = total;
+    info[4] = S.misc[0];
+    info[5] = tbits;
+    info[6] = data_bits;
+  }
+}
+
+// Bit offsets of every block, the combined CRC, the trailer position.
+__global__ void k_offsets(const uint32_t* __restrict__ info, const uint32_t* __restrict__ bcrc, uint32_t nb,
+                          uint64_t start_bit, uint32_t comb_in, uint64_t* __restrict__ boffbits,
+                          uint64_t* __restrict__ out_total, uint32_t* __restrict__ comb_out) {
+  if (threadIdx.x != 0) return;
+  uint64_t pos = start_bit;
+  uint32_t comb = comb_in;
+  for (uint32_t b = 0; b < nb; b++) {
+    boffbits[b] = pos;
+    pos += info[(size_t)b * 8 + 3];
+    comb = ((comb << 1) | (comb >> 31)) ^ bcrc[b];
+  }
+  *out_total = pos;
+  *comb_out = comb;
+}
+
+// MSB-first bit writer ORing big-endian 32-bit words into a zeroed buffer.
+struct BitWriter {
+  uint32_t* out;
+  uint64_t word;   // index of the word the accumulator starts at
+  uint64_t acc;    // bits left-aligned: bit 63 = first bit of `word` (+ already flushed)
+  uint32_t nacc;   // valid bits in acc (including the leading alignment bits)
+  __device__ BitWriter(uint32_t* o, uint64_t bitpos) : out(o), word(bitpos >> 5), acc(0), nacc((uint32_t)(bitpos & 31)) {}
+  __device__ __forceinline__ void put(uint32_t nbits, uint32_t v) {
+    // nbits <= 32
+    if (nbits == 0) return;
+    acc |= ((uint64_t)v << (64 - nbits)) >> nacc;
+    nacc += nbits;
+    if (nacc >= 32) {
+      const uint32_t hi = (uint32_t)(acc >> 32);
+      if (hi) atomicOr(&out[word], bswap32(hi));
+      ++word;
+      acc <<= 32;
+      nacc -= 32;
+    }
+  }
+  __device__ __forceinline__ void flush() {
+    if (nacc > 0) {
+      const uint32_t hi = (uint32_t)(acc >> 32);
+      if (hi) atomicOr(&out[word], bswap32(hi));
+    }
+  }
+};
+// nbits up to 32 may overflow the accumulator when nacc > 32 after a put; put() keeps
+// nacc < 32 on exit, so a put of <= 32 bits never loses bits.
+
+__global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, const uint32_t* __restrict__ mtf_off,
+                                             const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ inuse,
+                                             const uint32_t* __restrict__ bcrc, const uint32_t* __restrict__ origptr,
+                                             const uint8_t* __restrict__ lens_g, const uint32_t* __restrict__ codes_g,
+                                             const uint8_t* __restrict__ sel_g, const uint8_t* __restrict__ selmtf_g,
+                                             const uint16_t* __restrict__ gbits_g, const uint32_t* __restrict__ info_g,
+                                             const uint64_t* __restrict__ boffbits, uint32_t* __restrict__ out) {
+  __shared__ uint8_t len[kNGroups][kMaxAlpha + 2];
+  __shared__ uint32_t code[kNGroups][kMaxAlpha];
+  __shared__ uint32_t sh[8];
+  const uint32_t b = blockIdx.x;
+  const uint32_t* info = info_g + (size_t)b * 8;
+  const int ng = (int)info[0];
+  const uint32_t nsel = info[1];
+  const int alpha = (int)info[2];
+  const uint32_t nmtf = nmtf_g[b];
+  const uint16_t* mv = mtfv + mtf_off[b];
+  for (int i = threadIdx.x; i < ng * kMaxAlpha; i += kT) {
+    len[i / kMaxAlpha][i % kMaxAlpha] = lens_g[(size_t)b * kNGroups * kMaxAlpha + i];
+    code[i / kMaxAlpha][i % kMaxAlpha] = codes_g[(size_t)b * kNGroups * kMaxAlpha + i];
+  }
+  __syncthreads();
+  const uint64_t p0 = boffbits[b];
+  uint32_t used16 = 0;
+  for (int i = 0; i < 16; i++) {
+    const uint32_t w = inuse[b * 8 + (i >> 1)];
+    if ((i & 1) ? (w >> 16) : (w & 0xffffu)) used16++;
+  }
+  const uint64_t p_sel = p0 + 48 + 32 + 1 + 24 + 16 + 16 * used16 + 3 + 15;
+  const uint64_t p_tab = p_sel + info[4];
+  const uint64_t p_dat = p_tab + info[5];
+  // header, symbol map, nGroups, nSelectors: lane 0
+  if (threadIdx.x == 0) {
+    BitWriter w(out, p0);
+    w.put(24, 0x314159);
+    w.put(24, 0x265359);
+    w.put(32, bcrc[b]);
+    w.put(1, 0);
+    w.put(24, origptr[b]);
+    uint32_t top = 0;
+    for (int i = 0; i < 16; i++) {
+      const uint32_t wd = inuse[b * 8 + (i >> 1)];
+      const uint32_t half = (i & 1) ? (wd >> 16) : (wd & 0xffffu);
+      top = (top << 1) | (half ? 1u : 0u);
+    }
+    w.put(16, top);
+    for (int i = 0; i < 16; i++) {
+      const uint32_t wd = inuse[b * 8 + (i >> 1)];
+      const uint32_t half = (i & 1) ? (wd >> 16) : (wd & 0xffffu);
+      if (!half) continue;
+      uint32_t row = 0;
+      for (int j = 0; j < 16; j++) row = (row << 1) | ((half >> j) & 1u);
+      w.put(16, row);
+    }
+    w.put(3, (uint32_t)ng);
+    w.put(15, nsel);
+    w.flush();
+  }
+  // code-length tables: lane t writes table t
+  if (threadIdx.x < (unsigned)ng) {
+    const int t = threadIdx.x;
+    uint64_t pos = p_tab;
+    for (int u = 0; u < t; u++) {
+      int cur = len[u][0];
+      uint32_t bits = 5;
+      for (int v = 0; v < alpha; v++) {
+        const int l = len[u][v];
+        bits += 1 + 2 * (uint32_t)(l > cur ? l - cur : cur - l);
+        cur = l;
+      }
+      pos += bits;
+    }
+    BitWriter w(out, pos);
+    int cur = len[t][0];
+    w.put(5, (uint32_t)cur);
+    for (int v = 0; v < alpha; v++) {
+      const int l = len[t][v];
+      while (cur < l) {
+        w.put(2, 2);
+        cur++;
+      }
+      while (cur > l) {
+        w.put(2, 3);
+        cur--;
+      }
+      w.put(1, 0);
+    }
+    w.flush();
+  }
+  // selectors (unary MTF codes): thread-blocked ranges
+  const uint8_t* smo = selmtf_g + (size_t)b * kMaxSelectors;
+  {
+    const uint32_t per = ceil_div(nsel, kT);
+    const uint32_t lo = min(nsel, threadIdx.x * per), hi = min(nsel, lo + per);
+    uint32_t bits = 0;
+    for (uint32_t g = lo; g < hi; g++) bits += smo[g] + 1u;
+    const uint32_t incl = block_incl_sum(bits, sh, (uint32_t*)nullptr);
+    BitWriter w(out, p_sel + incl - bits);
+    for (uint32_t g = lo; g < hi; g++) {
+      const uint32_t j = smo[g];
+      w.put(j + 1, (1u << (j + 1)) - 2u);
+    }
+    w.flush();
+  }
+  // payload
+  {
+    const uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
+    const uint16_t* gb = gbits_g + (size_t)b * kMaxSelectors;
+    const uint32_t per = ceil_div(nsel, kT);
+    const uint32_t lo = min(nsel, threadIdx.x * per), hi = min(nsel, lo + per);
+    uint32_t bits = 0;
+    for (uint32_t g = lo; g < hi; g++) bits += gb[g];
+    const uint32_t incl = block_incl_sum(bits, sh, (uint32_t*)nullptr);
+    BitWriter w(out, p_dat + incl - bits);
+    for (uint32_t g = lo; g < hi; g++) {
+      const int t = selo[g];
+      const uint32_t gs = g * kGroupSize, ge = min(gs + kGroupSize, nmtf);
+      for (uint32_t i = gs; i < ge; i++) {
+        const uint32_t v = mv[i];
+        w.put(len[t][v], code[t][v]);
+      }
+    }
+    w.flush();
+  }
+}
+
+// Stream header ("BZh" + level) and/or trailer (0x177245385090 + combined CRC).
+__global__ void k_frame(uint32_t* __restrict__ out, int header, uint64_t hdr_bit, int level, int trailer,
+                        const uint64_t* __restrict__ tpos, const uint32_t* __restrict__ comb) {
+  if (threadIdx.x != 0) return;
+  if (header) {
+    BitWriter w(out, hdr_bit);
+    w.put(8, 'B');
+    w.put(8, 'Z');
+    w.put(8, 'h');
+    w.put(8, (uint32_t)('0' + level));
+    w.flush();
+  }
+  if (trailer) {
+    BitWriter w(out, *tpos);
+    w.put(24, 0x177245);
+    w.put(24, 0x385090);
+    w.put(32, *comb);
+    w.flush();
+  }
+}
+
+}  // namespace
+
+uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, const uint32_t* origptr, uint32_t nb,
+                    int level, bool final_batch, StreamCarry& carry, uint8_t* out, uint64_t out_cap, hipStream_t st) {
+  const size_t nbx = std::max<uint32_t>(nb, 1);
+  uint8_t* lens = ws.u8("code_lens", nbx * kNGroups * kMaxAlpha);
+  uint32_t* codes = ws.u32("code_codes", nbx * kNGroups * kMaxAlpha);
+  uint8_t* sel = ws.u8("code_sel", nbx * kMaxSelectors);
+  uint8_t* selmtf = ws.u8("code_selmtf", nbx * kMaxSelectors);
+  uint16_t* gbits = ws.u16("code_gbits", nbx * kMaxSelectors);
+  uint32_t* info = ws.u32("code_info", nbx * 8);
+  uint64_t* bbits = ws.typed<uint64_t>("code_bbits", nbx + 2);
+  uint32_t* comb = ws.u32("code_comb", 4);
+  static bool attr = false;
+  if (!attr) {
+    HIP_OK(hipFuncSetAttribute((const void*)k_tables, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(CodeLds)));
+    attr = true;
+  }
+  if (nb > 0) {
+    k_tables<<<nb, kT, sizeof(CodeLds), st>>>(m.mtfv, m.mtf_off, m.nmtf, m.freq, r.ninuse, r.inuse, lens, codes, sel,
+                                               selmtf, gbits, info);
+    HIP_OK(hipGetLastError());
+  }
+  const bool header = !carry.header_done;
+  const uint64_t start_bit = carry.carry_bits + (header ? 32 : 0);
+  k_offsets<<<1, 64, 0, st>>>(info, r.bcrc, nb, start_bit, carry.combined_crc, bbits, bbits + nbx, comb);
+  HIP_OK(hipGetLastError());
+  uint64_t total_bits;
+  uint32_t comb_h;
+  HIP_OK(hipMemcpyAsync(&total_bits, bbits + nbx, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(&comb_h, comb, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  const uint64_t end_bits = total_bits + (final_batch ? 80 : 0);
+  const uint64_t need = ceil_div64(end_bits, 32) * 4 + 8;
+  if (need > out_cap) throw HipFailure(hipErrorOutOfMemory);
+  HIP_OK(hipMemsetAsync(out, 0, need, st));
+  if (carry.carry_bits) HIP_OK(hipMemcpyAsync(out, &carry.carry_byte, 1, hipMemcpyHostToDevice, st));
+  if (nb > 0) {
+    k_pack<<<nb, kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, r.inuse, r.bcrc, origptr, lens, codes, sel, selmtf, gbits, info,
+                              bbits, (uint32_t*)out);
+    HIP_OK(hipGetLastError());
+  }
+  if (header || final_batch) {
+    k_frame<<<1, 64, 0, st>>>((uint32_t*)out, header ? 1 : 0, carry.carry_bits, level, final_batch ? 1 : 0,
+                              bbits + nbx, comb);
+    HIP_OK(hipGetLastError());
+  }
+  carry.header_done = true;
+  carry.combined_crc = comb_h;
+  if (final_batch) {
+    carry.carry_bits = 0;
+    carry.carry_byte = 0;
+    return ceil_div64(end_bits, 8);
+  }
+  const uint64_t full = end_bits >> 3;
+  carry.carry_bits = (uint8_t)(end_bits & 7);
+  if (carry.carry_bits) {
+    HIP_OK(hipMemcpyAsync(&carry.carry_byte, out + full, 1, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  } else {
+    carry.carry_byte = 0;
+  }
+  return full;
+}
+
+}  // namespace bzg

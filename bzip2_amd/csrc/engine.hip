@@ -1,0 +1,401 @@
+// engine.hip -- orchestration of the device pipeline and the bzg_* C ABI (include/bzg.h).
+//
+// One engine per process (device 0 of the process's visible devices; one process per GPU),
+// guarded by a mutex: bzlib streams from several host threads are serialised on it.
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+#include "../../include/bzg.h"
+#include "resolver.h"
+#include "stages.h"
+
+#define BZ_OK 0
+#define BZ_PARAM_ERROR (-2)
+#define BZ_MEM_ERROR (-3)
+#define BZ_OUTBUFF_FULL (-8)
+#define BZ_CONFIG_ERROR (-9)
+
+namespace bzg {
+
+// ---------------------------------------------------------------- workspace
+Workspace::~Workspace() { release_all(); }
+
+void Workspace::release_all() {
+  for (auto& kv : bufs_)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  bufs_.clear();
+  total_ = 0;
+  if (crc_) (void)hipFree(crc_);
+  if (xp2_) (void)hipFree(xp2_);
+  crc_ = xp2_ = nullptr;
+}
+
+void* Workspace::get(const std::string& name, size_t bytes) {
+  bytes = std::max<size_t>(bytes, 64);
+  Buf& b = bufs_[name];
+  if (b.bytes >= bytes) return b.p;
+  if (b.p) {
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipFree(b.p));
+    total_ -= b.bytes;
+  }
+  const size_t grow = bytes + bytes / 8;  // headroom so small growth does not realloc
+  HIP_OK(hipMalloc(&b.p, grow));
+  b.bytes = grow;
+  total_ += grow;
+  return b.p;
+}
+
+static uint32_t host_gf_mul(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+  for (int i = 31; i >= 0; i--) {
+    r = (r & 0x80000000u) ? (r << 1) ^ 0x04C11DB7u : (r << 1);
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
+}
+
+const uint32_t* Workspace::crc_table() {
+  if (!crc_) {
+    uint32_t t[256];
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t r = i << 24;
+      for (int k = 0; k < 8; k++) r = (r & 0x80000000u) ? (r << 1) ^ 0x04C11DB7u : (r << 1);
+      t[i] = r;
+    }
+    HIP_OK(hipMalloc(&crc_, sizeof(t)));
+    HIP_OK(hipMemcpy(crc_, t, sizeof(t), hipMemcpyHostToDevice));
+  }
+  return crc_;
+}
+
+const uint32_t* Workspace::xpow2_table() {
+  if (!xp2_) {
+    uint32_t t[48];
+    t[0] = 0x100u;  // x^8
+    for (int k = 1; k < 48; k++) t[k] = host_gf_mul(t[k - 1], t[k - 1]);
+    HIP_OK(hipMalloc(&xp2_, sizeof(t)));
+    HIP_OK(hipMemcpy(xp2_, t, sizeof(t), hipMemcpyHostToDevice));
+  }
+  return xp2_;
+}
+
+// ---------------------------------------------------------------- engine
+struct Engine {
+  std::mutex mu;
+  bool init = false;
+  bool ok = false;
+  hipStream_t stream = nullptr;
+  Workspace ws;
+  hipEvent_t ev[6];
+  bzg_stats last{};
+
+  bool ensure() {
+    if (init) return ok;
+    init = true;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ok = false;
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return ok = false;
+    for (auto& e : ev)
+      if (hipEventCreate(&e) != hipSuccess) return ok = false;
+    return ok = true;
+  }
+
+  // Compress one batch.  Throws HipFailure on device errors.
+  void batch(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
+             uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s) {
+    const int level = st->level;
+    const bool end_seg = flags & BZG_FLAG_END_SEGMENT;
+    const bool tail_merge = (flags & BZG_FLAG_TAIL_MERGE) && end_seg;
+    const bool trailer = (flags & BZG_FLAG_TRAILER) && end_seg;
+    HIP_OK(hipEventRecord(ev[0], s));
+    Rle1Result r;
+    rle1_stage(ws, d_in, n, level, end_seg, tail_merge, r, s);
+    HIP_OK(hipEventRecord(ev[1], s));
+    const uint32_t nb = r.nblocks;
+    MtfResult m;
+    uint32_t* origptr = ws.u32("origptr", nb + 2);
+    SortStats ss;
+    std::vector<uint32_t> hboff(nb + 1), hper(nb);
+    if (nb > 0) {
+      HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, s));
+      HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
+      uint8_t* bwt = ws.u8("bwt", hboff[nb] + 16);
+      uint32_t* rank0 = ws.u32("rank0", nb + 2);
+      bwt_stage(ws, r, hboff, hper, bwt, rank0, &ss, s);
+      std::vector<uint32_t> hr(nb);
+      HIP_OK(hipMemcpyAsync(hr.data(), rank0, 4 * nb, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
+      resolve_origptrs(r.blk, hboff, hper, hr);  // periodic roots: reference tie rank (A5)
+      HIP_OK(hipMemcpyAsync(origptr, hr.data(), 4 * nb, hipMemcpyHostToDevice, s));
+      HIP_OK(hipEventRecord(ev[2], s));
+      mtf_stage(ws, r, bwt, nb, hboff[nb], m, s);
+      HIP_OK(hipEventRecord(ev[3], s));
+    } else {
+      HIP_OK(hipEventRecord(ev[2], s));
+      HIP_OK(hipEventRecord(ev[3], s));
+    }
+    StreamCarry c;
+    c.combined_crc = st->combined_crc;
+    c.carry_bits = st->carry_bits;
+    c.carry_byte = st->carry_byte;
+    c.header_done = st->header_done;
+    *out_bytes = code_stage(ws, r, m, origptr, nb, level, trailer, c, d_out, out_cap, s);
+    HIP_OK(hipEventRecord(ev[4], s));
+    HIP_OK(hipEventSynchronize(ev[4]));
+    st->combined_crc = c.combined_crc;
+    st->carry_bits = c.carry_bits;
+    st->carry_byte = c.carry_byte;
+    st->header_done = c.header_done ? 1 : 0;
+    st->blocks_done += nb;
+    *consumed = end_seg ? n : r.consumed;
+    last = bzg_stats{};
+    (void)hipEventElapsedTime(&last.rle1_ms, ev[0], ev[1]);
+    (void)hipEventElapsedTime(&last.bwt_ms, ev[1], ev[2]);
+    (void)hipEventElapsedTime(&last.mtf_ms, ev[2], ev[3]);
+    (void)hipEventElapsedTime(&last.code_ms, ev[3], ev[4]);
+    (void)hipEventElapsedTime(&last.total_ms, ev[0], ev[4]);
+    last.nblocks = nb;
+    last.sort_iterations = (uint32_t)ss.iterations;
+    last.rle_bytes = nb ? hboff[nb] : 0;
+    last.sort_unsorted = ss.unsorted_elems;
+  }
+};
+
+static Engine& engine() {
+  static Engine* e = new Engine();  // never destroyed: device teardown order at exit is unsafe
+  return *e;
+}
+
+// Largest batch handled in one pass: keeps every block/slot offset in 32 bits.
+static constexpr uint64_t kMaxBatch = 1500ull * 1000 * 1000;
+
+}  // namespace bzg
+
+using namespace bzg;
+
+extern "C" {
+
+void bzg_stream_init(bzg_stream_state* st, int level) {
+  std::memset(st, 0, sizeof(*st));
+  st->level = (uint8_t)level;
+}
+
+uint64_t bzg_bound(uint64_t n) { return n + n / 50 + (n / 100000 + 2) * 64 + 4096; }
+
+int bzg_device_ok(void) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  return e.ensure() ? 1 : 0;
+}
+
+int bzg_compress_device(const void* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, void* d_out,
+                        uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, void* stream) {
+  if (!st || !out_bytes || !consumed || st->level < 1 || st->level > 9 || (n && !d_in) || !d_out)
+    return BZ_PARAM_ERROR;
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
+  try {
+    // Split oversized inputs: non-final passes emit complete blocks, the rest is resubmitted.
+    uint64_t done_in = 0, done_out = 0;
+    uint8_t* out = (uint8_t*)d_out;
+    for (;;) {
+      const uint64_t left = n - done_in;
+      const bool last_piece = left <= kMaxBatch;
+      const uint64_t take = last_piece ? left : kMaxBatch;
+      const unsigned f = last_piece ? flags : 0u;
+      uint64_t ob = 0, cons = 0;
+      e.batch((const uint8_t*)d_in + done_in, take, f, st, out + done_out, out_cap - done_out, &ob, &cons, s);
+      done_in += cons;
+      done_out += ob;
+      if (last_piece) break;
+      if (cons == 0) return BZ_MEM_ERROR;  // cannot happen: kMaxBatch holds many blocks
+    }
+    *out_bytes = done_out;
+    *consumed = done_in;
+    return BZ_OK;
+  } catch (const HipFailure& f) {
+    return f.err == hipErrorOutOfMemory ? BZ_OUTBUFF_FULL : BZ_CONFIG_ERROR;
+  } catch (const ResolverFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+}
+
+int bzg_compress_host(const void* src, uint64_t n, int level, void* dst, uint64_t dst_cap, uint64_t* dst_len) {
+  if (level < 1 || level > 9 || (n && !src) || !dst || !dst_len) return BZ_PARAM_ERROR;
+  Engine& e = engine();
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!e.ensure()) return BZ_CONFIG_ERROR;
+  }
+  const uint64_t cap = bzg_bound(n);
+  uint8_t *din = nullptr, *dout = nullptr;
+  int rc = BZ_OK;
+  try {
+    std::lock_guard<std::mutex> g(e.mu);
+    din = e.ws.u8("host_in", n + 16);
+    dout = e.ws.u8("host_out", cap);
+    if (n) HIP_OK(hipMemcpyAsync(din, src, n, hipMemcpyHostToDevice, e.stream));
+  } catch (const HipFailure&) {
+    return BZ_MEM_ERROR;
+  }
+  bzg_stream_state st;
+  bzg_stream_init(&st, level);
+  uint64_t ob = 0, cons = 0;
+  const unsigned flags = BZG_FLAG_END_SEGMENT | BZG_FLAG_TRAILER | (n ? BZG_FLAG_TAIL_MERGE : 0u);
+  rc = bzg_compress_device(din, n, flags, &st, dout, cap, &ob, &cons, nullptr);
+  if (rc != BZ_OK) return rc;
+  if (ob > dst_cap) return BZ_OUTBUFF_FULL;
+  try {
+    std::lock_guard<std::mutex> g(e.mu);
+    HIP_OK(hipMemcpyAsync(dst, dout, ob, hipMemcpyDeviceToHost, e.stream));
+    HIP_OK(hipStreamSynchronize(e.stream));
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+  *dst_len = ob;
+  return BZ_OK;
+}
+
+int bzg_compress_host_stream(const void* src, uint64_t n, unsigned flags, bzg_stream_state* st, void* dst,
+                             uint64_t dst_cap, uint64_t* dst_len, uint64_t* consumed) {
+  if (!st || !dst || !dst_len || !consumed || (n && !src)) return BZ_PARAM_ERROR;
+  Engine& e = engine();
+  {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!e.ensure()) return BZ_CONFIG_ERROR;
+  }
+  const uint64_t cap = bzg_bound(n);
+  uint8_t *din = nullptr, *dout = nullptr;
+  try {
+    std::lock_guard<std::mutex> g(e.mu);
+    din = e.ws.u8("host_in", n + 16);
+    dout = e.ws.u8("host_out", cap);
+    if (n) HIP_OK(hipMemcpyAsync(din, src, n, hipMemcpyHostToDevice, e.stream));
+  } catch (const HipFailure&) {
+    return BZ_MEM_ERROR;
+  }
+  uint64_t ob = 0;
+  int rc = bzg_compress_device(din, n, flags, st, dout, cap, &ob, consumed, nullptr);
+  if (rc != BZ_OK) return rc;
+  if (ob > dst_cap) return BZ_OUTBUFF_FULL;
+  try {
+    std::lock_guard<std::mutex> g(e.mu);
+    if (ob) HIP_OK(hipMemcpyAsync(dst, dout, ob, hipMemcpyDeviceToHost, e.stream));
+    HIP_OK(hipStreamSynchronize(e.stream));
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+  *dst_len = ob;
+  return BZ_OK;
+}
+
+void bzg_last_stats(bzg_stats* out) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (out) *out = e.last;
+}
+
+void bzg_release(void) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (e.init && e.ok) {
+    (void)hipDeviceSynchronize();
+    e.ws.release_all();
+  }
+}
+
+// ---------------------------------------------------------------- per-stage entry points
+int bzg_stage_rle1(const void* src, uint64_t n, int level, int tail_merge, uint8_t* blocks, uint64_t blocks_cap,
+                   uint32_t* offsets, uint32_t* crcs, uint32_t* nblocks, uint32_t max_blocks) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  try {
+    uint8_t* din = e.ws.u8("stage_in", n + 16);
+    HIP_OK(hipMemcpy(din, src, n, hipMemcpyHostToDevice));
+    Rle1Result r;
+    rle1_stage(e.ws, din, n, level, true, tail_merge != 0, r, e.stream);
+    HIP_OK(hipStreamSynchronize(e.stream));
+    if (r.nblocks > max_blocks) return BZ_OUTBUFF_FULL;
+    *nblocks = r.nblocks;
+    if (r.nblocks == 0) {
+      offsets[0] = 0;
+      return BZ_OK;
+    }
+    HIP_OK(hipMemcpy(offsets, r.boff, 4 * (r.nblocks + 1), hipMemcpyDeviceToHost));
+    if (offsets[r.nblocks] > blocks_cap) return BZ_OUTBUFF_FULL;
+    HIP_OK(hipMemcpy(blocks, r.blk, offsets[r.nblocks], hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(crcs, r.bcrc, 4 * r.nblocks, hipMemcpyDeviceToHost));
+    return BZ_OK;
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+}
+
+int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, uint8_t* bwt_out, int32_t* origptr) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  try {
+    if (nb == 0) return BZ_OK;
+    const uint32_t total = offsets[nb];
+    Rle1Result r;
+    r.nblocks = nb;
+    r.blk = e.ws.u8("blk", total + 16);
+    r.boff = e.ws.u32("boff", nb + 2);
+    HIP_OK(hipMemcpy(r.blk, blocks, total, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice));
+    block_info_stage(e.ws, r, e.stream);
+    std::vector<uint32_t> hboff(offsets, offsets + nb + 1), hper(nb), hr(nb);
+    HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, e.stream));
+    HIP_OK(hipStreamSynchronize(e.stream));
+    uint8_t* bwt = e.ws.u8("bwt", total + 16);
+    uint32_t* rank0 = e.ws.u32("rank0", nb + 2);
+    bwt_stage(e.ws, r, hboff, hper, bwt, rank0, nullptr, e.stream);
+    HIP_OK(hipMemcpyAsync(hr.data(), rank0, 4 * nb, hipMemcpyDeviceToHost, e.stream));
+    HIP_OK(hipStreamSynchronize(e.stream));
+    resolve_origptrs(r.blk, hboff, hper, hr);
+    HIP_OK(hipMemcpy(bwt_out, bwt, total, hipMemcpyDeviceToHost));
+    for (uint32_t b = 0; b < nb; b++) origptr[b] = (int32_t)hr[b];
+    return BZ_OK;
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  } catch (const ResolverFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+}
+
+int bzg_stage_mtf(const uint8_t* bwt_in, const uint32_t* offsets, uint32_t nb, uint16_t* mtfv, uint32_t* mtf_offsets,
+                  uint32_t* nmtf, uint32_t* freq) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  try {
+    if (nb == 0) return BZ_OK;
+    const uint32_t total = offsets[nb];
+    Rle1Result r;
+    r.nblocks = nb;
+    r.blk = e.ws.u8("blk", total + 16);
+    r.boff = e.ws.u32("boff", nb + 2);
+    HIP_OK(hipMemcpy(r.blk, bwt_in, total, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice));
+    block_info_stage(e.ws, r, e.stream);
+    MtfResult m;
+    mtf_stage(e.ws, r, r.blk, nb, total, m, e.stream);
+    HIP_OK(hipStreamSynchronize(e.stream));
+    HIP_OK(hipMemcpy(mtf_offsets, m.mtf_off, 4 * (nb + 1), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(nmtf, m.nmtf, 4 * nb, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(freq, m.freq, 4 * (size_t)nb * kMaxAlpha, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(mtfv, m.mtfv, 2 * (size_t)mtf_offsets[nb], hipMemcpyDeviceToHost));
+    return BZ_OK;
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+}
+
+}  // extern "C"

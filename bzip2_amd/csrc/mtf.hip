@@ -1,0 +1,327 @@
+// mtf.hip -- stage A6: move-to-front + RUNA/RUNB coding (reference compress.c:93-229).
+//
+// The reference walks each block once, sequentially.  Here every block is cut into chunks of
+// kChunk symbols and the list state is composed between chunks:
+//   1. sig(c): the distinct symbols of chunk c in order of last occurrence, most recent first
+//      (the MTF list after chunk c is sig(c) followed by the untouched rest of the list);
+//   2. one wave per block chains list_{c+1} = sig(c) ++ (list_c minus sig(c)) from the
+//      initial list (the in-use bytes ascending, compress.c:124-140);
+//   3. every chunk re-runs MTF from its own initial list and writes ranks;
+//   4. zero runs (which may span chunks) are written as bijective base-2 RUNA/RUNB digits,
+//      least significant first (compress.c:154-168); rank j != 0 becomes j+1; EOB =
+//      nInUse+1 closes the block (compress.c:225-226).
+#include "stages.h"
+
+namespace bzg {
+
+namespace {
+constexpr int kT = 256;
+constexpr uint32_t kChunk = 1024;
+
+__device__ __forceinline__ uint32_t nsym(uint32_t z) { return z ? 31u - (uint32_t)__builtin_clz(z + 1) : 0u; }
+
+// chunk geometry: block b = blockIdx.y, chunk c = blockIdx.x*kT + threadIdx.x
+struct ChunkRef {
+  bool valid;
+  uint32_t b, c, lo, hi, gidx;  // gidx = global chunk id
+};
+__device__ __forceinline__ ChunkRef chunk_ref(const uint32_t* __restrict__ boff, const uint32_t* __restrict__ cbase) {
+  ChunkRef r;
+  r.b = blockIdx.y;
+  r.c = blockIdx.x * kT + threadIdx.x;
+  const uint32_t n = boff[r.b + 1] - boff[r.b];
+  r.valid = r.c * kChunk < n;
+  r.lo = boff[r.b] + r.c * kChunk;
+  r.hi = r.valid ? min(boff[r.b + 1], r.lo + kChunk) : r.lo;
+  r.gidx = cbase[r.b] + r.c;
+  return r;
+}
+
+// 1. signatures
+__global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
+                                            const uint32_t* __restrict__ cbase, uint8_t* __restrict__ sig,
+                                            uint32_t* __restrict__ siglen) {
+  __shared__ uint32_t seen[8][kT];
+  const ChunkRef r = chunk_ref(boff, cbase);
+#pragma unroll
+  for (int k = 0; k < 8; k++) seen[k][threadIdx.x] = 0;
+  if (!r.valid) return;
+  uint8_t* out = sig + (size_t)r.gidx * 256;
+  uint32_t cnt = 0;
+  for (uint32_t i = r.hi; i > r.lo; i--) {
+    const uint32_t c = L[i - 1];
+    const uint32_t bit = 1u << (c & 31);
+    uint32_t w = seen[c >> 5][threadIdx.x];
+    if (!(w & bit)) {
+      seen[c >> 5][threadIdx.x] = w | bit;
+      out[cnt++] = (uint8_t)c;
+    }
+  }
+  siglen[r.gidx] = cnt;
+}
+
+// 2. list chaining, one wave per block; lane l holds list positions 4l..4l+3
+__global__ void __launch_bounds__(64) k_compose(const uint32_t* __restrict__ boff, const uint32_t* __restrict__ cbase,
+                                                const uint32_t* __restrict__ inuse, const uint8_t* __restrict__ sig,
+                                                const uint32_t* __restrict__ siglen, uint32_t* __restrict__ init) {
+  __shared__ uint8_t list[256];
+  __shared__ uint8_t nlist[256];
+  __shared__ uint32_t mem[8];
+  const uint32_t b = blockIdx.x, lane = threadIdx.x;
+  const uint32_t n = boff[b + 1] - boff[b];
+  const uint32_t nch = ceil_div(n, kChunk);
+  // initial list: in-use bytes ascending
+  uint32_t nu = 0;
+  {
+    const uint32_t w = inuse[b * 8 + (lane >> 3)];  // lane covers bytes 4l..4l+3
+    uint32_t cnt = 0;
+    for (int k = 0; k < 4; k++) cnt += (w >> ((lane * 4 + k) & 31)) & 1u;
+    uint32_t incl = wave_incl_sum(cnt);
+    uint32_t p = incl - cnt;
+    for (int k = 0; k < 4; k++) {
+      const uint32_t byte = lane * 4 + k;
+      if ((w >> (byte & 31)) & 1u) list[p++] = (uint8_t)byte;
+    }
+    nu = __shfl(incl, 63, 64);
+  }
+  __syncthreads();
+  for (uint32_t c = 0; c < nch; c++) {
+    const uint32_t g = cbase[b] + c;
+    // publish the initial list of chunk c
+    reinterpret_cast<uint32_t*>(init + (size_t)g * 64)[lane] = reinterpret_cast<const uint32_t*>(list)[lane];
+    const uint32_t sl = siglen[g];
+    if (lane < 8) mem[lane] = 0;
+    __syncthreads();
+    const uint8_t* sg = sig + (size_t)g * 256;
+    for (uint32_t k = lane; k < sl; k += 64) {
+      const uint8_t s = sg[k];
+      atomicOr(&mem[s >> 5], 1u << (s & 31));
+      nlist[k] = s;
+    }
+    __syncthreads();
+    uint32_t keep = 0;
+    uint8_t e[4];
+    for (int k = 0; k < 4; k++) {
+      const uint32_t pos = lane * 4 + k;
+      e[k] = list[pos];
+      const bool valid = pos < nu && !((mem[e[k] >> 5] >> (e[k] & 31)) & 1u);
+      keep |= (valid ? 1u : 0u) << k;
+    }
+    const uint32_t kc = __builtin_popcount(keep);
+    uint32_t p = sl + wave_incl_sum(kc) - kc;
+    for (int k = 0; k < 4; k++)
+      if ((keep >> k) & 1u) nlist[p++] = e[k];
+    __syncthreads();
+    reinterpret_cast<uint32_t*>(list)[lane] = reinterpret_cast<const uint32_t*>(nlist)[lane];
+    __syncthreads();
+  }
+}
+
+// 3. per-chunk MTF from the chunk's initial list.  The thread's list lives in LDS as 64
+// words laid out [word][thread] so that lanes touching the same word index hit distinct
+// banks.  Byte k of word w is list position 4w+k.
+__global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
+                                                const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
+                                                uint8_t* __restrict__ ranks) {
+  __shared__ uint32_t lst[64][kT];
+  const ChunkRef r = chunk_ref(boff, cbase);
+  if (!r.valid) return;
+  const uint32_t t = threadIdx.x;
+  const uint32_t* src = init + (size_t)r.gidx * 64;
+  for (int w = 0; w < 64; w++) lst[w][t] = src[w];
+  for (uint32_t i = r.lo; i < r.hi; i++) {
+    const uint32_t c = L[i];
+    const uint32_t pat = c * 0x01010101u;
+    // find word and byte of c
+    uint32_t w = 0, x = 0;
+    for (; w < 64; w++) {  // every block byte is in the list; the bound only keeps a bad input finite
+      x = lst[w][t] ^ pat;
+      const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
+      if (z) {
+        x = z;
+        break;
+      }
+    }
+    if (w == 64) {
+      w = 63;
+      x = 0x80000000u;
+    }
+    const uint32_t k = (uint32_t)__builtin_ctz(x) >> 3;  // byte within word
+    const uint32_t pos = w * 4 + k;
+    ranks[i] = (uint8_t)pos;
+    if (pos == 0) continue;
+    // shift positions [0, pos) up by one and put c at 0
+    uint32_t carry = c;
+    for (uint32_t q = 0; q < w; q++) {
+      const uint32_t v = lst[q][t];
+      lst[q][t] = (v << 8) | carry;
+      carry = v >> 24;
+    }
+    const uint32_t v = lst[w][t];
+    const uint32_t lowmask = (k == 3) ? 0xffffffffu : ((1u << (8 * (k + 1))) - 1u);  // bytes 0..k
+    lst[w][t] = (v & ~lowmask) | (((v << 8) | carry) & lowmask);
+  }
+}
+
+// 4a. per-chunk zero-run summary
+__global__ void __launch_bounds__(kT) k_rle2_count(const uint8_t* __restrict__ ranks, const uint32_t* __restrict__ boff,
+                                                   const uint32_t* __restrict__ cbase, uint32_t* __restrict__ lead,
+                                                   uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
+  const ChunkRef r = chunk_ref(boff, cbase);
+  if (!r.valid) return;
+  uint32_t ld = 0, z = 0, cnt = 0;
+  bool seen = false;
+  for (uint32_t i = r.lo; i < r.hi; i++) {
+    const uint32_t v = ranks[i];
+    if (v == 0) {
+      z++;
+    } else {
+      if (!seen) {
+        ld = z;
+        seen = true;
+      } else {
+        cnt += nsym(z);
+      }
+      z = 0;
+      cnt++;
+    }
+  }
+  lead[r.gidx] = seen ? ld : 0xffffffffu;  // all-zero chunk marker
+  trail[r.gidx] = z;
+  inner[r.gidx] = cnt;
+}
+
+// 4b. per block: carried zero runs, chunk output offsets, nMTF
+__global__ void k_rle2_plan(const uint32_t* __restrict__ boff, const uint32_t* __restrict__ cbase, uint32_t nb,
+                            const uint32_t* __restrict__ ninuse, const uint32_t* __restrict__ lead,
+                            const uint32_t* __restrict__ trail, const uint32_t* __restrict__ inner,
+                            uint32_t* __restrict__ zin, uint32_t* __restrict__ coff, uint32_t* __restrict__ finalrun,
+                            uint32_t* __restrict__ nmtf) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint32_t n = boff[b + 1] - boff[b];
+  const uint32_t nch = ceil_div(n, kChunk);
+  uint32_t zp = 0, off = 0;
+  for (uint32_t c = 0; c < nch; c++) {
+    const uint32_t g = cbase[b] + c;
+    coff[g] = off;
+    const uint32_t ld = lead[g];
+    if (ld == 0xffffffffu) {
+      zp += (c + 1 < nch ? kChunk : n - c * kChunk);
+      zin[g] = 0;
+      continue;
+    }
+    const uint32_t z = zp + ld;
+    zin[g] = z;
+    off += nsym(z) + inner[g];
+    zp = trail[g];
+  }
+  finalrun[b] = zp;
+  off += nsym(zp) + 1;  // final run + EOB, emitted by the last chunk
+  nmtf[b] = off;
+  (void)ninuse;
+}
+
+// 4c. emission + symbol frequencies
+__global__ void __launch_bounds__(kT) k_rle2_emit(const uint8_t* __restrict__ ranks, const uint32_t* __restrict__ boff,
+                                                  const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ ninuse,
+                                                  const uint32_t* __restrict__ zin, const uint32_t* __restrict__ coff,
+                                                  const uint32_t* __restrict__ finalrun, const uint32_t* __restrict__ mtf_off,
+                                                  uint16_t* __restrict__ mtfv, uint32_t* __restrict__ freq) {
+  __shared__ uint32_t hist[kMaxAlpha];
+  for (int i = threadIdx.x; i < kMaxAlpha; i += kT) hist[i] = 0;
+  __syncthreads();
+  const ChunkRef r = chunk_ref(boff, cbase);
+  if (r.valid) {
+    uint16_t* out = mtfv + mtf_off[r.b] + coff[r.gidx];
+    uint32_t z = 0, o = 0;
+    bool seen = false;
+    auto put_run = [&](uint32_t zz) {
+      while (zz > 0) {
+        zz--;
+        const uint32_t d = zz & 1u;
+        out[o++] = (uint16_t)d;
+        atomicAdd(&hist[d], 1u);
+        zz >>= 1;
+      }
+    };
+    for (uint32_t i = r.lo; i < r.hi; i++) {
+      const uint32_t v = ranks[i];
+      if (v == 0) {
+        z++;
+        continue;
+      }
+      put_run(seen ? z : zin[r.gidx]);
+      seen = true;
+      z = 0;
+      out[o++] = (uint16_t)(v + 1);
+      atomicAdd(&hist[v + 1], 1u);
+    }
+    const uint32_t n = boff[r.b + 1] - boff[r.b];
+    if ((r.c + 1) * kChunk >= n) {  // last chunk: final run + EOB
+      put_run(finalrun[r.b]);
+      const uint32_t eob = ninuse[r.b] + 1;
+      out[o++] = (uint16_t)eob;
+      atomicAdd(&hist[eob], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kMaxAlpha; i += kT)
+    if (hist[i]) atomicAdd(&freq[(size_t)r.b * kMaxAlpha + i], hist[i]);
+}
+
+}  // namespace
+
+void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t nb, uint32_t total_bytes,
+               MtfResult& res, hipStream_t st) {
+  (void)total_bytes;
+  if (nb == 0) return;
+  std::vector<uint32_t> hboff(nb + 1);
+  HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  std::vector<uint32_t> hcb(nb + 1), hmo(nb + 1);
+  uint32_t maxch = 0;
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint32_t nch = ceil_div(hboff[b + 1] - hboff[b], kChunk);
+    hcb[b + 1] = hcb[b] + nch;
+    maxch = std::max(maxch, nch);
+    hmo[b] = hboff[b] + b;  // nMTF <= n + 1
+  }
+  hmo[nb] = hboff[nb] + nb;
+  const uint32_t nchunks = hcb[nb];
+  uint32_t* cbase = ws.u32("mtf_cbase", nb + 1);
+  uint32_t* moff = ws.u32("mtf_off", nb + 1);
+  HIP_OK(hipMemcpyAsync(cbase, hcb.data(), 4 * (nb + 1), hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(moff, hmo.data(), 4 * (nb + 1), hipMemcpyHostToDevice, st));
+  uint8_t* sig = ws.u8("mtf_sig", (size_t)nchunks * 256);
+  uint32_t* siglen = ws.u32("mtf_siglen", nchunks);
+  uint32_t* init = ws.u32("mtf_init", (size_t)nchunks * 64);
+  uint8_t* ranks = ws.u8("mtf_ranks", hboff[nb] + 16);
+  uint32_t* lead = ws.u32("mtf_lead", nchunks);
+  uint32_t* trail = ws.u32("mtf_trail", nchunks);
+  uint32_t* inner = ws.u32("mtf_inner", nchunks);
+  uint32_t* zin = ws.u32("mtf_zin", nchunks);
+  uint32_t* coff = ws.u32("mtf_coff", nchunks);
+  uint32_t* finalrun = ws.u32("mtf_final", nb);
+  res.nmtf = ws.u32("mtf_n", nb);
+  res.freq = ws.u32("mtf_freq", (size_t)nb * kMaxAlpha);
+  res.mtfv = ws.u16("mtf_v", hmo[nb] + 16);
+  res.mtf_off = moff;
+  HIP_OK(hipMemsetAsync(res.freq, 0, (size_t)nb * kMaxAlpha * 4, st));
+  const dim3 g2(ceil_div(maxch, kT), nb);
+  k_sig<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, sig, siglen);
+  HIP_OK(hipGetLastError());
+  k_compose<<<nb, 64, 0, st>>>(r.boff, cbase, r.inuse, sig, siglen, init);
+  HIP_OK(hipGetLastError());
+  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, init, ranks);
+  HIP_OK(hipGetLastError());
+  k_rle2_count<<<g2, kT, 0, st>>>(ranks, r.boff, cbase, lead, trail, inner);
+  HIP_OK(hipGetLastError());
+  k_rle2_plan<<<ceil_div(nb, 64), 64, 0, st>>>(r.boff, cbase, nb, r.ninuse, lead, trail, inner, zin, coff, finalrun,
+                                                res.nmtf);
+  HIP_OK(hipGetLastError());
+  k_rle2_emit<<<g2, kT, 0, st>>>(ranks, r.boff, cbase, r.ninuse, zin, coff, finalrun, moff, res.mtfv, res.freq);
+  HIP_OK(hipGetLastError());
+}
+
+}  // namespace bzg

@@ -1,0 +1,436 @@
+// rle1.hip -- stage A1/A2: RLE1, block segmentation, block CRC, in-use maps, period test.
+//
+// Reference behaviour restated (bzlib.c:211-315 copy_input_until_stop, 361-396
+// handle_compress): a run of L equal bytes is cut into chunks of 255 (the last chunk holds
+// the remainder); a chunk of 1..3 bytes is copied, a chunk of 4..255 becomes 4 copies plus
+// the byte (len-4).  A byte is only consumed while the block holds < nblockMAX bytes, so a
+// chunk belongs to the current block iff its first output byte lands before
+// blockStart + nblockMAX.  The data-parallel restatement used here:
+//   r(i)  = (i - runStart(i)) mod 255          position inside the chunk
+//   e(i)  = r<=2 ? 1 : r==3 ? 1+last(i) : last(i)   output bytes produced by input byte i
+//   last(i) = chunk ends at i (next byte differs, end of input, or r == 254)
+// The output offset of byte i is the exclusive prefix sum of e; a chunk starts at r == 0.
+#include "stages.h"
+#include "scan.h"
+
+namespace bzg {
+
+namespace {
+constexpr int kT = 256;      // threads
+constexpr int kPer = 16;     // bytes per thread
+constexpr int kTile = kT * kPer;
+
+__device__ __forceinline__ void load16(const uint8_t* __restrict__ x, uint64_t n, uint64_t base,
+                                       uint8_t (&v)[kPer]) {
+  if (base + kPer <= n && ((base & 15) == 0)) {
+    uint4 q = *reinterpret_cast<const uint4*>(x + base);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < kPer; k++) v[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  } else {
+#pragma unroll
+    for (int k = 0; k < kPer; k++) v[k] = (base + k < n) ? x[base + k] : 0;
+  }
+}
+
+// Pass 1: per tile, the largest run-start position in the tile (0 if none).
+__global__ void __launch_bounds__(kT) k_run_starts(const uint8_t* __restrict__ x, uint64_t n,
+                                                   uint32_t* __restrict__ tile_max) {
+  __shared__ uint32_t sh[kT / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
+  uint8_t v[kPer];
+  load16(x, n, base, v);
+  uint8_t prev = (base > 0 && base - 1 < n) ? x[base - 1] : 0;
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    uint64_t i = base + k;
+    if (i < n && (i == 0 || v[k] != prev)) m = (uint32_t)i;
+    prev = v[k];
+  }
+  m = block_incl_max(m, sh);
+  if (threadIdx.x == kT - 1) tile_max[blockIdx.x] = m;
+}
+
+struct ByteInfo {
+  uint8_t e;  // output bytes
+  uint8_t r;  // position inside chunk (0..254)
+  bool last;  // chunk ends here
+};
+
+// Recomputes per-byte info for this thread's 16 bytes given the tile's run-start carry.
+// `thr` needs kT words.
+__device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_t n, uint64_t base,
+                                          const uint8_t (&v)[kPer], uint32_t carry_start,
+                                          uint32_t* sh, uint32_t* thr, ByteInfo (&bi)[kPer]) {
+  uint8_t prev = (base > 0 && base - 1 < n) ? x[base - 1] : 0;
+  uint32_t m = 0;
+  uint32_t st[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    uint64_t i = base + k;
+    if (i < n && (i == 0 || v[k] != prev)) m = (uint32_t)i;
+    st[k] = m;
+    prev = v[k];
+  }
+  const uint32_t incl = block_incl_max(m, sh);
+  thr[threadIdx.x] = incl;
+  __syncthreads();
+  uint32_t before = carry_start;
+  if (threadIdx.x > 0) {
+    const uint32_t w = thr[threadIdx.x - 1];
+    before = before > w ? before : w;
+  }
+  __syncthreads();
+  const uint8_t next_after = (base + kPer < n) ? x[base + kPer] : 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    uint64_t i = base + k;
+    uint32_t rs = st[k] > before ? st[k] : before;
+    uint32_t r = (uint32_t)((i - rs) % 255u);
+    uint8_t nx = (k + 1 < kPer) ? v[k + 1] : next_after;
+    bool last = (i + 1 >= n) || (nx != v[k]) || (r == 254);
+    uint8_t e = r <= 2 ? 1 : (r == 3 ? (uint8_t)(1 + (last ? 1 : 0)) : (uint8_t)(last ? 1 : 0));
+    if (i >= n) e = 0;
+    bi[k] = ByteInfo{e, (uint8_t)r, last};
+  }
+}
+
+// Pass 2: per tile, total output bytes.
+__global__ void __launch_bounds__(kT) k_emit_count(const uint8_t* __restrict__ x, uint64_t n,
+                                                   const uint32_t* __restrict__ carry,
+                                                   uint32_t* __restrict__ tile_sum) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t thr[kT];
+  const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
+  uint8_t v[kPer];
+  load16(x, n, base, v);
+  ByteInfo bi[kPer];
+  byte_info(x, n, base, v, carry[blockIdx.x], sh, thr, bi);
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) s += bi[k].e;
+  uint32_t tot;
+  block_incl_sum(s, sh, &tot);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
+}
+
+// Pass 3: write block bytes, chunk-start bitmap and chunk-start -> input position map.
+__global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint64_t n,
+                                             const uint32_t* __restrict__ carry,
+                                             const uint32_t* __restrict__ out_base,
+                                             uint8_t* __restrict__ out, uint32_t* __restrict__ cbits,
+                                             uint32_t* __restrict__ cinpos, uint32_t* __restrict__ last_len1) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t thr[kT];
+  const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
+  uint8_t v[kPer];
+  load16(x, n, base, v);
+  ByteInfo bi[kPer];
+  byte_info(x, n, base, v, carry[blockIdx.x], sh, thr, bi);
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) s += bi[k].e;
+  uint32_t incl = block_incl_sum(s, sh, (uint32_t*)nullptr);
+  uint32_t pos = out_base[blockIdx.x] + incl - s;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t i = base + k;
+    if (i >= n) break;
+    const ByteInfo b = bi[k];
+    if (i + 1 == n) *last_len1 = (b.r == 0) ? 1u : 0u;
+    if (b.r == 0) {
+      atomicOr(&cbits[pos >> 5], 1u << (pos & 31));
+      cinpos[pos] = (uint32_t)i;
+    }
+    if (b.r <= 3) {
+      out[pos] = v[k];
+      if (b.r == 3 && b.last) out[pos + 1] = 0;
+    } else if (b.last) {
+      out[pos] = (uint8_t)(b.r - 3);
+    }
+    pos += b.e;
+  }
+}
+
+// Smallest chunk start >= t (t < m), or m if none.
+__device__ uint32_t next_chunk_start(const uint32_t* __restrict__ cbits, uint32_t t, uint32_t m) {
+  uint32_t w = t >> 5;
+  uint32_t bits = cbits[w] & (~0u << (t & 31));
+  const uint32_t wend = (m + 31) >> 5;
+  while (bits == 0) {
+    if (++w >= wend) return m;
+    bits = cbits[w];
+  }
+  uint32_t p = (w << 5) + (uint32_t)__builtin_ctz(bits);
+  return p < m ? p : m;
+}
+
+// Sequential block-cut chain (one thread).  See file header for the rule.
+__global__ void k_segment(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ cinpos,
+                          const uint32_t* __restrict__ m_ptr, uint64_t n, uint32_t nblock_max,
+                          int final_batch, int tail_merge, const uint32_t* __restrict__ last_len1_ptr,
+                          uint32_t* __restrict__ boff, uint32_t* __restrict__ binst,
+                          uint32_t* __restrict__ nblocks, uint32_t max_blocks) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t m = *m_ptr;
+  const uint32_t last_chunk_len1 = *last_len1_ptr;
+  uint32_t b = 0, s = 0;
+  if (m == 0) {
+    boff[0] = 0;
+    binst[0] = 0;
+    *nblocks = 0;
+    return;
+  }
+  // out position of the last chunk start (for the tail-merge rule)
+  uint32_t last_start = 0;
+  {
+    uint32_t w = (m - 1) >> 5;
+    for (;;) {
+      uint32_t bits = cbits[w] & (w == ((m - 1) >> 5) ? (0xffffffffu >> (31 - ((m - 1) & 31))) : ~0u);
+      if (bits) { last_start = (w << 5) + 31 - (uint32_t)__builtin_clz(bits); break; }
+      if (w == 0) break;
+      --w;
+    }
+  }
+  for (;;) {
+    boff[b] = s;
+    binst[b] = cinpos[s];
+    uint32_t t = s + nblock_max;
+    uint32_t p = (t < m) ? next_chunk_start(cbits, t, m) : m;
+    if (p < m && final_batch && tail_merge && p == last_start && last_chunk_len1) p = m;
+    if (p >= m) {
+      if (final_batch) {
+        boff[b + 1] = m;
+        binst[b + 1] = (uint32_t)n;
+        *nblocks = b + 1;
+      } else {
+        *nblocks = b;  // block b is incomplete; it restarts the next batch at binst[b]
+      }
+      return;
+    }
+    if (b + 1 >= max_blocks) {  // cannot happen with the host's sizing; keep the grid finite
+      *nblocks = 0xffffffffu;
+      return;
+    }
+    ++b;
+    s = p;
+  }
+}
+
+// CRC helpers: MSB-first polynomial 0x04C11DB7.
+__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {  // a*b mod P
+  uint32_t r = 0;
+  for (int i = 31; i >= 0; i--) {
+    r = (r & 0x80000000u) ? (r << 1) ^ 0x04C11DB7u : (r << 1);
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
+}
+// x^(8*len) mod P via the table of x^(2^k) mod P for k = 3 .. 3+40
+__device__ __forceinline__ uint32_t xpow8(const uint32_t* __restrict__ xp2, uint64_t len) {
+  uint32_t r = 1u;  // x^0 (bit k of a CRC register is the coefficient of x^k)
+  int k = 0;
+  while (len) {
+    if (len & 1) r = gf_mul(r, xp2[k]);
+    len >>= 1;
+    ++k;
+  }
+  return r;
+}
+
+// Block CRC over input [binst[b], binst[b+1]): each thread takes a contiguous slice, slices
+// are folded in order with multiplications by x^(8*len).
+__global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x, const uint32_t* __restrict__ binst,
+                                                  const uint32_t* __restrict__ crc_table_g,
+                                                  const uint32_t* __restrict__ xp2_g,
+                                                  uint32_t* __restrict__ bcrc) {
+  __shared__ uint32_t tab[256];
+  __shared__ uint32_t xp2[48];
+  __shared__ uint32_t part[kT];
+  __shared__ uint64_t plen[kT];
+  const int b = blockIdx.x;
+  tab[threadIdx.x] = crc_table_g[threadIdx.x];
+  if (threadIdx.x < 48) xp2[threadIdx.x] = xp2_g[threadIdx.x];
+  __syncthreads();
+  const uint64_t lo = binst[b], hi = binst[b + 1], len = hi - lo;
+  const uint64_t per = (len + kT - 1) / kT;
+  uint64_t s = lo + per * threadIdx.x, e = s + per;
+  if (s > hi) s = hi;
+  if (e > hi) e = hi;
+  uint32_t c = 0;
+  for (uint64_t i = s; i < e; i++) c = (c << 8) ^ tab[(c >> 24) ^ x[i]];
+  part[threadIdx.x] = c;
+  plen[threadIdx.x] = e - s;
+  __syncthreads();
+  // tree fold: combine(a, b) = a * x^(8 len_b) ^ b
+  for (int stride = 1; stride < kT; stride <<= 1) {
+    int i = threadIdx.x;
+    if ((i % (2 * stride)) == 0 && i + stride < kT) {
+      uint64_t lb = plen[i + stride];
+      uint32_t a = part[i];
+      part[i] = (lb ? gf_mul(a, xpow8(xp2, lb)) : a) ^ part[i + stride];
+      plen[i] += lb;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    uint32_t init = len ? gf_mul(0xffffffffu, xpow8(xp2, len)) : 0xffffffffu;
+    bcrc[b] = ~(init ^ part[0]);
+  }
+}
+
+// In-use bitmap (8 words) and nInUse per block; blocks are boff[b]..boff[b+1] of blk.
+__global__ void __launch_bounds__(kT) k_in_use(const uint8_t* __restrict__ blk, const uint32_t* __restrict__ boff,
+                                               uint32_t* __restrict__ inuse, uint32_t* __restrict__ ninuse) {
+  __shared__ uint32_t f[8];
+  const int b = blockIdx.x;
+  if (threadIdx.x < 8) f[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lo = boff[b], hi = boff[b + 1];
+  uint32_t local[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) {
+    uint8_t c = blk[i];
+    local[c >> 5] |= 1u << (c & 31);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if (local[k]) atomicOr(&f[k], local[k]);
+  __syncthreads();
+  if (threadIdx.x < 8) inuse[b * 8 + threadIdx.x] = f[threadIdx.x];
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int k = 0; k < 8; k++) c += __builtin_popcount(f[k]);
+    ninuse[b] = c;
+  }
+}
+
+// Primitive period of each block: smallest divisor p of n with blk[i] == blk[i+p] for
+// all i < n-p (then the block is w^(n/p)); p = n when aperiodic.
+__global__ void __launch_bounds__(kT) k_period(const uint8_t* __restrict__ blk, const uint32_t* __restrict__ boff,
+                                               uint32_t* __restrict__ period) {
+  __shared__ uint32_t divs[512];
+  __shared__ uint32_t ndiv;
+  __shared__ int bad;
+  const int b = blockIdx.x;
+  const uint32_t lo = boff[b], n = boff[b + 1] - lo;
+  if (threadIdx.x == 0) ndiv = 0;
+  __syncthreads();
+  for (uint32_t d = 1 + threadIdx.x; (uint64_t)d * d <= n; d += kT) {
+    if (n % d == 0) {
+      uint32_t k = atomicAdd(&ndiv, 1u);
+      if (k < 512) divs[k] = d;
+      if (d != n / d) {
+        k = atomicAdd(&ndiv, 1u);
+        if (k < 512) divs[k] = n / d;
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t nd = ndiv < 512 ? ndiv : 512;
+  // ascending order (simple rank sort, nd <= 512)
+  __shared__ uint32_t sorted[512];
+  for (uint32_t i = threadIdx.x; i < nd; i += kT) {
+    uint32_t v = divs[i], r = 0;
+    for (uint32_t j = 0; j < nd; j++) r += divs[j] < v;
+    sorted[r] = v;
+  }
+  __syncthreads();
+  uint32_t result = n;
+  for (uint32_t q = 0; q < nd; q++) {
+    const uint32_t p = sorted[q];
+    if (p >= n) break;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < n - p; i0 += kT * 16) {
+      for (uint32_t i = i0 + threadIdx.x; i < n - p && i < i0 + kT * 16; i += kT)
+        if (blk[lo + i] != blk[lo + i + p]) bad = 1;
+      __syncthreads();
+      if (bad) break;
+    }
+    __syncthreads();
+    if (!bad) { result = p; break; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) period[b] = result;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool final_batch,
+                bool tail_merge, Rle1Result& res, hipStream_t st) {
+  const uint32_t nblock_max = 100000u * (uint32_t)level - 19u;
+  res.nblocks = 0;
+  res.consumed = 0;
+  res.m = 0;
+  if (n == 0) return;
+  const uint64_t tiles = ceil_div64(n, kTile);
+  const uint64_t mcap = n + n / 4 + 64;
+  uint32_t* tmax = ws.u32("rle_tmax", tiles + 64);
+  uint32_t* tsum = ws.u32("rle_tsum", tiles + 64);
+  uint32_t* scratch = ws.u32("rle_scan", scan_scratch_words(tiles) + 64);
+  uint32_t* mtot = ws.u32("rle_m", 16);
+  uint8_t* blk = ws.u8("blk", mcap + 64);
+  uint32_t* cbits = ws.u32("rle_cbits", mcap / 32 + 64);
+  uint32_t* cinpos = ws.u32("rle_cinpos", mcap + 64);
+  const uint32_t max_blocks = (uint32_t)(mcap / nblock_max + 8);
+  uint32_t* boff = ws.u32("boff", max_blocks + 2);
+  uint32_t* binst = ws.u32("binst", max_blocks + 2);
+  uint32_t* nbl = mtot + 4;
+
+  k_run_starts<<<tiles, kT, 0, st>>>(d_in, n, tmax);
+  HIP_OK(hipGetLastError());
+  scan_u32(ScanOp::Max, true, tmax, tmax, tiles, nullptr, scratch, st);
+  k_emit_count<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum);
+  HIP_OK(hipGetLastError());
+  scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
+  HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
+  k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, blk, cbits, cinpos, mtot + 8);
+  HIP_OK(hipGetLastError());
+
+  k_segment<<<1, 64, 0, st>>>(cbits, cinpos, mtot, n, nblock_max, final_batch ? 1 : 0, tail_merge ? 1 : 0,
+                              mtot + 8, boff, binst, nbl, max_blocks);
+  HIP_OK(hipGetLastError());
+  uint32_t hv[2];
+  HIP_OK(hipMemcpyAsync(hv, mtot, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(hv + 1, nbl, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (hv[1] == 0xffffffffu) throw HipFailure(hipErrorUnknown);
+  res.m = hv[0];
+  res.nblocks = hv[1];
+  if (res.nblocks == 0) {  // non-final batch with no complete block: consume nothing
+    res.consumed = final_batch ? n : 0;
+    return;
+  }
+  // binst[nblocks] is n for a final batch, else the input start of the incomplete block
+  // that opens the next batch (a chunk start, so RLE1 restarts there with fresh state).
+  uint32_t tmp;
+  HIP_OK(hipMemcpyAsync(&tmp, binst + res.nblocks, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  res.consumed = final_batch ? n : tmp;
+
+  const int B = (int)res.nblocks;
+  uint32_t* bcrc = ws.u32("bcrc", max_blocks + 2);
+  k_block_crc<<<B, kT, 0, st>>>(d_in, binst, ws.crc_table(), ws.xpow2_table(), bcrc);
+  HIP_OK(hipGetLastError());
+  res.bcrc = bcrc;
+  res.blk = blk;
+  res.boff = boff;
+  res.binst = binst;
+  block_info_stage(ws, res, st);
+}
+
+void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st) {
+  const uint32_t B = res.nblocks;
+  if (B == 0) return;
+  res.inuse = ws.u32("inuse", (size_t)(B + 2) * 8);
+  res.ninuse = ws.u32("ninuse", B + 2);
+  res.period = ws.u32("period", B + 2);
+  k_in_use<<<B, kT, 0, st>>>(res.blk, res.boff, res.inuse, res.ninuse);
+  HIP_OK(hipGetLastError());
+  k_period<<<B, kT, 0, st>>>(res.blk, res.boff, res.period);
+  HIP_OK(hipGetLastError());
+}
+
+}  // namespace bzg

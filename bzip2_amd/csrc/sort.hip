@@ -1,0 +1,623 @@
+// sort.hip -- stage A4: batched cyclic suffix sorting (BWT) for all blocks of a batch.
+//
+// Replaces the reference's divsufsort (blocksort.c:1503-1545).  For an aperiodic block all
+// rotations are distinct, so any correct sort yields the reference's last column and
+// origPtr (parity fact 3).  Periodic blocks (w^k) are reduced to their
+// primitive root w here; the tie rank among the k identical copies of rotation 0 is resolved
+// on the host (resolver.cpp, A5).
+//
+// Algorithm: prefix doubling (Manber-Myers / Larsson-Sadakane) over the rotations of every
+// unit at once, with a segmented sort specialised by group size:
+//   * every slot s of unit u holds SA[s] (a rotation start) and ISA[sbase_u + i] holds the
+//     slot of the first member of i's group ("rank"), a refinement consistent with the true
+//     order of rotations at depth >= h;
+//   * iteration h: for every member of an unsorted group, key = rank(i + h) (h = 0: the first
+//     four bytes); groups larger than kSmall are split by global MSD counting passes on key
+//     digits; groups/buckets of <= kSmall elements are packed into LDS tiles and finished by
+//     an in-LDS stable LSD radix sort on (item, key);
+//   * new groups of size >= 2 form the next iteration's list; h doubles.
+// All keys of an iteration are gathered before any rank is rewritten.
+#include <algorithm>
+
+#include "scan.h"
+#include "stages.h"
+
+namespace bzg {
+
+namespace {
+
+constexpr int kT = 256;
+constexpr uint32_t kSmall = 2048;   // max group size sorted in LDS
+constexpr uint32_t kWin = 2048;     // nominal tile window (tile <= kWin + kSmall - 1 elements)
+constexpr uint32_t kTileCap = 4096;
+constexpr uint32_t kDTile = 4096;   // elements per tile of a digit pass
+
+struct Unit {
+  uint32_t sbase, len, toff, pad;
+};
+struct Grp {
+  uint32_t start, size, unit, flags;  // flags bit0: data lives in the alt (sa2/key2) buffers
+};
+
+struct SortBufs {
+  uint32_t *sa, *isa, *key, *sa2, *key2;
+  const uint8_t* text;
+  const Unit* units;
+};
+
+// ---------------------------------------------------------------------------------
+// Binary search: largest g with P[g] <= x (P is an exclusive prefix, P[0] = 0).
+__device__ __forceinline__ uint32_t upper_idx(const uint32_t* __restrict__ P, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;  // answer in [lo, hi)
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (P[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void k_units_to_groups(const Unit* __restrict__ units, uint32_t nu, Grp* __restrict__ L,
+                                  uint32_t* __restrict__ sizes) {
+  uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nu) return;
+  L[u] = Grp{units[u].sbase, units[u].len, u, 0};
+  sizes[u] = units[u].len;
+}
+
+__global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ sizes) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) sizes[g] = L[g].size;
+}
+
+__global__ void k_group_tiles(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ cnt) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) cnt[g] = ceil_div(L[g].size, kDTile);
+}
+
+// SA[s] = s - sbase for every slot (identity order before sorting).
+__global__ void k_init_sa(const Grp* __restrict__ L, const uint32_t* __restrict__ P, uint32_t nL,
+                          uint32_t total, uint32_t* __restrict__ sa) {
+  uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= total) return;
+  uint32_t g = upper_idx(P, nL, x);
+  Grp G = L[g];
+  uint32_t off = x - P[g];
+  sa[G.start + off] = off;
+}
+
+// key[s] for every member of every group in L.
+__global__ void __launch_bounds__(kT) k_gather(const Grp* __restrict__ L, const uint32_t* __restrict__ P,
+                                               uint32_t nL, uint32_t total, uint32_t h, SortBufs B) {
+  uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= total) return;
+  uint32_t g = upper_idx(P, nL, x);
+  const Grp G = L[g];
+  const uint32_t s = G.start + (x - P[g]);
+  const Unit U = B.units[G.unit];
+  const uint32_t i = B.sa[s];
+  uint32_t k;
+  if (h == 0) {
+    const uint8_t* t = B.text + U.toff;
+    uint32_t i1 = i + 1 >= U.len ? i + 1 - U.len : i + 1;
+    uint32_t i2 = i1 + 1 >= U.len ? i1 + 1 - U.len : i1 + 1;
+    uint32_t i3 = i2 + 1 >= U.len ? i2 + 1 - U.len : i2 + 1;
+    k = ((uint32_t)t[i] << 24) | ((uint32_t)t[i1] << 16) | ((uint32_t)t[i2] << 8) | (uint32_t)t[i3];
+  } else {
+    uint32_t hh = h % U.len;
+    uint32_t j = i + hh;
+    if (j >= U.len) j -= U.len;
+    k = B.isa[U.sbase + j] - U.sbase;
+  }
+  B.key[s] = k;
+}
+
+// Split L into the large list (digit passes) and the small list (LDS tiles).
+__global__ void k_partition(const Grp* __restrict__ L, uint32_t nL, int force_large, Grp* __restrict__ large,
+                            uint32_t* __restrict__ n_large, Grp* __restrict__ small, uint32_t* __restrict__ n_small) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nL) return;
+  Grp G = L[g];
+  if (force_large || G.size > kSmall) large[atomicAdd(n_large, 1u)] = G;
+  else small[atomicAdd(n_small, 1u)] = G;
+}
+
+// ---------------------------------------------------------------- digit passes (large)
+__global__ void __launch_bounds__(kT) k_dhist(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+                                              uint32_t shift, SortBufs B, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  const uint32_t t = blockIdx.x;
+  const uint32_t g = upper_idx(TP, nG, t);
+  const Grp gr = G[g];
+  const uint32_t c = t - TP[g];
+  const uint32_t lo = c * kDTile, hi = min(gr.size, lo + kDTile);
+  const uint32_t* kk = (gr.flags & 1) ? B.key2 : B.key;
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t e = lo + threadIdx.x; e < hi; e += kT) atomicAdd(&h[(kk[gr.start + e] >> shift) & 255u], 1u);
+  __syncthreads();
+  hist[(size_t)t * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+// One workgroup per large group: bucket bases, per-tile offsets, bucket emission.
+// mode 0: emit small buckets to `small`, large to `next`;  mode 1 (forced): all to `next`;
+// mode 2 (last digit): small to `small`, large to `equal`.
+__global__ void __launch_bounds__(kT) k_doff(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+                                             uint32_t* __restrict__ hist, uint32_t* __restrict__ tot, int mode,
+                                             Grp* __restrict__ small, uint32_t* __restrict__ n_small,
+                                             Grp* __restrict__ next, uint32_t* __restrict__ n_next,
+                                             Grp* __restrict__ equal, uint32_t* __restrict__ n_equal) {
+  __shared__ uint32_t sh[kT / 64];
+  const uint32_t g = blockIdx.x;
+  const Grp gr = G[g];
+  const uint32_t t0 = TP[g], t1 = t0 + ceil_div(gr.size, kDTile);
+  const uint32_t d = threadIdx.x;
+  uint32_t total = 0;
+  for (uint32_t t = t0; t < t1; t++) total += hist[(size_t)t * 256 + d];
+  uint32_t incl = block_incl_sum(total, sh, (uint32_t*)nullptr);
+  uint32_t base = gr.start + incl - total;
+  tot[(size_t)g * 256 + d] = total;
+  uint32_t run = base;
+  for (uint32_t t = t0; t < t1; t++) {
+    uint32_t c = hist[(size_t)t * 256 + d];
+    hist[(size_t)t * 256 + d] = run;
+    run += c;
+  }
+  if (total >= 2) {
+    Grp nb{base, total, gr.unit, gr.flags ^ 1u};
+    if (mode == 1) next[atomicAdd(n_next, 1u)] = nb;
+    else if (total <= kSmall) small[atomicAdd(n_small, 1u)] = nb;
+    else if (mode == 0) next[atomicAdd(n_next, 1u)] = nb;
+    else equal[atomicAdd(n_equal, 1u)] = nb;
+  }
+}
+
+__global__ void __launch_bounds__(kT) k_dscatter(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+                                                 uint32_t shift, SortBufs B, const uint32_t* __restrict__ off,
+                                                 const uint32_t* __restrict__ tot) {
+  __shared__ uint32_t cnt[256];
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t single[256];
+  const uint32_t t = blockIdx.x;
+  const uint32_t g = upper_idx(TP, nG, t);
+  const Grp gr = G[g];
+  const uint32_t c = t - TP[g];
+  const uint32_t lo = c * kDTile, hi = min(gr.size, lo + kDTile);
+  const bool alt = gr.flags & 1;
+  const uint32_t* ks = alt ? B.key2 : B.key;
+  const uint32_t* vs = alt ? B.sa2 : B.sa;
+  uint32_t* kd = alt ? B.key : B.key2;
+  uint32_t* vd = alt ? B.sa : B.sa2;
+  cnt[threadIdx.x] = 0;
+  base[threadIdx.x] = off[(size_t)t * 256 + threadIdx.x];
+  single[threadIdx.x] = tot[(size_t)g * 256 + threadIdx.x] == 1;
+  __syncthreads();
+  const uint32_t sb = B.units[gr.unit].sbase;
+  for (uint32_t e = lo + threadIdx.x; e < hi; e += kT) {
+    const uint32_t k = ks[gr.start + e], v = vs[gr.start + e];
+    const uint32_t d = (k >> shift) & 255u;
+    const uint32_t pos = base[d] + atomicAdd(&cnt[d], 1u);
+    kd[pos] = k;
+    vd[pos] = v;
+    if (single[d]) B.isa[sb + v] = pos;  // a bucket of one: its rotation is now fully ordered
+  }
+}
+
+// Singletons scattered into the alt buffers move to the primary SA.  (Writing them to the
+// primary SA inside k_dscatter would race with other workgroups still reading it.)
+__global__ void __launch_bounds__(kT) k_dsingle(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+                                                SortBufs B, const uint32_t* __restrict__ tot) {
+  __shared__ uint32_t base[257];
+  __shared__ uint32_t sh[kT / 64];
+  const uint32_t t = blockIdx.x;
+  const uint32_t g = upper_idx(TP, nG, t);
+  const Grp gr = G[g];
+  if (gr.flags & 1) return;  // data came from alt: singletons already landed in the primary SA
+  const uint32_t c = t - TP[g];
+  const uint32_t lo = c * kDTile, hi = min(gr.size, lo + kDTile);
+  const uint32_t tv = tot[(size_t)g * 256 + threadIdx.x];
+  const uint32_t incl = block_incl_sum(tv, sh, (uint32_t*)nullptr);
+  base[threadIdx.x] = incl - tv;
+  if (threadIdx.x == kT - 1) base[256] = incl;
+  __syncthreads();
+  for (uint32_t e = lo + threadIdx.x; e < hi; e += kT) {
+    uint32_t a = 0, b = 256;  // bucket d with base[d] <= e < base[d+1]
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (base[m] <= e) a = m;
+      else b = m;
+    }
+    if (base[a + 1] - base[a] == 1) B.sa[gr.start + e] = B.sa2[gr.start + e];
+  }
+}
+
+// ---------------------------------------------------------------- small groups (LDS)
+// tile index of item i = P[i] / kWin; mark the first item of each tile.
+__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_t* __restrict__ first) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t t = P[i] / kWin;
+  if (i == 0 || P[i - 1] / kWin != t) first[t] = i;
+}
+
+struct TileLds {
+  uint32_t keyA[kTileCap], valA[kTileCap], keyB[kTileCap], valB[kTileCap];
+  uint32_t hist[4][256];
+  // items start inside a kWin window and hold >= 2 elements: at most kWin / 2 per tile
+  uint32_t ioff[kWin / 2 + 1];  // tile-local offset of each item (+ end)
+  uint32_t istart[kWin / 2];
+  uint32_t iunit[kWin / 2];
+  uint32_t sh[8];
+  uint32_t misc[8];
+};
+
+// Stable LSD radix sort of n (<= kTileCap) (key, val) pairs in LDS over bits [0, nbits).
+// 4 waves; wave w owns elements [w*1024, w*1024+1024), visited 64 at a time in order.
+__device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*& keys, uint32_t*& vals) {
+  uint32_t* kin = S.keyA;
+  uint32_t* vin = S.valA;
+  uint32_t* kout = S.keyB;
+  uint32_t* vout = S.valB;
+  const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
+  for (uint32_t shift = 0; shift < nbits; shift += 8) {
+    for (int i = threadIdx.x; i < 4 * 256; i += kT) (&S.hist[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t dig[16], loc[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t e = w * 1024 + j * 64 + lane;
+      const bool act = e < n;
+      const uint64_t amask = __ballot(act);
+      uint32_t d = act ? (kin[e] >> shift) & 255u : 0u;
+      const uint64_t peers = match_byte(d, amask);
+      const uint32_t rank = __popcll(peers & lanemask_lt());
+      uint32_t old = act ? S.hist[w][d] : 0u;
+      const bool leader = act && ((peers & lanemask_lt()) == 0);
+      if (leader) S.hist[w][d] = old + (uint32_t)__popcll(peers);
+      dig[j] = d;
+      loc[j] = old + rank;
+    }
+    __syncthreads();
+    {  // digit bases: exclusive over (digit, wave)
+      const uint32_t d = threadIdx.x;
+      uint32_t c0 = S.hist[0][d], c1 = S.hist[1][d], c2 = S.hist[2][d], c3 = S.hist[3][d];
+      uint32_t tot = c0 + c1 + c2 + c3;
+      uint32_t incl = block_incl_sum(tot, S.sh, (uint32_t*)nullptr);
+      uint32_t b = incl - tot;
+      S.hist[0][d] = b;
+      S.hist[1][d] = b + c0;
+      S.hist[2][d] = b + c0 + c1;
+      S.hist[3][d] = b + c0 + c1 + c2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t e = w * 1024 + j * 64 + lane;
+      if (e < n) {
+        const uint32_t dst = S.hist[w][dig[j]] + loc[j];
+        kout[dst] = kin[e];
+        vout[dst] = vin[e];
+      }
+    }
+    __syncthreads();
+    uint32_t* t;
+    t = kin; kin = kout; kout = t;
+    t = vin; vin = vout; vout = t;
+  }
+  keys = kin;
+  vals = vin;
+}
+
+__global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small, uint32_t n_small,
+                                                  const uint32_t* __restrict__ P, const uint32_t* __restrict__ first,
+                                                  uint32_t key_bits, SortBufs B, Grp* __restrict__ next,
+                                                  uint32_t* __restrict__ n_next) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  TileLds& S = *reinterpret_cast<TileLds*>(smem);
+  const uint32_t t = blockIdx.x;
+  const uint32_t i0 = first[t];
+  if (i0 == 0xffffffffu) return;
+  // items of this tile: i0 .. i1-1 with P[i]/kWin == t
+  if (threadIdx.x == 0) S.misc[0] = n_small;
+  __syncthreads();
+  for (uint32_t i = i0 + threadIdx.x; i < n_small && i < i0 + kWin / 2 + 1; i += kT)
+    if (P[i] / kWin != t) atomicMin(&S.misc[0], i);
+  __syncthreads();
+  const uint32_t i1 = min(S.misc[0], i0 + kWin / 2);
+  const uint32_t ni = i1 - i0;
+  const uint32_t p0 = P[i0];
+  for (uint32_t j = threadIdx.x; j < ni; j += kT) {
+    const Grp g = small[i0 + j];
+    S.ioff[j] = P[i0 + j] - p0;
+    S.istart[j] = g.start;
+    S.iunit[j] = g.unit | ((g.flags & 1u) << 31);
+    if (j == ni - 1) S.ioff[ni] = P[i0 + j] - p0 + g.size;
+  }
+  __syncthreads();
+  const uint32_t n = S.ioff[ni];
+  const uint32_t kmask = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
+  for (uint32_t e = threadIdx.x; e < n; e += kT) {
+    // item of element e
+    uint32_t lo = 0, hi = ni;
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (S.ioff[mid] <= e) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t s = S.istart[lo] + (e - S.ioff[lo]);
+    const bool alt = S.iunit[lo] >> 31;
+    const uint32_t k = alt ? B.key2[s] : B.key[s];
+    const uint32_t v = alt ? B.sa2[s] : B.sa[s];
+    S.keyA[e] = (lo << key_bits) | (k & kmask);
+    S.valA[e] = v;
+  }
+  __syncthreads();
+  const uint32_t item_bits = 32 - __builtin_clz(ni);  // ni >= 1
+  uint32_t *keys, *vals;
+  lds_radix_sort(S, n, key_bits + item_bits, keys, vals);
+  // group detection over the sorted composite keys; thread t owns [16t, 16t+16)
+  uint32_t starts = 0;
+  const uint32_t e0 = threadIdx.x * 16;
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const uint32_t e = e0 + q;
+    if (e < n && (e == 0 || keys[e] != keys[e - 1])) starts++;
+  }
+  uint32_t ngroups;
+  uint32_t incl = block_incl_sum(starts, S.sh, &ngroups);
+  // gpos[o] = first element of group o, stored in the free B/A buffer (not keys/vals)
+  uint32_t* gpos = (keys == S.keyA) ? S.keyB : S.keyA;
+  {
+    uint32_t o = incl - starts;
+    for (int q = 0; q < 16; q++) {
+      const uint32_t e = e0 + q;
+      if (e < n && (e == 0 || keys[e] != keys[e - 1])) gpos[o++] = e;
+    }
+  }
+  if (threadIdx.x == 0) gpos[ngroups] = n;
+  __syncthreads();
+  // groups of size >= 2 go to the next iteration
+  uint32_t nnew = 0;
+  {
+    uint32_t o = incl - starts;
+    for (int q = 0; q < 16; q++) {
+      const uint32_t e = e0 + q;
+      if (e < n && (e == 0 || keys[e] != keys[e - 1])) {
+        if (gpos[o + 1] - e >= 2) nnew++;
+        o++;
+      }
+    }
+  }
+  uint32_t tot_new;
+  uint32_t incl_new = block_incl_sum(nnew, S.sh, &tot_new);
+  if (threadIdx.x == 0) S.misc[1] = tot_new ? atomicAdd(n_next, tot_new) : 0;
+  __syncthreads();
+  uint32_t wpos = S.misc[1] + incl_new - nnew;
+  uint32_t o = incl - starts;
+  uint32_t gstart = 0;
+  // group start for the first element of this thread: the last start <= e0
+  if (e0 < n) {
+    uint32_t lo = 0, hi = ngroups;  // largest o with gpos[o] <= e0
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (gpos[mid] <= e0) lo = mid;
+      else hi = mid;
+    }
+    gstart = gpos[lo];
+  }
+  for (int q = 0; q < 16; q++) {
+    const uint32_t e = e0 + q;
+    if (e >= n) break;
+    const bool st = (e == 0 || keys[e] != keys[e - 1]);
+    if (st) gstart = e;
+    const uint32_t item = keys[e] >> key_bits;
+    const uint32_t base = S.istart[item] - S.ioff[item];
+    const uint32_t unit = S.iunit[item] & 0x7fffffffu;
+    const uint32_t v = vals[e];
+    const uint32_t slot = base + e, gslot = base + gstart;
+    B.sa[slot] = v;
+    B.isa[B.units[unit].sbase + v] = gslot;
+    if (st) {
+      const uint32_t sz = gpos[o + 1] - e;
+      if (sz >= 2) next[wpos++] = Grp{gslot, sz, unit, 0};
+      o++;
+    }
+  }
+}
+
+// Equal-key groups larger than kSmall: everyone gets the bucket start as rank.
+__global__ void __launch_bounds__(kT) k_equal(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+                                              SortBufs B, Grp* __restrict__ next, uint32_t* __restrict__ n_next) {
+  const uint32_t t = blockIdx.x;
+  const uint32_t g = upper_idx(TP, nG, t);
+  const Grp gr = G[g];
+  const uint32_t c = t - TP[g];
+  const uint32_t lo = c * kDTile, hi = min(gr.size, lo + kDTile);
+  const uint32_t sb = B.units[gr.unit].sbase;
+  const uint32_t* vs = (gr.flags & 1) ? B.sa2 : B.sa;
+  for (uint32_t e = lo + threadIdx.x; e < hi; e += kT) {
+    const uint32_t v = vs[gr.start + e];
+    B.sa[gr.start + e] = v;
+    B.isa[sb + v] = gr.start;
+  }
+  if (c == 0 && threadIdx.x == 0) next[atomicAdd(n_next, 1u)] = Grp{gr.start, gr.size, gr.unit, 0};
+}
+
+// ---------------------------------------------------------------- output
+// bwt[boff[b] + q] = root[(SA[sbase + q / k] - 1) mod p] for q < n_b, k = n_b / p.
+__global__ void k_bwt_out(const uint32_t* __restrict__ boff, uint32_t nb, const Unit* __restrict__ units,
+                          const uint32_t* __restrict__ sa, const uint8_t* __restrict__ text, uint32_t total,
+                          uint8_t* __restrict__ bwt) {
+  uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= total) return;
+  uint32_t b = upper_idx(boff, nb, x);
+  const Unit U = units[b];
+  const uint32_t nbytes = boff[b + 1] - boff[b];
+  const uint32_t k = nbytes / U.len;
+  const uint32_t q = x - boff[b];
+  const uint32_t v = sa[U.sbase + q / k];
+  bwt[x] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
+}
+
+__global__ void k_rank0(const Unit* __restrict__ units, uint32_t nb, const uint32_t* __restrict__ isa,
+                        uint32_t* __restrict__ rank0) {
+  uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < nb) rank0[b] = isa[units[b].sbase] - units[b].sbase;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& h_boff,
+               const std::vector<uint32_t>& h_period, uint8_t* bwt, uint32_t* rank0, SortStats* stats,
+               hipStream_t st) {
+  const uint32_t nb = r.nblocks;
+  if (nb == 0) return;
+  // Units: one per block, the primitive root of the block.
+  std::vector<Unit> hu(nb);
+  uint64_t S = 0;
+  for (uint32_t b = 0; b < nb; b++) {
+    hu[b] = Unit{(uint32_t)S, h_period[b], h_boff[b], 0};
+    S += h_period[b];
+  }
+  Unit* units = ws.typed<Unit>("sort_units", nb);
+  HIP_OK(hipMemcpyAsync(units, hu.data(), sizeof(Unit) * nb, hipMemcpyHostToDevice, st));
+
+  SortBufs B;
+  B.sa = ws.u32("sort_sa", S + 16);
+  B.isa = ws.u32("sort_isa", S + 16);
+  B.key = ws.u32("sort_key", S + 16);
+  B.sa2 = ws.u32("sort_sa2", S + 16);
+  B.key2 = ws.u32("sort_key2", S + 16);
+  B.text = r.blk;
+  B.units = units;
+
+  const size_t lcap = S / 2 + nb + 16;        // groups of >= 2 members
+  // large-list entries: groups larger than kSmall, plus (first pass at h = 0) every bucket
+  // of >= 2 members of every unit
+  const size_t bigcap = S / kSmall + std::min<uint64_t>(256ull * nb, S / 2) + nb + 16;
+  Grp* L = ws.typed<Grp>("sort_L", lcap);
+  Grp* Ln = ws.typed<Grp>("sort_Ln", lcap);
+  Grp* small = ws.typed<Grp>("sort_small", lcap);
+  Grp* large = ws.typed<Grp>("sort_large", bigcap);
+  Grp* large2 = ws.typed<Grp>("sort_large2", bigcap);
+  Grp* equal = ws.typed<Grp>("sort_equal", bigcap);
+  uint32_t* P = ws.u32("sort_P", lcap + 16);
+  uint32_t* TP = ws.u32("sort_TP", bigcap + S / kDTile + 64);
+  uint32_t* first = ws.u32("sort_first", S / kWin + 64);
+  const size_t max_dtiles = S / kDTile + bigcap + 16;
+  uint32_t* hist = ws.u32("sort_hist", max_dtiles * 256);
+  uint32_t* tot = ws.u32("sort_tot", bigcap * 256);
+  uint32_t* cnt = ws.u32("sort_cnt", 64);  // device counters
+  uint32_t* scratch = ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(lcap, max_dtiles)) + 64);
+  // counters: 0 total(scan), 1 n_large, 2 n_small, 3 n_next(L'), 4 n_large2, 5 n_equal, 6 tiles
+  uint32_t hc[8];
+  auto read_counters = [&]() {
+    HIP_OK(hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  };
+  auto grid = [](uint64_t n) { return (unsigned)std::max<uint64_t>(1, ceil_div64(n, kT)); };
+
+  // initial list = units
+  uint32_t nL = nb;
+  k_units_to_groups<<<grid(nb), kT, 0, st>>>(units, nb, L, P);
+  HIP_OK(hipGetLastError());
+  scan_u32(ScanOp::Sum, true, P, P, nL, cnt + 0, scratch, st);
+  k_init_sa<<<grid(S), kT, 0, st>>>(L, P, nL, (uint32_t)S, B.sa);
+  HIP_OK(hipGetLastError());
+
+  const size_t tile_lds = sizeof(TileLds);
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_OK(hipFuncSetAttribute((const void*)k_tile_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
+    attr_set = true;
+  }
+  uint32_t h = 0;
+  int iters = 0;
+  uint64_t unsorted = 0;
+  while (nL > 0) {
+    ++iters;
+    // element prefix over L (for h == 0 it was computed above)
+    if (h > 0) {
+      k_group_sizes<<<grid(nL), kT, 0, st>>>(L, nL, P);
+      HIP_OK(hipGetLastError());
+      scan_u32(ScanOp::Sum, true, P, P, nL, cnt + 0, scratch, st);
+    }
+    HIP_OK(hipMemsetAsync(cnt + 1, 0, 7 * 4, st));
+    read_counters();
+    const uint32_t totalL = hc[0];
+    unsorted += totalL;
+    k_gather<<<grid(totalL), kT, 0, st>>>(L, P, nL, totalL, h, B);
+    HIP_OK(hipGetLastError());
+    k_partition<<<grid(nL), kT, 0, st>>>(L, nL, h == 0 ? 1 : 0, large, cnt + 1, small, cnt + 2);
+    HIP_OK(hipGetLastError());
+    read_counters();
+    uint32_t n_large = hc[1];
+    static const uint32_t dig0[4] = {24, 16, 8, 0};
+    static const uint32_t digh[3] = {12, 4, 0};
+    const uint32_t* digs = h == 0 ? dig0 : digh;
+    const int ndig = h == 0 ? 4 : 3;
+    Grp* lg = large;
+    Grp* lg2 = large2;
+    for (int di = 0; di < ndig && n_large > 0; di++) {
+      const int mode = (h == 0 && di == 0) ? 1 : (di == ndig - 1 ? 2 : 0);
+      k_group_tiles<<<grid(n_large), kT, 0, st>>>(lg, n_large, TP);
+      HIP_OK(hipGetLastError());
+      scan_u32(ScanOp::Sum, true, TP, TP, n_large, cnt + 6, scratch, st);
+      HIP_OK(hipMemsetAsync(cnt + 4, 0, 4, st));
+      read_counters();
+      const uint32_t ntiles = hc[6];
+      k_dhist<<<ntiles, kT, 0, st>>>(lg, n_large, TP, digs[di], B, hist);
+      HIP_OK(hipGetLastError());
+      k_doff<<<n_large, kT, 0, st>>>(lg, n_large, TP, hist, tot, mode, small, cnt + 2, lg2, cnt + 4, equal, cnt + 5);
+      HIP_OK(hipGetLastError());
+      k_dscatter<<<ntiles, kT, 0, st>>>(lg, n_large, TP, digs[di], B, hist, tot);
+      HIP_OK(hipGetLastError());
+      k_dsingle<<<ntiles, kT, 0, st>>>(lg, n_large, TP, B, tot);
+      HIP_OK(hipGetLastError());
+      read_counters();
+      n_large = hc[4];
+      std::swap(lg, lg2);
+    }
+    read_counters();
+    const uint32_t n_small = hc[2];
+    const uint32_t n_equal = hc[5];
+    HIP_OK(hipMemsetAsync(cnt + 3, 0, 4, st));
+    if (n_small > 0) {
+      k_group_sizes<<<grid(n_small), kT, 0, st>>>(small, n_small, P);
+      HIP_OK(hipGetLastError());
+      scan_u32(ScanOp::Sum, true, P, P, n_small, cnt + 0, scratch, st);
+      read_counters();
+      const uint32_t tot_small = hc[0];
+      const uint32_t ntiles = ceil_div(tot_small, kWin);
+      HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
+      k_tile_first<<<grid(n_small), kT, 0, st>>>(P, n_small, first);
+      HIP_OK(hipGetLastError());
+      k_tile_sort<<<ntiles, kT, tile_lds, st>>>(small, n_small, P, first, h == 0 ? 16u : 20u, B, Ln, cnt + 3);
+      HIP_OK(hipGetLastError());
+    }
+    if (n_equal > 0) {
+      k_group_tiles<<<grid(n_equal), kT, 0, st>>>(equal, n_equal, TP);
+      HIP_OK(hipGetLastError());
+      scan_u32(ScanOp::Sum, true, TP, TP, n_equal, cnt + 6, scratch, st);
+      read_counters();
+      k_equal<<<hc[6], kT, 0, st>>>(equal, n_equal, TP, B, Ln, cnt + 3);
+      HIP_OK(hipGetLastError());
+    }
+    read_counters();
+    nL = hc[3];
+    std::swap(L, Ln);
+    h = h == 0 ? 4 : h * 2;
+    if (iters > 40) throw HipFailure(hipErrorUnknown);  // cannot happen for aperiodic roots
+  }
+  k_bwt_out<<<grid(h_boff[nb]), kT, 0, st>>>(r.boff, nb, units, B.sa, r.blk, h_boff[nb], bwt);
+  HIP_OK(hipGetLastError());
+  k_rank0<<<grid(nb), kT, 0, st>>>(units, nb, B.isa, rank0);
+  HIP_OK(hipGetLastError());
+  if (stats) {
+    stats->iterations = iters;
+    stats->unsorted_elems = unsorted;
+  }
+}
+
+}  // namespace bzg

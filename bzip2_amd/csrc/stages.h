@@ -1,0 +1,100 @@
+// stages.h -- the per-batch pipeline stages of the MI355X bzip2 engine and their shared
+// device workspace.  A "batch" is a contiguous run of input bytes in HBM whose blocks are
+// compressed together: RLE1/segmentation (rle1.hip) -> cyclic suffix sort and BWT
+// (sort.hip) -> MTF/RUNA-RUNB (mtf.hip) -> table optimisation, Huffman codes and bit
+// packing (code.hip).
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace bzg {
+
+// Device buffers keyed by name, grown on demand (contents are not preserved on growth).
+class Workspace {
+ public:
+  Workspace() = default;
+  ~Workspace();
+  Workspace(const Workspace&) = delete;
+  Workspace& operator=(const Workspace&) = delete;
+
+  void* get(const std::string& name, size_t bytes);
+  uint8_t* u8(const std::string& name, size_t n) { return (uint8_t*)get(name, n); }
+  uint16_t* u16(const std::string& name, size_t n) { return (uint16_t*)get(name, n * 2); }
+  uint32_t* u32(const std::string& name, size_t n) { return (uint32_t*)get(name, n * 4); }
+  template <typename T>
+  T* typed(const std::string& name, size_t n) { return (T*)get(name, n * sizeof(T)); }
+
+  const uint32_t* crc_table();   // 256 entries, MSB-first CRC-32 (poly 0x04C11DB7)
+  const uint32_t* xpow2_table(); // 48 entries: x^(8*2^k) mod P
+  size_t bytes_reserved() const { return total_; }
+  void release_all();
+
+ private:
+  struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::map<std::string, Buf> bufs_;
+  size_t total_ = 0;
+  uint32_t* crc_ = nullptr;
+  uint32_t* xp2_ = nullptr;
+};
+
+// ---- stage A1/A2 ---------------------------------------------------------------------
+struct Rle1Result {
+  uint64_t consumed = 0;  // input bytes covered by the emitted blocks
+  uint32_t m = 0;         // RLE1 output bytes produced for the whole batch
+  uint32_t nblocks = 0;
+  // device arrays (owned by the workspace)
+  uint8_t* blk = nullptr;       // block bytes, block b at [boff[b], boff[b+1])
+  uint32_t* boff = nullptr;     // nblocks+1
+  uint32_t* binst = nullptr;    // nblocks+1 input offsets (relative to batch start)
+  uint32_t* bcrc = nullptr;     // finalised block CRC
+  uint32_t* inuse = nullptr;    // 8 words per block
+  uint32_t* ninuse = nullptr;
+  uint32_t* period = nullptr;   // primitive period of each block
+};
+void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool final_batch,
+                bool tail_merge, Rle1Result& res, hipStream_t st);
+// in-use maps, nInUse and primitive periods of res.nblocks blocks given res.blk / res.boff
+void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st);
+
+// ---- stage A4 ------------------------------------------------------------------------
+// Sorts the rotations of every block (of its primitive root when periodic) and writes the
+// BWT last column to `bwt` (same offsets as the blocks) and rank0[b] = rank of rotation 0
+// among the distinct rotations of the root.
+struct SortStats {
+  int iterations = 0;
+  uint64_t unsorted_elems = 0;  // sum over iterations of elements in unsorted groups
+};
+void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& h_boff,
+               const std::vector<uint32_t>& h_period, uint8_t* bwt, uint32_t* rank0,
+               SortStats* stats, hipStream_t st);
+
+// ---- stage A6 ------------------------------------------------------------------------
+struct MtfResult {
+  uint16_t* mtfv = nullptr;   // block b at [mtf_off[b], mtf_off[b] + nmtf[b])
+  uint32_t* mtf_off = nullptr;
+  uint32_t* nmtf = nullptr;
+  uint32_t* freq = nullptr;   // 258 per block
+};
+void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t nblocks,
+               uint32_t total_bytes, MtfResult& res, hipStream_t st);
+
+// ---- stage A7/A8/A3 --------------------------------------------------------------------
+struct StreamCarry {
+  uint32_t combined_crc = 0;
+  uint8_t carry_byte = 0;   // pending high bits of an unfinished output byte
+  uint8_t carry_bits = 0;   // 0..7
+  bool header_done = false;
+};
+// Encodes all blocks into `out` (device), starting with the carried partial byte; when
+// `final_batch` appends the stream trailer.  Returns bytes fully written; updates carry.
+uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, const uint32_t* origptr,
+                    uint32_t nblocks, int level, bool final_batch, StreamCarry& carry, uint8_t* out,
+                    uint64_t out_cap, hipStream_t st);
+
+}  // namespace bzg

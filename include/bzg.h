@@ -1,0 +1,90 @@
+/* bzg.h -- C ABI of the MI355X bzip2 compression engine (libbz2_amd.so).
+ *
+ * The engine is the device-side replacement of the reference's per-block compression path:
+ *   BZ2_compressBlock (reference compress.c:822-881) with BZ2_blockSort (blocksort.c:1534),
+ *   generateMTFValues (compress.c:93), sendMTFValues (compress.c:250) and the RLE1 /
+ *   block-segmentation loop copy_input_until_stop / handle_compress (bzlib.c:211-396).
+ * The same library also exports the unchanged bzlib.h ABI (see include/bzlib.h); these bzg_*
+ * entry points are the thin C layer under it, usable directly with device-resident buffers.
+ *
+ * All pointers are plain pointers; sizes are bytes.  d_* pointers are HIP device pointers on
+ * the engine's current device.  `stream` is a hipStream_t (NULL = the engine's own stream).
+ * Return values use the bzlib.h codes (BZ_OK, BZ_PARAM_ERROR, BZ_MEM_ERROR, BZ_OUTBUFF_FULL,
+ * BZ_CONFIG_ERROR when no usable GPU is present).  The engine never calls exit().
+ */
+#ifndef BZG_H
+#define BZG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Stream state carried between batches of one .bz2 stream. */
+typedef struct {
+  uint32_t combined_crc; /* running combined CRC (compress.c:827-828) */
+  uint32_t blocks_done;  /* blocks emitted so far */
+  uint8_t carry_byte;    /* pending high bits of an unfinished output byte */
+  uint8_t carry_bits;    /* 0..7 */
+  uint8_t header_done;   /* "BZh<level>" already emitted */
+  uint8_t level;         /* blockSize100k, 1..9 */
+} bzg_stream_state;
+
+void bzg_stream_init(bzg_stream_state *st, int level);
+
+/* Flags for bzg_compress_device. */
+#define BZG_FLAG_END_SEGMENT 1u /* flush the pending run (FLUSH/FINISH semantics)        */
+#define BZG_FLAG_TAIL_MERGE 2u  /* the last input byte arrived with FLUSH/FINISH          */
+#define BZG_FLAG_TRAILER 4u     /* write the end-of-stream trailer (FINISH)              */
+
+/* Compress a device-resident byte range as the continuation of stream `st`.
+ * Without BZG_FLAG_END_SEGMENT only complete blocks are emitted and *consumed may be < n:
+ * the caller re-submits input from d_in + *consumed (RUN semantics, bzlib.c:383-386).
+ * The output written to d_out starts with st->carry_bits pending bits (merged), and
+ * *out_bytes whole bytes are final; the unfinished last byte moves to st->carry_*.
+ * Replaces: the compress half of handle_compress (bzlib.c:361-396). */
+int bzg_compress_device(const void *d_in, uint64_t n, unsigned flags, bzg_stream_state *st, void *d_out,
+                        uint64_t out_cap, uint64_t *out_bytes, uint64_t *consumed, void *stream);
+
+/* Host-buffer convenience: one whole .bz2 stream (FINISH with all input, i.e. the segmentation
+ * of BZ2_bzBuffToBuffCompress, bzlib.c:1309-1357).  Returns BZ_OK / BZ_OUTBUFF_FULL / ... */
+int bzg_compress_host(const void *src, uint64_t n, int level, void *dst, uint64_t dst_cap, uint64_t *dst_len);
+
+/* Host buffers, stream continuation: the same contract as bzg_compress_device with src/dst in
+ * host memory (one H2D and one D2H copy).  Used by BZ2_bzCompress's staging. */
+int bzg_compress_host_stream(const void *src, uint64_t n, unsigned flags, bzg_stream_state *st, void *dst,
+                             uint64_t dst_cap, uint64_t *dst_len, uint64_t *consumed);
+
+/* Worst-case output bytes for n input bytes (for sizing d_out). */
+uint64_t bzg_bound(uint64_t n);
+
+/* Per-stage entry points (host buffers), used by the parity tests to compare each stage with
+ * the oracle.  Blocks are concatenated; offsets have nblocks+1 entries. */
+int bzg_stage_rle1(const void *src, uint64_t n, int level, int tail_merge, uint8_t *blocks, uint64_t blocks_cap,
+                   uint32_t *offsets, uint32_t *crcs, uint32_t *nblocks, uint32_t max_blocks);
+int bzg_stage_bwt(const uint8_t *blocks, const uint32_t *offsets, uint32_t nblocks, uint8_t *bwt, int32_t *origptr);
+int bzg_stage_mtf(const uint8_t *bwt, const uint32_t *offsets, uint32_t nblocks, uint16_t *mtfv,
+                  uint32_t *mtf_offsets, uint32_t *nmtf, uint32_t *freq);
+
+/* Timing of the last bzg_compress_device call, per stage, from HIP events (ms). */
+typedef struct {
+  float rle1_ms, bwt_ms, mtf_ms, code_ms, total_ms;
+  uint32_t nblocks;
+  uint32_t sort_iterations;
+  uint64_t rle_bytes;         /* RLE1 output bytes (block bytes) */
+  uint64_t sort_unsorted;     /* elements revisited by doubling iterations */
+  uint64_t mtf_symbols;       /* total nMTF */
+} bzg_stats;
+void bzg_last_stats(bzg_stats *out);
+
+/* Release the engine's device memory (it is re-acquired on the next call). */
+void bzg_release(void);
+
+/* 1 if a HIP device is usable by the engine. */
+int bzg_device_ok(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
