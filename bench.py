@@ -1,0 +1,169 @@
+"""bench.py -- input-side MB/s of the MI355X bzip2 compression path at -9 (BASELINE.json metric).
+
+Workload (per GPU): 1e9 bytes of seeded enwik9-class synthetic text (tests/datagen.py; enwik9
+itself is not available offline), resident in HBM before the timed region; one step = one
+complete .bz2 stream (RLE1 -> BWT -> MTF -> Huffman -> packing, bit-exact with the reference)
+written to HBM.  N GPUs = N ranks, each compressing its own 1e9-byte stream (independent
+objects, no data-path collective): scaling "weak", value = total bytes / max-over-ranks time.
+
+Also reported on rank 0: the reference CPU path timed on a bounded sample of the same text
+(oracle/_ref = the reference's own blocksort.c/compress.c build, 1 thread), a bit-exactness
+check of the GPU stream against it on that sample, the per-stage split from HIP events, and
+the roofline of SURVEY.md section 8(d): B_alg = 1 + 25*rho + 3*c bytes per input byte against
+the 8 TB/s HBM peak.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bzip2_amd as B  # noqa: E402
+from tests import datagen  # noqa: E402
+
+METRIC = "input-side MB/s at -9 on enwik9, bit-exact .bz2, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--bytes", type=int, default=1_000_000_000, help="input bytes per GPU")
+    p.add_argument("--level", type=int, default=9)
+    p.add_argument("--cpu-sample", type=int, default=200_000_000, help="bytes for the CPU reference timing")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    if dist:
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    t0 = time.time()
+    data = datagen.text(a.bytes, 0x5EED0001 + rank)
+    gen_s = time.time() - t0
+    d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+    cap = B.bound(len(data))
+    d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def step():
+        nb, cons, _ = B.compress_device(d_in.data_ptr(), len(data), a.level, d_out.data_ptr(), cap, stream_ptr=sp)
+        return nb
+
+    for _ in range(a.warmup):
+        out_bytes = step()
+    torch.cuda.synchronize()
+    stage_ms = {"rle1": 0.0, "bwt": 0.0, "mtf": 0.0, "code": 0.0, "total": 0.0}
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        out_bytes = step()
+        s = B.last_stats()
+        for k in ("rle1", "bwt", "mtf", "code", "total"):
+            stage_ms[k] += s[k + "_ms"] / a.steps
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = B.last_stats()
+    ms_per_step = elapsed * 1000.0 / a.steps
+    total_bytes = a.bytes * world * a.steps
+    value = total_bytes / elapsed / 1e6  # MB/s, whole job
+
+    if rank == 0:
+        ratio = out_bytes / a.bytes
+        rho = stats["rle_bytes"] / a.bytes
+        b_alg = 1.0 + 25.0 * rho + 3.0 * ratio
+        achieved = a.bytes * b_alg / (ms_per_step / 1000.0) / 1e9
+        bwt_alg = 11.0 * stats["rle_bytes"]  # read T + write SA + read SA + gather T + write L
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"enwik9-class synthetic text (tests/datagen.py), {a.bytes} B per GPU, -{a.level}",
+                       "level": a.level, "bytes_per_gpu": a.bytes, "blocks": stats["nblocks"],
+                       "bz2_ratio": round(ratio, 4), "rle1_rho": round(rho, 4),
+                       "parallelism": f"{world} independent streams"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "model": "SURVEY.md 8(d) B_alg = 1 + 25*rho + 3*c bytes per input byte, whole pipeline",
+                         "b_alg_per_byte": round(b_alg, 3),
+                         "dominant_stage": {"name": "bwt", "ms": round(stage_ms["bwt"], 3),
+                                            "alg_bytes": bwt_alg,
+                                            "achieved_GBps": round(bwt_alg / (stage_ms["bwt"] / 1e3) / 1e9, 2)
+                                            if stage_ms["bwt"] > 0 else None}},
+            "stages_ms": {k: round(v, 3) for k, v in stage_ms.items()},
+            "sort_iterations": stats["sort_iterations"],
+            "gen_s": round(gen_s, 1),
+        }
+        if not a.no_cpu:
+            result.update(cpu_and_parity(data, a, d_in))
+        print(json.dumps(result), flush=True)
+    if dist:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+def cpu_and_parity(data, a, d_in):
+    """Reference CPU timing on a bounded sample, and GPU-vs-reference bytes on it."""
+    from tests import oracles as O
+
+    n = min(a.cpu_sample, len(data))
+    sample = data[:n]
+    if O.has_ref():
+        kind = "reference"
+        t = time.perf_counter()
+        ref_out = O.ref_compress(sample, a.level)
+        cpu_s = time.perf_counter() - t
+    else:
+        kind = "port"
+        t = time.perf_counter()
+        ref_out = O.orc_compress(sample, a.level)
+        cpu_s = time.perf_counter() - t
+    cap = B.bound(n)
+    d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    nb, _, _ = B.compress_device(d_in.data_ptr(), n, a.level, d_out.data_ptr(), cap)
+    torch.cuda.synchronize()
+    gpu_sample = d_out[:nb].cpu().numpy().tobytes()
+    return {
+        "cpu_baseline": {"value": round(n / cpu_s / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": kind,
+                         "sample": f"first {n} B of the rank-0 input, BZ2_bzBuffToBuffCompress -{a.level}, "
+                                   f"{cpu_s:.1f} s"},
+        "parity": {"sample_bytes": n, "bit_exact": gpu_sample == ref_out, "against": kind,
+                   "out_bytes": len(ref_out)},
+    }
+
+
+if __name__ == "__main__":
+    main()

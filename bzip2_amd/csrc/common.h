@@ -120,6 +120,18 @@ __device__ __forceinline__ uint64_t match_byte(uint32_t d, uint64_t active) {
   return m;
 }
 
+// List append with one atomic per wave: every lane of the wave must call it; lanes with
+// `pred` get consecutive slots.  Returns the slot (undefined when !pred).
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0) return 0;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if (__lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = (uint32_t)__shfl((int)base, leader, 64);
+  return base + (uint32_t)__popcll(m & lanemask_lt());
+}
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 }  // namespace bzg

@@ -18,6 +18,7 @@
 //   * new groups of size >= 2 form the next iteration's list; h doubles.
 // All keys of an iteration are gathered before any rank is rewritten.
 #include <algorithm>
+#include <cstdlib>
 
 #include "scan.h"
 #include "stages.h"
@@ -115,11 +116,15 @@ __global__ void __launch_bounds__(kT) k_gather(const Grp* __restrict__ L, const 
 // Split L into the large list (digit passes) and the small list (LDS tiles).
 __global__ void k_partition(const Grp* __restrict__ L, uint32_t nL, int force_large, Grp* __restrict__ large,
                             uint32_t* __restrict__ n_large, Grp* __restrict__ small, uint32_t* __restrict__ n_small) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nL) return;
-  Grp G = L[g];
-  if (force_large || G.size > kSmall) large[atomicAdd(n_large, 1u)] = G;
-  else small[atomicAdd(n_small, 1u)] = G;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = g < nL;
+  Grp G{0, 0, 0, 0};
+  if (valid) G = L[g];
+  const bool big = valid && (force_large || G.size > kSmall);
+  const uint32_t pl = wave_append(n_large, big);
+  const uint32_t ps = wave_append(n_small, valid && !big);
+  if (big) large[pl] = G;
+  else if (valid) small[ps] = G;
 }
 
 // ---------------------------------------------------------------- digit passes (large)
@@ -163,13 +168,17 @@ __global__ void __launch_bounds__(kT) k_doff(const Grp* __restrict__ G, uint32_t
     hist[(size_t)t * 256 + d] = run;
     run += c;
   }
-  if (total >= 2) {
-    Grp nb{base, total, gr.unit, gr.flags ^ 1u};
-    if (mode == 1) next[atomicAdd(n_next, 1u)] = nb;
-    else if (total <= kSmall) small[atomicAdd(n_small, 1u)] = nb;
-    else if (mode == 0) next[atomicAdd(n_next, 1u)] = nb;
-    else equal[atomicAdd(n_equal, 1u)] = nb;
-  }
+  const Grp nb{base, total, gr.unit, gr.flags ^ 1u};
+  const bool emit = total >= 2;
+  const bool to_next = emit && (mode == 1 || (total > kSmall && mode == 0));
+  const bool to_small = emit && !to_next && total <= kSmall;
+  const bool to_equal = emit && !to_next && !to_small;
+  const uint32_t pn = wave_append(n_next, to_next);
+  const uint32_t ps = wave_append(n_small, to_small);
+  const uint32_t pe = wave_append(n_equal, to_equal);
+  if (to_next) next[pn] = nb;
+  if (to_small) small[ps] = nb;
+  if (to_equal) equal[pe] = nb;
 }
 
 __global__ void __launch_bounds__(kT) k_dscatter(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
@@ -526,6 +535,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   k_init_sa<<<grid(S), kT, 0, st>>>(L, P, nL, (uint32_t)S, B.sa);
   HIP_OK(hipGetLastError());
 
+  static const bool debug = getenv("BZG_DEBUG") != nullptr;
+  std::vector<uint32_t> hsz;  // debug: sizes of the groups in L
   const size_t tile_lds = sizeof(TileLds);
   static bool attr_set = false;
   if (!attr_set) {
@@ -547,6 +558,21 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     read_counters();
     const uint32_t totalL = hc[0];
     unsorted += totalL;
+    if (debug) {
+      std::vector<Grp> hg(nL);
+      HIP_OK(hipMemcpy(hg.data(), L, sizeof(Grp) * nL, hipMemcpyDeviceToHost));
+      uint64_t bins[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // elements in groups of size 2,3-4,5-8,9-32,33-256,257-2048,>2048
+      uint64_t gb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (const Grp& g : hg) {
+        const int bi = g.size <= 2 ? 0 : g.size <= 4 ? 1 : g.size <= 8 ? 2 : g.size <= 32 ? 3 : g.size <= 256 ? 4
+                       : g.size <= 2048 ? 5 : 6;
+        bins[bi] += g.size;
+        gb[bi]++;
+      }
+      fprintf(stderr, "[bzg sort] h=%u groups=%u elems=%u | elems by group size 2:%lu 3-4:%lu 5-8:%lu 9-32:%lu "
+              "33-256:%lu 257-2k:%lu >2k:%lu | groups >2k:%lu\n", h, nL, totalL, bins[0], bins[1], bins[2], bins[3],
+              bins[4], bins[5], bins[6], gb[6]);
+    }
     k_gather<<<grid(totalL), kT, 0, st>>>(L, P, nL, totalL, h, B);
     HIP_OK(hipGetLastError());
     k_partition<<<grid(nL), kT, 0, st>>>(L, nL, h == 0 ? 1 : 0, large, cnt + 1, small, cnt + 2);
