@@ -42,7 +42,7 @@ EXPORTS = [
 ENGINE_EXPORTS = [
     "bzg_stream_init", "bzg_compress_device", "bzg_compress_host", "bzg_compress_host_stream",
     "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_last_stats",
-    "bzg_release", "bzg_device_ok",
+    "bzg_release", "bzg_device_ok", "bzg_periodic_origptr",
 ]
 
 
@@ -113,6 +113,8 @@ def lib() -> ctypes.CDLL:
         L.bzg_stage_bwt.argtypes = [vp, vp, u32, vp, vp]
         L.bzg_stage_mtf.argtypes = [vp, vp, u32, vp, vp, vp, vp]
         L.bzg_last_stats.argtypes = [ctypes.POINTER(bzg_stats)]
+        L.bzg_periodic_origptr.argtypes = [vp, ctypes.c_int32]
+        L.bzg_periodic_origptr.restype = ctypes.c_int32
         _lib = L
     return _lib
 
@@ -213,6 +215,11 @@ def compress_device(d_in_ptr: int, n: int, level: int, d_out_ptr: int, out_cap: 
     if rc != BZ_OK:
         raise BzError(rc, "bzg_compress_device")
     return ob.value, cons.value, st
+
+
+def periodic_origptr(block: bytes) -> int:
+    """origPtr the reference assigns to an exactly periodic block (host replay, A5)."""
+    return int(lib().bzg_periodic_origptr(bytes(block), len(block)))
 
 
 def last_stats() -> dict:

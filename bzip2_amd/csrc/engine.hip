@@ -309,6 +309,15 @@ void bzg_release(void) {
   }
 }
 
+int32_t bzg_periodic_origptr(const uint8_t* block, int32_t n) {
+  if (!block || n <= 0) return -1;
+  try {
+    return periodic_origptr(block, n);
+  } catch (const ResolverFailure&) {
+    return -1;
+  }
+}
+
 // ---------------------------------------------------------------- per-stage entry points
 int bzg_stage_rle1(const void* src, uint64_t n, int level, int tail_merge, uint8_t* blocks, uint64_t blocks_cap,
                    uint32_t* offsets, uint32_t* crcs, uint32_t* nblocks, uint32_t max_blocks) {

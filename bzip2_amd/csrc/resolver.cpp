@@ -1,32 +1,1440 @@
-// resolver.cpp -- see resolver.h.
+// resolver.cpp -- origPtr of exactly periodic blocks.
+//
+// For an aperiodic block every rotation is distinct and the GPU sort alone determines the
+// BWT and origPtr.  For a block w^k (k >= 2) the k copies of each rotation are identical:
+// the BWT bytes are still determined, but the reference's origPtr is the position its
+// divsufsort happened to leave rotation 0 in among its copies.  That choice is a property of
+// the exact sequence of partitions, merges, heap sorts and budget checks the reference's
+// modified divsufsort performs (reference blocksort.c:83-1545), so the only way to reproduce
+// it is to replay that algorithm.  This file does so on the host, for periodic blocks only
+// (one 900 kB replay per distinct periodic block; results are memoised), following the
+// reference operation for operation:
+//   * type classification / B* bucketing with the cyclic wrap (blocksort.c:1314-1376),
+//   * B*-substring sort: multikey introsort over 1024-element runs merged in place with an
+//     auxiliary buffer, plus the wrap-around last suffix (blocksort.c:83-664),
+//   * tandem-repeat sort of the reduced string with its work budget and the
+//     Larsson-Sadakane fallback (blocksort.c:669-1309),
+//   * induced sort that reports origPtr (blocksort.c:1439-1501).
+// The algorithm is Yuta Mori's divsufsort (MIT licence, reproduced below as that licence
+// requires) as modified by the reference for cyclic rotations.
+//
+// divsufsort  Copyright (c) 2003-2007 Yuta Mori All Rights Reserved.
+// Permission is hereby granted, free of charge, to any person obtaining a copy of this
+// software and associated documentation files (the "Software"), to deal in the Software
+// without restriction, including without limitation the rights to use, copy, modify, merge,
+// publish, distribute, sublicense, and/or sell copies of the Software, and to permit persons
+// to whom the Software is furnished to do so, subject to the following conditions: The above
+// copyright notice and this permission notice shall be included in all copies or substantial
+// portions of the Software.  THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND,
+// EXPRESS OR IMPLIED, INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY, FITNESS
+// FOR A PARTICULAR PURPOSE AND NONINFRINGEMENT. IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT
+// HOLDERS BE LIABLE FOR ANY CLAIM, DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF
+// CONTRACT, TORT OR OTHERWISE, ARISING FROM, OUT OF OR IN CONNECTION WITH THE SOFTWARE OR THE
+// USE OR OTHER DEALINGS IN THE SOFTWARE.
 #include "resolver.h"
 
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <map>
 #include <string>
+#include <utility>
 
 namespace bzg {
 
+namespace a5 {
+
+using i32 = int32_t;
+using i64 = int64_t;
+using u8 = uint8_t;
+
+constexpr int kInsertion = 8;     // INSERTIONSORT_THRESHOLD
+constexpr int kRun = 1024;        // SS_BLOCKSIZE
+
+template <typename T>
+inline void swp(T& a, T& b) {
+  T t = a;
+  a = b;
+  b = t;
+}
+
+// floor(log2(n)) with -1 for 0, as a 256-entry table lookup applied per byte.
+inline int lg8(unsigned v) {
+  int r = -1;
+  while (v) {
+    v >>= 1;
+    ++r;
+  }
+  return r;
+}
+// substring-sort variant: only bits 0..15 are ever examined
+inline i64 lg_ss(i64 n) { return (n & 0xff00) ? 8 + lg8((unsigned)((n >> 8) & 0xff)) : lg8((unsigned)(n & 0xff)); }
+inline i32 lg_tr(i32 n) {
+  const unsigned u = (unsigned)n;
+  if (u & 0xffff0000u) return (u & 0xff000000u) ? 24 + lg8((u >> 24) & 0xff) : 16 + lg8((u >> 16) & 0xff);
+  return (u & 0x0000ff00u) ? 8 + lg8((u >> 8) & 0xff) : lg8(u & 0xff);
+}
+
+// LIFO work stack (the reference keeps fixed 64-entry arrays; order is what matters).
+template <typename E>
+struct Stack {
+  std::vector<E> v;
+  void push(const E& e) { v.push_back(e); }
+  bool pop(E& e) {
+    if (v.empty()) return false;
+    e = v.back();
+    v.pop_back();
+    return true;
+  }
+};
+
+// ====================================================================== B*-substring sort
+struct SubstringSorter {
+  const u8* T;   // block text, T[-1] and T[n] valid
+  const i32* PA; // B* positions (ascending), PA[i] ... PA[i+1] delimit substring i
+
+  // compare substrings p1 and p2 starting at depth Td-T (blocksort.c:83-101)
+  i64 cmp(const i32* p1, const i32* p2, const u8* Td) const {
+    const u8 *a = Td + *p1, *b = Td + *p2, *ae = T + *(p1 + 1), *be = T + *(p2 + 1);
+    while (a < ae && b < be && *a == *b) ++a, ++b;
+    if (a < ae) return b < be ? (i64)*a - (i64)*b : 1;
+    return b < be ? -1 : 0;
+  }
+  i64 cmp_merge(const i32* p1, const i32* p2) const { return cmp(p1, p2, T); }
+  // the last B* substring wraps around the end of the block (blocksort.c:122-148)
+  i64 cmp_last(const i32* p1, const i32* p2, i64 size) const {
+    const u8 *a = T + *p1, *b = T + *p2, *ae = T + size - 2, *be = T + *(p2 + 1);
+    while (a < ae && b < be && *a == *b) ++a, ++b;
+    if (a < ae) return b < be ? (i64)*a - (i64)*b : 1;
+    if (b == be) return 1;
+    for (a -= size, ae = T + PA[0]; a < ae && b < be && *a == *b; ++a, ++b) {
+    }
+    if (a < ae) return b < be ? (i64)*a - (i64)*b : 1;
+    return b < be ? -1 : 0;
+  }
+
+  void insertion(i32* first, i32* last, const u8* Td) const {
+    i64 r = 0;
+    for (i32* i = last - 2; first <= i; --i) {
+      const i32 t = *i;
+      i32* j = i + 1;
+      while (0 < (r = cmp(PA + t, PA + *j, Td))) {
+        do {
+          *(j - 1) = *j;
+        } while (++j < last && *j < 0);
+        if (last <= j) break;
+      }
+      if (r == 0) *j = ~*j;
+      *(j - 1) = t;
+    }
+  }
+
+  int key(const u8* Td, i32 s) const { return Td[PA[s]]; }
+
+  void sift(const u8* Td, i32* SA, i64 i, i64 size) const {
+    const i32 v = SA[i];
+    const int c = key(Td, v);
+    i64 j, k;
+    while ((j = 2 * i + 1) < size) {
+      k = j++;
+      int d = key(Td, SA[k]);
+      const int e = key(Td, SA[j]);
+      if (d < e) {
+        k = j;
+        d = e;
+      }
+      if (d <= c) break;
+      SA[i] = SA[k];
+      i = k;
+    }
+    SA[i] = v;
+  }
+
+  void heapsort(const u8* Td, i32* SA, i64 size) const {
+    i64 m = size;
+    if (size % 2 == 0) {
+      --m;
+      if (key(Td, SA[m / 2]) < key(Td, SA[m])) swp(SA[m], SA[m / 2]);
+    }
+    for (i64 i = m / 2 - 1; 0 <= i; --i) sift(Td, SA, i, m);
+    if (size % 2 == 0) {
+      swp(SA[0], SA[m]);
+      sift(Td, SA, 0, m);
+    }
+    for (i64 i = m - 1; 0 < i; --i) {
+      const i32 t = SA[0];
+      SA[0] = SA[i];
+      sift(Td, SA, 0, i);
+      SA[i] = t;
+    }
+  }
+
+  i32* med3(const u8* Td, i32* a, i32* b, i32* c) const {
+    if (key(Td, *a) > key(Td, *b)) swp(a, b);
+    if (key(Td, *b) > key(Td, *c)) return key(Td, *a) > key(Td, *c) ? a : c;
+    return b;
+  }
+  i32* med5(const u8* Td, i32* a, i32* b, i32* c, i32* d, i32* e) const {
+    if (key(Td, *b) > key(Td, *c)) swp(b, c);
+    if (key(Td, *d) > key(Td, *e)) swp(d, e);
+    if (key(Td, *b) > key(Td, *d)) {
+      swp(b, d);
+      swp(c, e);
+    }
+    if (key(Td, *a) > key(Td, *c)) swp(a, c);
+    if (key(Td, *a) > key(Td, *d)) {
+      swp(a, d);
+      swp(c, e);
+    }
+    return key(Td, *c) > key(Td, *d) ? d : c;
+  }
+  i32* pivot(const u8* Td, i32* first, i32* last) const {
+    i64 t = last - first;
+    i32* mid = first + t / 2;
+    if (t <= 512) {
+      if (t <= 32) return med3(Td, first, mid, last - 1);
+      t >>= 2;
+      return med5(Td, first, first + t, mid, last - 1 - t, last - 1);
+    }
+    t >>= 3;
+    return med3(Td, med3(Td, first, first + t, first + (t << 1)), med3(Td, mid - t, mid, mid + t),
+                med3(Td, last - 1 - (t << 1), last - 1 - t, last - 1));
+  }
+
+  // moves substrings that end before depth to the front, marking them (blocksort.c:282-298)
+  i32* partition(i32* first, i32* last, i64 depth) const {
+    i32 *a = first - 1, *b = last;
+    for (;;) {
+      while (++a < b && ((i64)PA[*a] + depth) >= ((i64)PA[*a + 1] - 1)) *a = ~*a;
+      while (a < --b && ((i64)PA[*b] + depth) < ((i64)PA[*b + 1] - 1)) {
+      }
+      if (b <= a) break;
+      const i32 t = ~*b;
+      *b = *a;
+      *a = t;
+    }
+    if (first < a) *first = ~*first;
+    return a;
+  }
+
+  struct MkFrame {
+    i32 *a, *b;
+    const u8* c;
+    i64 d;
+  };
+
+  // multikey introsort (blocksort.c:300-424)
+  void multikey(i32* first, i32* last) const {
+    Stack<MkFrame> st;
+    const u8* Td = T;
+    i64 limit = lg_ss(last - first);
+    i32 *a, *b, *c, *d, *e, *f;
+    i64 s, t;
+    int v, x = 0;
+    for (;;) {
+      if (last - first <= kInsertion) {
+        if (1 < last - first) insertion(first, last, Td);
+        MkFrame fr;
+        if (!st.pop(fr)) return;
+        first = fr.a, last = fr.b, Td = fr.c, limit = fr.d;
+        continue;
+      }
+      if (limit-- == 0) heapsort(Td, first, last - first);
+      if (limit < 0) {
+        for (a = first + 1, v = key(Td, *first); a < last; ++a) {
+          if ((x = key(Td, *a)) != v) {
+            if (1 < a - first) break;
+            v = x;
+            first = a;
+          }
+        }
+        if (Td[PA[*first] - 1] < (u8)v) first = partition(first, a, Td - T);
+        if (a - first <= last - a) {
+          if (1 < a - first) {
+            st.push({a, last, Td, -1});
+            last = a, Td += 1, limit = lg_ss(a - first);
+          } else {
+            first = a, limit = -1;
+          }
+        } else {
+          if (1 < last - a) {
+            st.push({first, a, Td + 1, lg_ss(a - first)});
+            first = a, limit = -1;
+          } else {
+            last = a, Td += 1, limit = lg_ss(a - first);
+          }
+        }
+        continue;
+      }
+      a = pivot(Td, first, last);
+      v = key(Td, *a);
+      swp(*first, *a);
+      for (b = first; ++b < last && (x = key(Td, *b)) == v;) {
+      }
+      if ((a = b) < last && x < v) {
+        for (; ++b < last && (x = key(Td, *b)) <= v;)
+          if (x == v) {
+            swp(*b, *a);
+            ++a;
+          }
+      }
+      for (c = last; b < --c && (x = key(Td, *c)) == v;) {
+      }
+      if (b < (d = c) && x > v) {
+        for (; b < --c && (x = key(Td, *c)) >= v;)
+          if (x == v) {
+            swp(*c, *d);
+            --d;
+          }
+      }
+      for (; b < c;) {
+        swp(*b, *c);
+        for (; ++b < c && (x = key(Td, *b)) <= v;)
+          if (x == v) {
+            swp(*b, *a);
+            ++a;
+          }
+        for (; b < --c && (x = key(Td, *c)) >= v;)
+          if (x == v) {
+            swp(*c, *d);
+            --d;
+          }
+      }
+      if (a <= d) {
+        c = b - 1;
+        if ((s = a - first) > (t = b - a)) s = t;
+        for (e = first, f = b - s; 0 < s; --s, ++e, ++f) swp(*e, *f);
+        if ((s = d - c) > (t = last - d - 1)) s = t;
+        for (e = b, f = last - s; 0 < s; --s, ++e, ++f) swp(*e, *f);
+        a = first + (b - a), c = last - (d - c);
+        b = ((u8)v <= Td[PA[*a] - 1]) ? a : partition(a, c, Td - T);
+        if (a - first <= last - c) {
+          if (last - c <= c - b) {
+            st.push({b, c, Td + 1, lg_ss(c - b)});
+            st.push({c, last, Td, limit});
+            last = a;
+          } else if (a - first <= c - b) {
+            st.push({c, last, Td, limit});
+            st.push({b, c, Td + 1, lg_ss(c - b)});
+            last = a;
+          } else {
+            st.push({c, last, Td, limit});
+            st.push({first, a, Td, limit});
+            first = b, last = c, Td += 1, limit = lg_ss(c - b);
+          }
+        } else {
+          if (a - first <= c - b) {
+            st.push({b, c, Td + 1, lg_ss(c - b)});
+            st.push({first, a, Td, limit});
+            first = c;
+          } else if (last - c <= c - b) {
+            st.push({first, a, Td, limit});
+            st.push({b, c, Td + 1, lg_ss(c - b)});
+            first = c;
+          } else {
+            st.push({first, a, Td, limit});
+            st.push({c, last, Td, limit});
+            first = b, last = c, Td += 1, limit = lg_ss(c - b);
+          }
+        }
+      } else {
+        limit += 1;
+        if (Td[PA[*first] - 1] < (u8)v) {
+          first = partition(first, last, Td - T);
+          limit = lg_ss(last - first);
+        }
+        Td += 1;
+      }
+    }
+  }
+
+  static void block_swap(i32* p, i32* q, i64 n) {
+    for (; 0 < n; --n, ++p, ++q) swp(*p, *q);
+  }
+
+  // merge with the left run moved to buf (blocksort.c:436-481)
+  void merge_fwd(i32* buf, i32* first, i32* middle, i32* last) const {
+    i32* bufend = buf + (middle - first);
+    block_swap(buf, first, middle - first);
+    const i32 t = *first;
+    i32 *i = first, *j = buf, *k = middle;
+    for (;;) {
+      const i64 r = cmp_merge(PA + *j, PA + *k);
+      if (r < 0) {
+        do {
+          *i++ = *j;
+          *j++ = *i;
+          if (bufend <= j) {
+            *(bufend - 1) = t;
+            return;
+          }
+        } while (*j < 0);
+      } else if (r > 0) {
+        do {
+          *i++ = *k;
+          *k++ = *i;
+          if (last <= k) {
+            do {
+              *i++ = *j;
+              *j++ = *i;
+            } while (j < bufend);
+            *(bufend - 1) = t;
+            return;
+          }
+        } while (*k < 0);
+      } else {
+        *k = ~*k;
+        do {
+          *i++ = *j;
+          *j++ = *i;
+          if (bufend <= j) {
+            *(bufend - 1) = t;
+            return;
+          }
+        } while (*j < 0);
+        do {
+          *i++ = *k;
+          *k++ = *i;
+          if (last <= k) {
+            do {
+              *i++ = *j;
+              *j++ = *i;
+            } while (j < bufend);
+            *(bufend - 1) = t;
+            return;
+          }
+        } while (*k < 0);
+      }
+    }
+  }
+
+  // merge with the right run moved to buf (blocksort.c:483-542)
+  void merge_bwd(i32* buf, i32* first, i32* middle, i32* last) const {
+    i32* bufend = buf + (last - middle);
+    block_swap(buf, middle, last - middle);
+    const i32* p1;
+    const i32* p2;
+    int x = 0;
+    if (*(bufend - 1) < 0) {
+      x |= 1;
+      p1 = PA + ~*(bufend - 1);
+    } else {
+      p1 = PA + *(bufend - 1);
+    }
+    if (*(middle - 1) < 0) {
+      x |= 2;
+      p2 = PA + ~*(middle - 1);
+    } else {
+      p2 = PA + *(middle - 1);
+    }
+    const i32 t = *(last - 1);
+    i32 *i = last - 1, *j = bufend - 1, *k = middle - 1;
+    for (;;) {
+      const i64 r = cmp_merge(p1, p2);
+      if (r > 0) {
+        if (x & 1) {
+          do {
+            *i-- = *j;
+            *j-- = *i;
+          } while (*j < 0);
+        }
+        *i-- = *j;
+        *j-- = *i;
+        if (j < buf) {
+          *buf = t;
+          return;
+        }
+        if (*j < 0) {
+          x |= 1;
+          p1 = PA + ~*j;
+        } else {
+          x &= ~1;
+          p1 = PA + *j;
+        }
+      } else if (r < 0) {
+        if (x & 2) {
+          do {
+            *i-- = *k;
+            *k-- = *i;
+          } while (*k < 0);
+        }
+        *i-- = *k;
+        *k-- = *i;
+        if (k < first) {
+          do {
+            *i-- = *j;
+            *j-- = *i;
+          } while (buf <= j);
+          *buf = t;
+          return;
+        }
+        if (*k < 0) {
+          x |= 2;
+          p2 = PA + ~*k;
+        } else {
+          x &= ~2;
+          p2 = PA + *k;
+        }
+      } else {
+        if (x & 1) {
+          do {
+            *i-- = *j;
+            *j-- = *i;
+          } while (*j < 0);
+        }
+        *i-- = ~*j;
+        *j-- = *i;
+        if (j < buf) {
+          *buf = t;
+          return;
+        }
+        if (x & 2) {
+          do {
+            *i-- = *k;
+            *k-- = *i;
+          } while (*k < 0);
+        }
+        *i-- = *k;
+        *k-- = *i;
+        if (k < first) {
+          while (buf <= j) {
+            *i-- = *j;
+            *j-- = *i;
+          }
+          *buf = t;
+          return;
+        }
+        if (*j < 0) {
+          x |= 1;
+          p1 = PA + ~*j;
+        } else {
+          x &= ~1;
+          p1 = PA + *j;
+        }
+        if (*k < 0) {
+          x |= 2;
+          p2 = PA + ~*k;
+        } else {
+          x &= ~2;
+          p2 = PA + *k;
+        }
+      }
+    }
+  }
+
+  static i32 idx(i32 a) { return 0 <= a ? a : ~a; }
+  void mark_equal(i32* a) const {
+    if (0 <= *a && cmp_merge(PA + idx(*(a - 1)), PA + *a) == 0) *a = ~*a;
+  }
+
+  struct MgFrame {
+    i32 *a, *b, *c;
+    i64 d;
+  };
+
+  // in-place merge using a buffer of bufsize elements (blocksort.c:544-622)
+  void merge(i32* first, i32* middle, i32* last, i32* buf, i64 bufsize) const {
+    Stack<MgFrame> st;
+    i64 check = 0, next;
+    for (;;) {
+      if (last - middle <= bufsize) {
+        if (first < middle && middle < last) merge_bwd(buf, first, middle, last);
+        if (check & 1) mark_equal(first);
+        if (check & 2) mark_equal(last);
+        MgFrame fr;
+        if (!st.pop(fr)) return;
+        first = fr.a, middle = fr.b, last = fr.c, check = fr.d;
+        continue;
+      }
+      if (middle - first <= bufsize) {
+        if (first < middle) merge_fwd(buf, first, middle, last);
+        if (check & 1) mark_equal(first);
+        if (check & 2) mark_equal(last);
+        MgFrame fr;
+        if (!st.pop(fr)) return;
+        first = fr.a, middle = fr.b, last = fr.c, check = fr.d;
+        continue;
+      }
+      i64 m = 0, len = std::min<i64>(middle - first, last - middle), half = len >> 1;
+      for (; 0 < len; len = half, half >>= 1) {
+        if (cmp_merge(PA + idx(*(middle + m + half)), PA + idx(*(middle - m - half - 1))) < 0) {
+          m += half + 1;
+          half -= (len & 1) ^ 1;
+        }
+      }
+      if (0 < m) {
+        block_swap(middle - m, middle, m);
+        i32 *i = middle, *j = middle;
+        next = 0;
+        if (middle + m < last) {
+          if (*(middle + m) < 0) {
+            for (; *(i - 1) < 0; --i) {
+            }
+            *(middle + m) = ~*(middle + m);
+          }
+          for (j = middle; *j < 0; ++j) {
+          }
+          next = 1;
+        }
+        if (i - first <= last - j) {
+          st.push({j, middle + m, last, (check & 2) | (next & 1)});
+          middle -= m, last = i, check = (check & 1);
+        } else {
+          if (i == middle && middle == j) next <<= 1;
+          st.push({first, middle - m, i, (check & 1) | (next & 2)});
+          first = j, middle += m, check = (check & 2) | (next & 1);
+        }
+      } else {
+        if (check & 1) mark_equal(first);
+        mark_equal(middle);
+        if (check & 2) mark_equal(last);
+        MgFrame fr;
+        if (!st.pop(fr)) return;
+        first = fr.a, middle = fr.b, last = fr.c, check = fr.d;
+      }
+    }
+  }
+
+  // sorts one 2-character bucket of B* substrings (blocksort.c:625-664)
+  void run(i32* first, i32* last, i32* buf, i64 bufsize, i64 lastsuffix, i64 size) const {
+    if (lastsuffix != 0) ++first;
+    i32* a = first;
+    i64 i = 0;
+    for (; a + kRun < last; a += kRun, ++i) {
+      multikey(a, a + kRun);
+      i32* curbuf = a + kRun;
+      i64 curbufsize = last - (a + kRun);
+      if (curbufsize <= bufsize) curbufsize = bufsize, curbuf = buf;
+      i32* b = a;
+      i64 k = kRun, j = i;
+      for (; j & 1; b -= k, k <<= 1, j >>= 1) merge(b - k, b, b + k, curbuf, curbufsize);
+    }
+    multikey(a, last);
+    for (i64 k = kRun; i != 0; k <<= 1, i >>= 1) {
+      if (i & 1) {
+        merge(a - k, a, last, buf, bufsize);
+        a -= k;
+      }
+    }
+    if (lastsuffix != 0) {
+      i64 r = 1;
+      const i32 li = *(first - 1);
+      for (a = first; a < last && (*a < 0 || 0 < (r = cmp_last(PA + li, PA + *a, size))); ++a) *(a - 1) = *a;
+      if (r == 0) *a = ~*a;
+      *(a - 1) = li;
+    }
+  }
+};
+
+// ====================================================================== tandem-repeat sort
+struct TandemSorter {
+  i32* ISA;
+  const i32* ISAn;
+  i32* SA;
+
+  // ISAd[p] with a single cyclic wrap over the ISA array (blocksort.c:669)
+  i32 at(const i32* ISAd, i32 p) const { return (ISAd + p < ISAn) ? ISAd[p] : ISAd[ISA - ISAn + p]; }
+
+  void sift(const i32* ISAd, i32* A, i32 i, i32 size) const {
+    const i32 v = A[i];
+    const i32 c = at(ISAd, v);
+    i32 j, k;
+    while ((j = 2 * i + 1) < size) {
+      k = j++;
+      i32 d = at(ISAd, A[k]);
+      const i32 e = at(ISAd, A[j]);
+      if (d < e) {
+        k = j;
+        d = e;
+      }
+      if (d <= c) break;
+      A[i] = A[k];
+      i = k;
+    }
+    A[i] = v;
+  }
+  void heapsort(const i32* ISAd, i32* A, i32 size) const {
+    i32 m = size;
+    if (size % 2 == 0) {
+      --m;
+      if (at(ISAd, A[m / 2]) < at(ISAd, A[m])) swp(A[m], A[m / 2]);
+    }
+    for (i32 i = m / 2 - 1; 0 <= i; --i) sift(ISAd, A, i, m);
+    if (size % 2 == 0) {
+      swp(A[0], A[m]);
+      sift(ISAd, A, 0, m);
+    }
+    for (i32 i = m - 1; 0 < i; --i) {
+      const i32 t = A[0];
+      A[0] = A[i];
+      sift(ISAd, A, 0, i);
+      A[i] = t;
+    }
+  }
+  void insertion(const i32* ISAd, i32* first, i32* last) const {
+    for (i32* a = first + 1; a < last; ++a) {
+      const i32 t = *a;
+      i32* b = a - 1;
+      i32 r;
+      while (0 > (r = at(ISAd, t) - at(ISAd, *b))) {
+        do {
+          *(b + 1) = *b;
+        } while (first <= --b && *b < 0);
+        if (b < first) break;
+      }
+      if (r == 0) *b = ~*b;
+      *(b + 1) = t;
+    }
+  }
+  i32* med3(const i32* ISAd, i32* a, i32* b, i32* c) const {
+    if (at(ISAd, *a) > at(ISAd, *b)) swp(a, b);
+    if (at(ISAd, *b) > at(ISAd, *c)) return at(ISAd, *a) > at(ISAd, *c) ? a : c;
+    return b;
+  }
+  i32* med5(const i32* ISAd, i32* a, i32* b, i32* c, i32* d, i32* e) const {
+    if (at(ISAd, *b) > at(ISAd, *c)) swp(b, c);
+    if (at(ISAd, *d) > at(ISAd, *e)) swp(d, e);
+    if (at(ISAd, *b) > at(ISAd, *d)) {
+      swp(b, d);
+      swp(c, e);
+    }
+    if (at(ISAd, *a) > at(ISAd, *c)) swp(a, c);
+    if (at(ISAd, *a) > at(ISAd, *d)) {
+      swp(a, d);
+      swp(c, e);
+    }
+    return at(ISAd, *c) > at(ISAd, *d) ? d : c;
+  }
+  i32* pivot(const i32* ISAd, i32* first, i32* last) const {
+    i32 t = (i32)(last - first);
+    i32* mid = first + t / 2;
+    if (t <= 512) {
+      if (t <= 32) return med3(ISAd, first, mid, last - 1);
+      t >>= 2;
+      return med5(ISAd, first, first + t, mid, last - 1 - t, last - 1);
+    }
+    t >>= 3;
+    return med3(ISAd, med3(ISAd, first, first + t, first + (t << 1)), med3(ISAd, mid - t, mid, mid + t),
+                med3(ISAd, last - 1 - (t << 1), last - 1 - t, last - 1));
+  }
+
+  // Three-way partition around v; returns the [pa, pb) of elements equal to v, elements
+  // smaller before, larger after (used by tr_partition and the introsort bodies).
+  void three_way(const i32* ISAd, i32* first, i32* last, i32 v, i32** pa, i32** pb, i32** pb_raw, i32** pc_raw,
+                 i32** pa_raw, i32** pd_raw) const {
+    i32 *a, *b, *c, *d;
+    i32 x = 0;
+    for (b = first - 1; ++b < last && (x = at(ISAd, *b)) == v;) {
+    }
+    if ((a = b) < last && x < v) {
+      for (; ++b < last && (x = at(ISAd, *b)) <= v;)
+        if (x == v) {
+          swp(*b, *a);
+          ++a;
+        }
+    }
+    for (c = last; b < --c && (x = at(ISAd, *c)) == v;) {
+    }
+    if (b < (d = c) && x > v) {
+      for (; b < --c && (x = at(ISAd, *c)) >= v;)
+        if (x == v) {
+          swp(*c, *d);
+          --d;
+        }
+    }
+    for (; b < c;) {
+      swp(*b, *c);
+      for (; ++b < c && (x = at(ISAd, *b)) <= v;)
+        if (x == v) {
+          swp(*b, *a);
+          ++a;
+        }
+      for (; b < --c && (x = at(ISAd, *c)) >= v;)
+        if (x == v) {
+          swp(*c, *d);
+          --d;
+        }
+    }
+    *pa_raw = a;
+    *pb_raw = b;
+    *pc_raw = c;
+    *pd_raw = d;
+    (void)pa;
+    (void)pb;
+  }
+
+  // tr_partition (blocksort.c:964-1004): partition starting at first (no pivot swap)
+  void part(const i32* ISAd, i32* first, i32* last, i32** pa, i32** pb, i32 v) const {
+    i32 *a, *b, *c, *d;
+    three_way(ISAd, first, last, v, nullptr, nullptr, &b, &c, &a, &d);
+    if (a <= d) {
+      c = b - 1;
+      i64 s, t;
+      if ((s = a - first) > (t = b - a)) s = t;
+      for (i32 *e = first, *f = b - s; 0 < s; --s, ++e, ++f) swp(*e, *f);
+      if ((s = d - c) > (t = last - d - 1)) s = t;
+      for (i32 *e = b, *f = last - s; 0 < s; --s, ++e, ++f) swp(*e, *f);
+      first += (b - a), last -= (d - c);
+    }
+    *pa = first, *pb = last;
+  }
+
+  // tr_copy (blocksort.c:1006-1029)
+  void copy(i32* first, i32* a, i32* b, i32* last, i32 depth) const {
+    const i32 v = (i32)(b - SA - 1);
+    i32 *c, *d, *e;
+    i32 s;
+    for (c = first, d = a - 1; c <= d; ++c) {
+      if ((s = *c - depth) < 0) s += (i32)(ISAn - ISA);
+      if (ISA[s] == v) {
+        *++d = s;
+        ISA[s] = (i32)(d - SA);
+      }
+    }
+    for (c = last - 1, e = d + 1, d = b; e < d; --c) {
+      if ((s = *c - depth) < 0) s += (i32)(ISAn - ISA);
+      if (ISA[s] == v) {
+        *--d = s;
+        ISA[s] = (i32)(d - SA);
+      }
+    }
+  }
+
+  struct Fr {
+    const i32* a;
+    i32 *b, *c;
+    i32 d;
+  };
+
+  // tr_introsort (blocksort.c:1031-1281).  The budget is only charged here: the reference's
+  // UPDATE_BUDGET 'break' leaves its own do{}while(0), so the check happens in trsort.
+  void introsort(const i32* ISAd, i32* first, i32* last, i32* budget) {
+    Stack<Fr> st;
+    i32 *a, *b, *c;
+    i32 v, x = 0, limit, next;
+    i64 s, tt;
+    auto pop = [&](const i32*& I, i32*& f, i32*& l, i32& lim) -> bool {
+      Fr fr;
+      if (!st.pop(fr)) return false;
+      I = fr.a, f = fr.b, l = fr.c, lim = fr.d;
+      return true;
+    };
+    for (limit = lg_tr((i32)(last - first));;) {
+      if (limit < 0) {
+        if (limit == -1) {
+          i32 *pa, *pb;
+          part(ISAd - 1, first, last, &pa, &pb, (i32)(last - SA - 1));
+          a = pa, b = pb;
+          if (first < a || b < last) {
+            if (a < last)
+              for (c = first, v = (i32)(a - SA - 1); c < a; ++c) ISA[*c] = v;
+            if (b < last)
+              for (c = a, v = (i32)(b - SA - 1); c < b; ++c) ISA[*c] = v;
+            if (1 < b - a) {
+              st.push({nullptr, a, b, 0});
+              st.push({ISAd - 1, first, last, -2});
+            }
+            if (a - first <= last - b) {
+              if (1 < a - first) {
+                st.push({ISAd, b, last, lg_tr((i32)(last - b))});
+                last = a, limit = lg_tr((i32)(a - first));
+              } else if (1 < last - b) {
+                first = b, limit = lg_tr((i32)(last - b));
+              } else if (!pop(ISAd, first, last, limit)) {
+                return;
+              }
+            } else {
+              if (1 < last - b) {
+                st.push({ISAd, first, a, lg_tr((i32)(a - first))});
+                first = b, limit = lg_tr((i32)(last - b));
+              } else if (1 < a - first) {
+                last = a, limit = lg_tr((i32)(a - first));
+              } else if (!pop(ISAd, first, last, limit)) {
+                return;
+              }
+            }
+          } else {
+            for (c = first; c < last; ++c) ISA[*c] = (i32)(c - SA);
+            if (!pop(ISAd, first, last, limit)) return;
+          }
+        } else if (limit == -2) {
+          Fr fr = st.v.back();
+          st.v.pop_back();
+          a = fr.b, b = fr.c;
+          copy(first, a, b, last, (i32)(ISAd - ISA));
+          if (!pop(ISAd, first, last, limit)) return;
+        } else {
+          if (0 <= *first) {
+            a = first;
+            do {
+              ISA[*a] = (i32)(a - SA);
+            } while (++a < last && 0 <= *a);
+            first = a;
+          }
+          if (first < last) {
+            a = first;
+            do {
+              *a = ~*a;
+            } while (*++a < 0);
+            b = a;
+            a = b + 1;
+            next = (ISA[*b] != at(ISAd, *b)) ? lg_tr((i32)(a - first)) : -1;
+            if (a < last)
+              for (c = first, v = (i32)(a - SA - 1); c < a; ++c) ISA[*c] = v;
+            if (a - first <= last - a) {
+              st.push({ISAd, a, last, -3});
+              ISAd += 1, last = a, limit = next;
+            } else {
+              if (1 < last - a) {
+                st.push({ISAd + 1, first, a, next});
+                first = a, limit = -3;
+              } else {
+                ISAd += 1, last = a, limit = next;
+              }
+            }
+          } else if (!pop(ISAd, first, last, limit)) {
+            return;
+          }
+        }
+        continue;
+      }
+
+      if (last - first <= kInsertion) {
+        *budget -= (i32)(last - first);
+        insertion(ISAd, first, last);
+        for (;;) {
+          if (0 <= *first) {
+            a = first;
+            do {
+              ISA[*a] = (i32)(a - SA);
+            } while (++a < last && 0 <= *a);
+            first = a;
+          }
+          if (first < last) {
+            a = first;
+            do {
+              *a = ~*a;
+            } while (*++a < 0);
+            b = a;
+            a = b + 1;
+            if (ISA[*b] == at(ISAd, *b)) limit = -1;
+            if (a < last)
+              for (c = first, v = (i32)(a - SA - 1); c < a; ++c) ISA[*c] = v;
+            if (1 < last - a) st.push({ISAd, a, last, -4});
+            ISAd += 1, last = a;
+            if (limit == -1) break;
+            *budget -= (i32)(last - first);
+            insertion(ISAd, first, last);
+          } else {
+            if (!pop(ISAd, first, last, limit)) return;
+            if (limit != -4) break;
+          }
+        }
+        continue;
+      }
+
+      if (limit-- == 0) {
+        *budget -= (i32)(last - first);
+        heapsort(ISAd, first, (i32)(last - first));
+        for (a = last - 2, v = at(ISAd, *(last - 1)); first <= a; --a) {
+          if ((x = at(ISAd, *a)) == v) *a = ~*a;
+          else v = x;
+        }
+        limit = -3;
+        continue;
+      }
+
+      a = pivot(ISAd, first, last);
+      swp(*first, *a);
+      v = at(ISAd, *first);
+      i32 *qa, *qb, *qc, *qd;
+      three_way(ISAd, first + 1, last, v, nullptr, nullptr, &qb, &qc, &qa, &qd);
+      if (qa <= qd) {
+        c = qb - 1;
+        if ((s = qa - first) > (tt = qb - qa)) s = tt;
+        for (i32 *e = first, *f = qb - s; 0 < s; --s, ++e, ++f) swp(*e, *f);
+        if ((s = qd - c) > (tt = last - qd - 1)) s = tt;
+        for (i32 *e = qb, *f = last - s; 0 < s; --s, ++e, ++f) swp(*e, *f);
+        a = first + (qb - qa), b = last - (qd - c);
+        next = (ISA[*a] == at(ISAd, *a)) ? -1 : lg_tr((i32)(b - a));
+        for (c = first, v = (i32)(a - SA - 1); c < a; ++c) ISA[*c] = v;
+        if (b < last)
+          for (c = a, v = (i32)(b - SA - 1); c < b; ++c) ISA[*c] = v;
+        *budget -= (i32)(last - first);
+        if (a - first <= last - b) {
+          if (last - b <= b - a) {
+            if (1 < a - first) {
+              st.push({ISAd + 1, a, b, next});
+              st.push({ISAd, b, last, limit});
+              last = a;
+            } else if (1 < last - b) {
+              st.push({ISAd + 1, a, b, next});
+              first = b;
+            } else if (1 < b - a) {
+              ISAd += 1, first = a, last = b, limit = next;
+            } else if (!pop(ISAd, first, last, limit)) {
+              return;
+            }
+          } else if (a - first <= b - a) {
+            if (1 < a - first) {
+              st.push({ISAd, b, last, limit});
+              st.push({ISAd + 1, a, b, next});
+              last = a;
+            } else if (1 < b - a) {
+              st.push({ISAd, b, last, limit});
+              ISAd += 1, first = a, last = b, limit = next;
+            } else {
+              first = b;
+            }
+          } else {
+            if (1 < b - a) {
+              st.push({ISAd, b, last, limit});
+              st.push({ISAd, first, a, limit});
+              ISAd += 1, first = a, last = b, limit = next;
+            } else {
+              st.push({ISAd, b, last, limit});
+              last = a;
+            }
+          }
+        } else {
+          if (a - first <= b - a) {
+            if (1 < last - b) {
+              st.push({ISAd + 1, a, b, next});
+              st.push({ISAd, first, a, limit});
+              first = b;
+            } else if (1 < a - first) {
+              st.push({ISAd + 1, a, b, next});
+              last = a;
+            } else if (1 < b - a) {
+              ISAd += 1, first = a, last = b, limit = next;
+            } else if (!pop(ISAd, first, last, limit)) {
+              return;
+            }
+          } else if (last - b <= b - a) {
+            if (1 < last - b) {
+              st.push({ISAd, first, a, limit});
+              st.push({ISAd + 1, a, b, next});
+              first = b;
+            } else if (1 < b - a) {
+              st.push({ISAd, first, a, limit});
+              ISAd += 1, first = a, last = b, limit = next;
+            } else {
+              last = a;
+            }
+          } else {
+            if (1 < b - a) {
+              st.push({ISAd, first, a, limit});
+              st.push({ISAd, b, last, limit});
+              ISAd += 1, first = a, last = b, limit = next;
+            } else {
+              st.push({ISAd, first, a, limit});
+              first = b;
+            }
+          }
+        }
+      } else {
+        limit = (ISA[*first] == at(ISAd, *first)) ? -1 : (limit + 1);
+        ISAd += 1;
+        *budget -= (i32)(last - first);
+      }
+    }
+  }
+
+  // ls_updategroup (blocksort.c:812-831)
+  void ls_update(i32* first, i32* last) const {
+    for (i32* a = first; a < last; ++a) {
+      if (0 <= *a) {
+        i32* b = a;
+        do {
+          ISA[*a] = (i32)(a - SA);
+        } while (++a < last && 0 <= *a);
+        *b = (i32)(b - a);
+        if (last <= a) break;
+      }
+      i32* b = a;
+      do {
+        *a = ~*a;
+      } while (*++a < 0);
+      const i32 t = (i32)(a - SA);
+      do {
+        ISA[*b] = t;
+      } while (++b <= a);
+    }
+  }
+
+  struct LsFr {
+    i32 *a, *b;
+    i32 c;
+  };
+
+  // ls_introsort (blocksort.c:833-924)
+  void ls_intro(const i32* ISAd, i32* first, i32* last) {
+    Stack<LsFr> st;
+    i32 *a, *b, *c;
+    i32 v, x = 0, limit;
+    i64 s, t;
+    auto pop = [&](i32*& f, i32*& l, i32& lim) -> bool {
+      LsFr fr;
+      if (!st.pop(fr)) return false;
+      f = fr.a, l = fr.b, lim = fr.c;
+      return true;
+    };
+    for (limit = lg_tr((i32)(last - first));;) {
+      if (last - first <= kInsertion) {
+        if (1 < last - first) {
+          insertion(ISAd, first, last);
+          ls_update(first, last);
+        } else if (last - first == 1) {
+          *first = -1;
+        }
+        if (!pop(first, last, limit)) return;
+        continue;
+      }
+      if (limit-- == 0) {
+        heapsort(ISAd, first, (i32)(last - first));
+        for (a = last - 2, v = at(ISAd, *(last - 1)); first <= a; --a) {
+          if ((x = at(ISAd, *a)) == v) *a = ~*a;
+          else v = x;
+        }
+        ls_update(first, last);
+        if (!pop(first, last, limit)) return;
+        continue;
+      }
+      a = pivot(ISAd, first, last);
+      swp(*first, *a);
+      v = at(ISAd, *first);
+      i32 *qa, *qb, *qc, *qd;
+      three_way(ISAd, first + 1, last, v, nullptr, nullptr, &qb, &qc, &qa, &qd);
+      if (qa <= qd) {
+        c = qb - 1;
+        if ((s = qa - first) > (t = qb - qa)) s = t;
+        for (i32 *e = first, *f = qb - s; 0 < s; --s, ++e, ++f) swp(*e, *f);
+        if ((s = qd - c) > (t = last - qd - 1)) s = t;
+        for (i32 *e = qb, *f = last - s; 0 < s; --s, ++e, ++f) swp(*e, *f);
+        a = first + (qb - qa), b = last - (qd - c);
+        for (c = first, v = (i32)(a - SA - 1); c < a; ++c) ISA[*c] = v;
+        if (b < last)
+          for (c = a, v = (i32)(b - SA - 1); c < b; ++c) ISA[*c] = v;
+        if (b - a == 1) *a = -1;
+        if (a - first <= last - b) {
+          if (first < a) {
+            st.push({b, last, limit});
+            last = a;
+          } else {
+            first = b;
+          }
+        } else {
+          if (b < last) {
+            st.push({first, a, limit});
+            first = b;
+          } else {
+            last = a;
+          }
+        }
+      } else {
+        if (!pop(first, last, limit)) return;
+      }
+    }
+  }
+
+  // lssort (blocksort.c:926-959)
+  void lssort(i32 n, i32 depth) {
+    const i32* ISAd;
+    i32 *first, *last, *i;
+    i32 t, skip;
+    for (ISAd = ISA + depth; -n < *SA; ISAd += (ISAd - ISA)) {
+      first = SA;
+      skip = 0;
+      do {
+        if ((t = *first) < 0) {
+          first -= t;
+          skip += t;
+        } else {
+          if (skip != 0) {
+            *(first + skip) = skip;
+            skip = 0;
+          }
+          last = SA + ISA[t] + 1;
+          ls_intro(ISAd, first, last);
+          first = last;
+        }
+      } while (first < SA + n);
+      if (skip != 0) *(first + skip) = skip;
+      if (n < (ISAd - ISA)) {
+        first = SA;
+        do {
+          if ((t = *first) < 0) {
+            first -= t;
+          } else {
+            last = SA + ISA[t] + 1;
+            for (i = first; i < last; ++i) ISA[*i] = (i32)(i - SA);
+            first = last;
+          }
+        } while (first < SA + n);
+        break;
+      }
+    }
+  }
+
+  // trsort (blocksort.c:1283-1309)
+  void trsort(i32 n, i32 depth) {
+    if (-n < *SA) {
+      i32* first = SA;
+      i32 budget = (lg_tr(n) * 2 / 3 + 1) * n;
+      do {
+        const i32 t = *first;
+        if (t < 0) {
+          first -= t;
+        } else {
+          i32* last = SA + ISA[t] + 1;
+          introsort(ISA + depth, first, last, &budget);
+          first = last;
+          if (budget <= 0) {
+            *SA = -(i32)(first - SA);
+            lssort(n, depth);
+            break;
+          }
+        }
+      } while (first < SA + n);
+    }
+  }
+};
+
+// ====================================================================== driver
+struct Cyclic {
+  std::vector<u8> tbuf;
+  const u8* T = nullptr;
+  i32 n = 0;
+  std::vector<i32> sa;
+  i32 bucketA[256];
+  std::vector<i32> bucketB;
+
+  i32& BA(int c) { return bucketA[c]; }
+  i32& BB(int c0, int c1) { return bucketB[(c1 << 8) + c0]; }
+  i32& BS(int c0, int c1) { return bucketB[(c0 << 8) + c1]; }
+
+  // sort_typeBstar (blocksort.c:1314-1437); returns m, the number of B* suffixes
+  i32 typeBstar() {
+    i32* SA = sa.data();
+    i32 tempbuf[256];
+    for (int i = 0; i < 256; i++) bucketA[i] = 0;
+    std::fill(bucketB.begin(), bucketB.end(), 0);
+    int c0, c1;
+    i64 i, j, k, t, m;
+    i32 flag;
+    for (i = 1, c1 = T[0]; i < n && T[i] == (u8)c1; ++i) {
+    }
+    flag = (u8)c1 <= T[i];
+    i = n - 1, m = n;
+    if ((c0 = T[i]) < c1 || (c0 == c1 && flag != 0)) {
+      if (flag == 0) {
+        ++BS(c0, c1);
+        SA[--m] = (i32)i;
+      } else {
+        ++BB(c0, c1);
+      }
+      for (; c1 = c0, 0 <= --i && (c0 = T[i]) <= c1;) ++BB(c0, c1);
+    }
+    while (0 <= i) {
+      do {
+        ++BA(c0);
+        c1 = c0;
+      } while (0 <= --i && (c0 = T[i]) >= c1);
+      if (0 <= i) {
+        ++BS(c0, c1);
+        SA[--m] = (i32)i;
+        for (; c1 = c0, 0 <= --i && (c0 = T[i]) <= c1;) ++BB(c0, c1);
+      }
+    }
+    m = n - m;
+    if (m == 0) {
+      for (i = 0, c0 = T[0]; i < n; ++i) SA[i] = c0;
+      return 0;
+    }
+    for (c0 = 0, i = -1, j = 0; c0 < 256; ++c0) {
+      t = i + BA(c0);
+      BA(c0) = (i32)(i + j);
+      i = t + BB(c0, c0);
+      for (c1 = c0 + 1; c1 < 256; ++c1) {
+        j += BS(c0, c1);
+        BS(c0, c1) = (i32)j;
+        i += BB(c0, c1);
+      }
+    }
+    i32* PAb = SA + n - m;
+    for (i = m - 2; 0 <= i; --i) {
+      t = PAb[i], c0 = T[t], c1 = T[t + 1];
+      SA[--BS(c0, c1)] = (i32)i;
+    }
+    t = PAb[m - 1], c0 = T[t], c1 = T[t + 1];
+    SA[--BS(c0, c1)] = (i32)(m - 1);
+
+    flag = -1;
+    if (3 * m > n) flag = SA[2 * m - 1];
+
+    i32* buf = SA + m;
+    i64 bufsize = n - (2 * m);
+    if (bufsize <= 256) buf = tempbuf, bufsize = 256;
+    SubstringSorter ss{T + 2, PAb};  // the substring sort runs on T+2 (blocksort.c:1321)
+    for (c0 = 255, j = m; 0 < j; --c0) {
+      for (c1 = 255; c0 < c1; j = i, --c1) {
+        i = BS(c0, c1);
+        if (1 < j - i) ss.run(SA + i, SA + j, buf, bufsize, *(SA + i) == (m - 1), n);
+      }
+    }
+
+    i32* ISAb = SA + m;
+    for (i = m - 1; 0 <= i; --i) {
+      if (0 <= (t = SA[i])) {
+        j = i;
+        do {
+          ISAb[t] = (i32)i;
+        } while (0 <= --i && 0 <= (t = SA[i]));
+        SA[i + 1] = (i32)(i - j);
+        if (i <= 0) break;
+      }
+      j = i;
+      do {
+        ISAb[SA[i] = (i32)~t] = (i32)j;
+      } while ((t = SA[--i]) < 0);
+      ISAb[t] = (i32)j;
+    }
+
+    TandemSorter tr{ISAb, ISAb + m, SA};
+    tr.trsort((i32)m, 1);
+
+    if (flag < 0) {
+      for (j = m - 1, k = n - 1; j >= 0; k--, j--) {
+        i = SA[k];
+        SA[ISAb[j]] = (T[i - 1] > T[i] ? ~(i32)i : (i32)i);
+      }
+    } else {
+      for (j = m - 1, k = n - 1, t = 2 * m; k >= t; j--, k--) {
+        i = SA[k];
+        SA[ISAb[j]] = (T[i - 1] > T[i] ? ~(i32)i : (i32)i);
+      }
+      for (i = flag; j > 0; j--) {
+        SA[ISAb[j]] = (T[i - 1] > T[i] ? ~(i32)i : (i32)i);
+        do {
+          --i;
+        } while (T[i] <= T[i + 1]);
+        do {
+          --i;
+        } while (T[i] >= T[i + 1]);
+      }
+      SA[ISAb[j]] = (T[i - 1] > T[i] ? ~(i32)i : (i32)i);
+    }
+
+    BB(255, 255) = n;
+    for (c0 = 254, i = n - 1, k = m - 1; 0 <= c0; --c0) {
+      i = BA(c0 + 1);
+      for (c1 = 255; c0 < c1; --c1) {
+        t = i - BB(c0, c1);
+        BB(c0, c1) = (i32)(i + 1);
+        for (i = t, j = BS(c0, c1); j <= k; --i, --k) SA[i] = SA[k];
+      }
+      BS(c0, c0 + 1) = (i32)(i - BB(c0, c0) + 1);
+      BB(c0, c0) = (i32)(i + 1);
+    }
+    return (i32)m;
+  }
+
+  // construct_SA (blocksort.c:1439-1501): induced sort, returns origPtr
+  i32 induce() {
+    i32* SA = sa.data();
+    i32 *i, *j, *t;
+    i64 s, c2;
+    int c0, c1;
+    i32 orig = -1;
+    for (c1 = 254; 0 <= c1; --c1) {
+      for (i = SA + BS(c1, c1 + 1), j = SA + BB(c1, 255) - 1, t = SA + BB(c2 = 0, c1); i <= j; --j) {
+        if (0 <= (s = *j)) {
+          if (--s < 0) {
+            s = n - 1;
+            orig = (i32)(j - SA);
+          }
+          c0 = T[s];
+          if (T[s - 1] > (u8)c0) s = ~s;
+          if (c2 != c0) {
+            BB((int)c2, c1) = (i32)(t - SA);
+            t = SA + BB((int)(c2 = c0), c1);
+          }
+          *j = c0;
+          *--t = (i32)s;
+        }
+      }
+    }
+    t = SA + BA((int)(c2 = 255));
+    for (i = SA, j = SA + n; i < j; ++i) {
+      if (0 > (s = *i)) {
+        s = ~s;
+        if (--s < 0) {
+          s = n - 1;
+          orig = (i32)(i - SA);
+        }
+        c0 = T[s];
+        c1 = T[s - 1];
+        *i = c0;
+        if (c0 != c2) {
+          BA((int)c2) = (i32)(t - SA);
+          t = SA + BA((int)(c2 = c0));
+        }
+        if (c1 >= c0) {
+          s = ~s;
+        } else {
+          if (s == 0) orig = (i32)(t - SA + 1);
+          s = c1;
+        }
+        *++t = (i32)s;
+      }
+    }
+    return orig;
+  }
+
+  i32 run(const u8* blk, i32 len) {
+    n = len;
+    if (n == 1) return 0;
+    tbuf.assign((size_t)n + 2, 0);
+    std::memcpy(tbuf.data() + 1, blk, (size_t)n);
+    tbuf[0] = blk[n - 1];  // block[-1] = block[n-1]  (blocksort.c:1541)
+    tbuf[(size_t)n + 1] = blk[0];  // block[n] = block[0]  (blocksort.c:1540)
+    T = tbuf.data() + 1;
+    sa.assign((size_t)n + 2, 0);
+    bucketB.assign(65536, 0);
+    const i32 m = typeBstar();
+    if (0 < m) return induce();
+    return 0;
+  }
+};
+
+}  // namespace a5
+
 int32_t periodic_origptr(const uint8_t* blk, int32_t n) {
-  (void)blk;
-  (void)n;
-  throw ResolverFailure();  // A5 tie order not implemented yet
+  a5::Cyclic c;
+  const int32_t o = c.run(blk, n);
+  if (o < 0) throw ResolverFailure();
+  return o;
 }
 
 void resolve_origptrs(const uint8_t* d_blk, const std::vector<uint32_t>& boff, const std::vector<uint32_t>& period,
                       std::vector<uint32_t>& rank) {
   const size_t nb = rank.size();
-  std::map<std::string, int32_t> memo;  // identical periodic blocks resolve once
+  static std::map<std::string, int32_t> memo;  // identical periodic blocks resolve once per process
   for (size_t b = 0; b < nb; b++) {
     const uint32_t n = boff[b + 1] - boff[b], p = period[b];
     const uint32_t k = n / p;
-    if (k == 1) continue;                // aperiodic: the rank is the origPtr
-    if (p == 1) { rank[b] = 0; continue; }  // one symbol: no B* suffix, origPtr 0 (blocksort.c:1349)
+    if (k == 1) continue;                   // aperiodic: the rank is the origPtr
+    if (p == 1) {                           // one symbol: no B* suffix, origPtr 0 (blocksort.c:1349)
+      rank[b] = 0;
+      continue;
+    }
     std::string bytes(n, '\0');
     if (hipMemcpy(&bytes[0], d_blk + boff[b], n, hipMemcpyDeviceToHost) != hipSuccess) throw ResolverFailure();
     auto it = memo.find(bytes);
-    if (it == memo.end()) it = memo.emplace(bytes, periodic_origptr((const uint8_t*)bytes.data(), (int32_t)n)).first;
+    if (it == memo.end()) {
+      if (memo.size() > 64) memo.clear();
+      it = memo.emplace(bytes, periodic_origptr((const uint8_t*)bytes.data(), (int32_t)n)).first;
+    }
     rank[b] = (uint32_t)it->second;
   }
 }

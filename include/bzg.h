@@ -67,6 +67,11 @@ int bzg_stage_bwt(const uint8_t *blocks, const uint32_t *offsets, uint32_t nbloc
 int bzg_stage_mtf(const uint8_t *bwt, const uint32_t *offsets, uint32_t nblocks, uint16_t *mtfv,
                   uint32_t *mtf_offsets, uint32_t *nmtf, uint32_t *freq);
 
+/* origPtr the reference assigns to one exactly periodic block w^k (SURVEY.md 8a row A5;
+ * host-side replay of the reference's divsufsort tie order, bzip2_amd/csrc/resolver.cpp).
+ * Returns -1 on failure.  Needs no GPU. */
+int32_t bzg_periodic_origptr(const uint8_t *block, int32_t n);
+
 /* Timing of the last bzg_compress_device call, per stage, from HIP events (ms). */
 typedef struct {
   float rle1_ms, bwt_ms, mtf_ms, code_ms, total_ms;

@@ -9,6 +9,7 @@ import subprocess
 import pytest
 
 import bzip2_amd
+import bzip2_amd as B
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -107,3 +108,21 @@ def test_decoder_streaming_small_chunks(lib):
     L.BZ2_bzDecompressEnd(ctypes.byref(strm))
     assert bytes(out) == plain
     assert tail[pos:] == b"TRAILING"  # input consumed exactly to the end of the stream
+
+
+def test_periodic_resolver_matches_reference(lib):
+    """A5: origPtr of exactly periodic blocks replays the reference's divsufsort tie order."""
+    from tests import oracles as O
+    if not O.has_ref():
+        pytest.skip("oracle/_ref not built")
+    import random
+    rng = random.Random(5)
+    cases = [b"abc" * k for k in (2, 8, 16, 17, 100, 255, 256, 257, 1000, 4096)]
+    cases += [b"abcabcabd" * k for k in (2, 8, 255, 1000)]
+    cases += [b"bababac" * k for k in (16, 100, 256)]
+    cases += [bytes([c] * 4 + [0xFB]) * 19997 for c in (0x00, 0x61, 0xFB, 0xFF)]
+    for _ in range(200):
+        w = bytes(rng.randrange(rng.choice([2, 4, 256])) for _ in range(rng.randint(1, 40)))
+        cases.append(w * rng.randint(2, 300))
+    for blk in cases:
+        assert B.periodic_origptr(blk) == O.ref_blocksort(blk)[1], (blk[:12], len(blk))

@@ -175,6 +175,19 @@ def test_edge_streams(data):
         assert B.buff_to_buff_compress(data, level) == expected(data, level)
 
 
+@pytest.mark.parametrize("c", [0x00, 0x61, 0xFB, 0xFF])
+def test_single_byte_periodic_blocks(c):
+    """Config 4 shape at -1: full blocks are (c c c c 0xFB)^k, exactly periodic (A5)."""
+    data = bytes([c]) * 6_000_000
+    assert B.buff_to_buff_compress(data, 1) == expected(data, 1)
+
+
+def test_periodic_text_blocks():
+    w = datagen.text(3_001, 99)
+    for data in (w * 300, b"abcabcabd" * 120_000, b"ab" * 500_000):
+        assert B.buff_to_buff_compress(data, 2) == expected(data, 2)
+
+
 def test_single_byte_aperiodic_tail():
     # one symbol per block: period-1 blocks take origPtr 0 (blocksort.c:1349)
     for c in (0x00, 0xFB):
