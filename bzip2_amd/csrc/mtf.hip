@@ -20,6 +20,35 @@ constexpr uint32_t kChunk = 1024;
 
 __device__ __forceinline__ uint32_t nsym(uint32_t z) { return z ? 31u - (uint32_t)__builtin_clz(z + 1) : 0u; }
 
+// Visits bytes [lo, hi) of p with aligned 16-byte loads (buffers carry >= 16 B of padding),
+// forwards or backwards.  f(i, byte).
+template <bool kForward, typename F>
+__device__ __forceinline__ void for_bytes(const uint8_t* __restrict__ p, uint32_t lo, uint32_t hi, F f) {
+  if (lo >= hi) return;
+  if (kForward) {
+    for (uint32_t a = lo & ~15u; a < hi; a += 16) {
+      const uint4 q = *reinterpret_cast<const uint4*>(p + a);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const uint32_t i = a + k;
+        if (i >= lo && i < hi) f(i, (w[k >> 2] >> (8 * (k & 3))) & 0xffu);
+      }
+    }
+  } else {
+    for (uint32_t a = (hi - 1) & ~15u;; a -= 16) {
+      const uint4 q = *reinterpret_cast<const uint4*>(p + a);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 15; k >= 0; k--) {
+        const uint32_t i = a + k;
+        if (i >= lo && i < hi) f(i, (w[k >> 2] >> (8 * (k & 3))) & 0xffu);
+      }
+      if (a <= lo) break;
+    }
+  }
+}
+
 // chunk geometry: block b = blockIdx.y, chunk c = blockIdx.x*kT + threadIdx.x
 struct ChunkRef {
   bool valid;
@@ -48,15 +77,14 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
   if (!r.valid) return;
   uint8_t* out = sig + (size_t)r.gidx * 256;
   uint32_t cnt = 0;
-  for (uint32_t i = r.hi; i > r.lo; i--) {
-    const uint32_t c = L[i - 1];
+  for_bytes<false>(L, r.lo, r.hi, [&](uint32_t, uint32_t c) {
     const uint32_t bit = 1u << (c & 31);
-    uint32_t w = seen[c >> 5][threadIdx.x];
+    const uint32_t w = seen[c >> 5][threadIdx.x];
     if (!(w & bit)) {
       seen[c >> 5][threadIdx.x] = w | bit;
       out[cnt++] = (uint8_t)c;
     }
-  }
+  });
   siglen[r.gidx] = cnt;
 }
 
@@ -129,8 +157,8 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
   const uint32_t t = threadIdx.x;
   const uint32_t* src = init + (size_t)r.gidx * 64;
   for (int w = 0; w < 64; w++) lst[w][t] = src[w];
-  for (uint32_t i = r.lo; i < r.hi; i++) {
-    const uint32_t c = L[i];
+  uint32_t racc = 0;  // 4 ranks packed, stored as one word when aligned
+  for_bytes<true>(L, r.lo, r.hi, [&](uint32_t i, uint32_t c) {
     const uint32_t pat = c * 0x01010101u;
     // find word and byte of c
     uint32_t w = 0, x = 0;
@@ -148,8 +176,16 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
     }
     const uint32_t k = (uint32_t)__builtin_ctz(x) >> 3;  // byte within word
     const uint32_t pos = w * 4 + k;
-    ranks[i] = (uint8_t)pos;
-    if (pos == 0) continue;
+    racc |= pos << (8 * (i & 3));
+    if ((i & 3) == 3 || i + 1 == r.hi) {
+      if ((i & 3) == 3 && i >= r.lo + 3) {
+        *reinterpret_cast<uint32_t*>(ranks + i - 3) = racc;
+      } else {
+        for (uint32_t q = (i & ~3u) > r.lo ? (i & ~3u) : r.lo; q <= i; q++) ranks[q] = (uint8_t)(racc >> (8 * (q & 3)));
+      }
+      racc = 0;
+    }
+    if (pos == 0) return;
     // shift positions [0, pos) up by one and put c at 0
     uint32_t carry = c;
     for (uint32_t q = 0; q < w; q++) {
@@ -160,7 +196,7 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
     const uint32_t v = lst[w][t];
     const uint32_t lowmask = (k == 3) ? 0xffffffffu : ((1u << (8 * (k + 1))) - 1u);  // bytes 0..k
     lst[w][t] = (v & ~lowmask) | (((v << 8) | carry) & lowmask);
-  }
+  });
 }
 
 // 4a. per-chunk zero-run summary
@@ -171,8 +207,7 @@ __global__ void __launch_bounds__(kT) k_rle2_count(const uint8_t* __restrict__ r
   if (!r.valid) return;
   uint32_t ld = 0, z = 0, cnt = 0;
   bool seen = false;
-  for (uint32_t i = r.lo; i < r.hi; i++) {
-    const uint32_t v = ranks[i];
+  for_bytes<true>(ranks, r.lo, r.hi, [&](uint32_t, uint32_t v) {
     if (v == 0) {
       z++;
     } else {
@@ -185,7 +220,7 @@ __global__ void __launch_bounds__(kT) k_rle2_count(const uint8_t* __restrict__ r
       z = 0;
       cnt++;
     }
-  }
+  });
   lead[r.gidx] = seen ? ld : 0xffffffffu;  // all-zero chunk marker
   trail[r.gidx] = z;
   inner[r.gidx] = cnt;
@@ -245,18 +280,18 @@ __global__ void __launch_bounds__(kT) k_rle2_emit(const uint8_t* __restrict__ ra
         zz >>= 1;
       }
     };
-    for (uint32_t i = r.lo; i < r.hi; i++) {
-      const uint32_t v = ranks[i];
+    const uint32_t z_in = zin[r.gidx];
+    for_bytes<true>(ranks, r.lo, r.hi, [&](uint32_t, uint32_t v) {
       if (v == 0) {
         z++;
-        continue;
+        return;
       }
-      put_run(seen ? z : zin[r.gidx]);
+      put_run(seen ? z : z_in);
       seen = true;
       z = 0;
       out[o++] = (uint16_t)(v + 1);
       atomicAdd(&hist[v + 1], 1u);
-    }
+    });
     const uint32_t n = boff[r.b + 1] - boff[r.b];
     if ((r.c + 1) * kChunk >= n) {  // last chunk: final run + EOB
       put_run(finalrun[r.b]);

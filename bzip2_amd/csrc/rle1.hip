@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
                                              const uint32_t* __restrict__ carry,
                                              const uint32_t* __restrict__ out_base,
                                              uint8_t* __restrict__ out, uint32_t* __restrict__ cbits,
-                                             uint32_t* __restrict__ cinpos, uint32_t* __restrict__ last_len1) {
+                                             uint32_t* __restrict__ last_len1) {
   __shared__ uint32_t sh[kT / 64];
   __shared__ uint32_t thr[kT];
   const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
@@ -133,6 +133,9 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
   for (int k = 0; k < kPer; k++) s += bi[k].e;
   uint32_t incl = block_incl_sum(s, sh, (uint32_t*)nullptr);
   uint32_t pos = out_base[blockIdx.x] + incl - s;
+  // chunk-start bits of this thread's outputs span <= 2 words (<= 32 output bytes)
+  const uint32_t w0 = pos >> 5;
+  uint32_t bits0 = 0, bits1 = 0;
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const uint64_t i = base + k;
@@ -140,8 +143,9 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
     const ByteInfo b = bi[k];
     if (i + 1 == n) *last_len1 = (b.r == 0) ? 1u : 0u;
     if (b.r == 0) {
-      atomicOr(&cbits[pos >> 5], 1u << (pos & 31));
-      cinpos[pos] = (uint32_t)i;
+      const uint32_t w = pos >> 5;
+      if (w == w0) bits0 |= 1u << (pos & 31);
+      else bits1 |= 1u << (pos & 31);
     }
     if (b.r <= 3) {
       out[pos] = v[k];
@@ -150,6 +154,45 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
       out[pos] = (uint8_t)(b.r - 3);
     }
     pos += b.e;
+  }
+  if (bits0) atomicOr(&cbits[w0], bits0);
+  if (bits1) atomicOr(&cbits[w0 + 1], bits1);
+}
+
+// Input offset of the chunk whose first output byte is p (p a chunk start), by re-deriving
+// the byte info of the one RLE tile that produced p.  One workgroup per queried boundary.
+__global__ void __launch_bounds__(kT) k_chunk_inpos(const uint8_t* __restrict__ x, uint64_t n,
+                                                    const uint32_t* __restrict__ carry,
+                                                    const uint32_t* __restrict__ out_base, uint32_t ntiles,
+                                                    const uint32_t* __restrict__ qpos, uint32_t nq,
+                                                    uint32_t* __restrict__ inpos) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t thr[kT];
+  const uint32_t q = blockIdx.x;
+  if (q >= nq) return;
+  const uint32_t p = qpos[q];
+  // tile whose output range contains p: largest t with out_base[t] <= p
+  uint32_t lo = 0, hi = ntiles;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (out_base[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  const uint64_t base = (uint64_t)lo * kTile + (uint64_t)threadIdx.x * kPer;
+  uint8_t v[kPer];
+  load16(x, n, base, v);
+  ByteInfo bi[kPer];
+  byte_info(x, n, base, v, carry[lo], sh, thr, bi);
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) s += bi[k].e;
+  uint32_t incl = block_incl_sum(s, sh, (uint32_t*)nullptr);
+  uint32_t pos = out_base[lo] + incl - s;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    if (base + k >= n) break;
+    if (pos == p && bi[k].r == 0) inpos[q] = (uint32_t)(base + k);
+    pos += bi[k].e;
   }
 }
 
@@ -167,18 +210,16 @@ __device__ uint32_t next_chunk_start(const uint32_t* __restrict__ cbits, uint32_
 }
 
 // Sequential block-cut chain (one thread).  See file header for the rule.
-__global__ void k_segment(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ cinpos,
+__global__ void k_segment(const uint32_t* __restrict__ cbits,
                           const uint32_t* __restrict__ m_ptr, uint64_t n, uint32_t nblock_max,
                           int final_batch, int tail_merge, const uint32_t* __restrict__ last_len1_ptr,
-                          uint32_t* __restrict__ boff, uint32_t* __restrict__ binst,
-                          uint32_t* __restrict__ nblocks, uint32_t max_blocks) {
+                          uint32_t* __restrict__ boff, uint32_t* __restrict__ nblocks, uint32_t max_blocks) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const uint32_t m = *m_ptr;
   const uint32_t last_chunk_len1 = *last_len1_ptr;
   uint32_t b = 0, s = 0;
   if (m == 0) {
     boff[0] = 0;
-    binst[0] = 0;
     *nblocks = 0;
     return;
   }
@@ -195,17 +236,15 @@ __global__ void k_segment(const uint32_t* __restrict__ cbits, const uint32_t* __
   }
   for (;;) {
     boff[b] = s;
-    binst[b] = cinpos[s];
     uint32_t t = s + nblock_max;
     uint32_t p = (t < m) ? next_chunk_start(cbits, t, m) : m;
     if (p < m && final_batch && tail_merge && p == last_start && last_chunk_len1) p = m;
     if (p >= m) {
       if (final_batch) {
         boff[b + 1] = m;
-        binst[b + 1] = (uint32_t)n;
         *nblocks = b + 1;
       } else {
-        *nblocks = b;  // block b is incomplete; it restarts the next batch at binst[b]
+        *nblocks = b;  // block b is incomplete; it restarts the next batch at its input start
       }
       return;
     }
@@ -373,7 +412,6 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   uint32_t* mtot = ws.u32("rle_m", 16);
   uint8_t* blk = ws.u8("blk", mcap + 64);
   uint32_t* cbits = ws.u32("rle_cbits", mcap / 32 + 64);
-  uint32_t* cinpos = ws.u32("rle_cinpos", mcap + 64);
   const uint32_t max_blocks = (uint32_t)(mcap / nblock_max + 8);
   uint32_t* boff = ws.u32("boff", max_blocks + 2);
   uint32_t* binst = ws.u32("binst", max_blocks + 2);
@@ -386,11 +424,11 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
   HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
-  k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, blk, cbits, cinpos, mtot + 8);
+  k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, blk, cbits, mtot + 8);
   HIP_OK(hipGetLastError());
 
-  k_segment<<<1, 64, 0, st>>>(cbits, cinpos, mtot, n, nblock_max, final_batch ? 1 : 0, tail_merge ? 1 : 0,
-                              mtot + 8, boff, binst, nbl, max_blocks);
+  k_segment<<<1, 64, 0, st>>>(cbits, mtot, n, nblock_max, final_batch ? 1 : 0, tail_merge ? 1 : 0,
+                              mtot + 8, boff, nbl, max_blocks);
   HIP_OK(hipGetLastError());
   uint32_t hv[2];
   HIP_OK(hipMemcpyAsync(hv, mtot, 4, hipMemcpyDeviceToHost, st));
@@ -399,6 +437,20 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   if (hv[1] == 0xffffffffu) throw HipFailure(hipErrorUnknown);
   res.m = hv[0];
   res.nblocks = hv[1];
+  // input offsets of the block starts (chunk starts): binst[b] for b < nblocks (+ the
+  // incomplete block's start for a non-final batch); binst[nblocks] = n for a final batch
+  {
+    const uint32_t nq = final_batch ? res.nblocks : res.nblocks + 1;
+    if (nq > 0) {
+      k_chunk_inpos<<<nq, kT, 0, st>>>(d_in, n, tmax, tsum, (uint32_t)tiles, boff, nq, binst);
+      HIP_OK(hipGetLastError());
+    }
+    if (final_batch) {
+      const uint32_t nn = (uint32_t)n;
+      HIP_OK(hipMemcpyAsync(binst + res.nblocks, &nn, 4, hipMemcpyHostToDevice, st));
+      HIP_OK(hipStreamSynchronize(st));
+    }
+  }
   if (res.nblocks == 0) {  // non-final batch with no complete block: consume nothing
     res.consumed = final_batch ? n : 0;
     return;

@@ -32,6 +32,7 @@ constexpr uint32_t kSmall = 2048;   // max group size sorted in LDS
 constexpr uint32_t kWin = 2048;     // nominal tile window (tile <= kWin + kSmall - 1 elements)
 constexpr uint32_t kTileCap = 4096;
 constexpr uint32_t kDTile = 4096;   // elements per tile of a digit pass
+constexpr uint32_t kRankMax = 48;   // tiles whose groups are all this small sort by rank counting
 
 struct Unit {
   uint32_t sbase, len, toff, pad;
@@ -113,18 +114,17 @@ __global__ void __launch_bounds__(kT) k_gather(const Grp* __restrict__ L, const 
   B.key[s] = k;
 }
 
-// Split L into the large list (digit passes) and the small list (LDS tiles).
-__global__ void k_partition(const Grp* __restrict__ L, uint32_t nL, int force_large, Grp* __restrict__ large,
-                            uint32_t* __restrict__ n_large, Grp* __restrict__ small, uint32_t* __restrict__ n_small) {
+// Groups too large for an LDS tile go to the digit passes; the rest are tile-sorted in place
+// from L (the tiles skip the large ones).  Large groups are rare, so appends are cheap.
+__global__ void k_extract_large(const Grp* __restrict__ L, uint32_t nL, int force_all, Grp* __restrict__ large,
+                                uint32_t* __restrict__ n_large) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = g < nL;
   Grp G{0, 0, 0, 0};
   if (valid) G = L[g];
-  const bool big = valid && (force_large || G.size > kSmall);
+  const bool big = valid && (force_all || G.size > kSmall);
   const uint32_t pl = wave_append(n_large, big);
-  const uint32_t ps = wave_append(n_small, valid && !big);
   if (big) large[pl] = G;
-  else if (valid) small[ps] = G;
 }
 
 // ---------------------------------------------------------------- digit passes (large)
@@ -253,9 +253,9 @@ struct TileLds {
   uint32_t keyA[kTileCap], valA[kTileCap], keyB[kTileCap], valB[kTileCap];
   uint32_t hist[4][256];
   // items start inside a kWin window and hold >= 2 elements: at most kWin / 2 per tile
-  uint32_t ioff[kWin / 2 + 1];  // tile-local offset of each item (+ end)
-  uint32_t istart[kWin / 2];
-  uint32_t iunit[kWin / 2];
+  uint32_t ioff[kWin / 2 + 8];  // tile-local offset of each item (+ end)
+  uint32_t istart[kWin / 2 + 8];
+  uint32_t iunit[kWin / 2 + 8];
   uint32_t sh[8];
   uint32_t misc[8];
 };
@@ -334,16 +334,41 @@ __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small,
   __syncthreads();
   const uint32_t i1 = min(S.misc[0], i0 + kWin / 2);
   const uint32_t ni = i1 - i0;
-  const uint32_t p0 = P[i0];
-  for (uint32_t j = threadIdx.x; j < ni; j += kT) {
-    const Grp g = small[i0 + j];
-    S.ioff[j] = P[i0 + j] - p0;
-    S.istart[j] = g.start;
-    S.iunit[j] = g.unit | ((g.flags & 1u) << 31);
-    if (j == ni - 1) S.ioff[ni] = P[i0 + j] - p0 + g.size;
+  // Items larger than kSmall (sorted by the digit passes) are compacted away: their
+  // tile-local size is 0.  Offsets are recomputed over the kept items.
+  if (threadIdx.x == 0) S.misc[2] = 0;
+  __syncthreads();
+  uint32_t my_sz[kWin / 2 / kT + 1];
+  uint32_t my_sum = 0;
+#pragma unroll
+  for (int q = 0; q < (int)(kWin / 2 / kT + 1); q++) {
+    const uint32_t j = threadIdx.x * (kWin / 2 / kT + 1) + q;
+    uint32_t sz = 0;
+    if (j < ni) {
+      const Grp g = small[i0 + j];
+      sz = g.size <= kSmall ? g.size : 0u;
+      S.istart[j] = g.start;
+      S.iunit[j] = g.unit | ((g.flags & 1u) << 31);
+      if (g.size > kSmall) atomicMax(&S.misc[2], 1u);
+    }
+    my_sz[q] = sz;
+    my_sum += sz;
+  }
+  {
+    uint32_t tot_e;
+    const uint32_t incl = block_incl_sum(my_sum, S.sh, &tot_e);
+    uint32_t o = incl - my_sum;
+#pragma unroll
+    for (int q = 0; q < (int)(kWin / 2 / kT + 1); q++) {
+      const uint32_t j = threadIdx.x * (kWin / 2 / kT + 1) + q;
+      if (j < ni) S.ioff[j] = o;
+      o += my_sz[q];
+    }
+    if (threadIdx.x == 0) S.ioff[ni] = tot_e;
   }
   __syncthreads();
   const uint32_t n = S.ioff[ni];
+  if (n == 0) return;
   const uint32_t kmask = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
   for (uint32_t e = threadIdx.x; e < n; e += kT) {
     // item of element e
@@ -362,8 +387,36 @@ __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small,
   }
   __syncthreads();
   const uint32_t item_bits = 32 - __builtin_clz(ni);  // ni >= 1
+  // largest item in the tile decides the method
+  {
+    uint32_t mx = 0;
+    for (uint32_t j = threadIdx.x; j < ni; j += kT) mx = max(mx, S.ioff[j + 1] - S.ioff[j]);
+    mx = block_incl_max(mx, S.sh);
+    if (threadIdx.x == kT - 1) S.misc[3] = mx;
+    __syncthreads();
+  }
   uint32_t *keys, *vals;
-  lds_radix_sort(S, n, key_bits + item_bits, keys, vals);
+  if (S.misc[3] <= kRankMax) {
+    // rank counting: element e goes to ioff[item] + #{f in item : (key_f, f) < (key_e, e)};
+    // lanes of one item read the same key at each step (LDS broadcast)
+    for (uint32_t e = threadIdx.x; e < n; e += kT) {
+      const uint32_t ke = S.keyA[e];
+      const uint32_t item = ke >> key_bits;
+      const uint32_t lo = S.ioff[item], hi = S.ioff[item + 1];
+      uint32_t r = 0;
+      for (uint32_t f = lo; f < hi; f++) {
+        const uint32_t kf = S.keyA[f];
+        r += (kf < ke) | ((kf == ke) & (f < e));
+      }
+      S.keyB[lo + r] = ke;
+      S.valB[lo + r] = S.valA[e];
+    }
+    __syncthreads();
+    keys = S.keyB;
+    vals = S.valB;
+  } else {
+    lds_radix_sort(S, n, key_bits + item_bits, keys, vals);
+  }
   // group detection over the sorted composite keys; thread t owns [16t, 16t+16)
   uint32_t starts = 0;
   const uint32_t e0 = threadIdx.x * 16;
@@ -575,7 +628,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     }
     k_gather<<<grid(totalL), kT, 0, st>>>(L, P, nL, totalL, h, B);
     HIP_OK(hipGetLastError());
-    k_partition<<<grid(nL), kT, 0, st>>>(L, nL, h == 0 ? 1 : 0, large, cnt + 1, small, cnt + 2);
+    k_extract_large<<<grid(nL), kT, 0, st>>>(L, nL, h == 0 ? 1 : 0, large, cnt + 1);
     HIP_OK(hipGetLastError());
     read_counters();
     uint32_t n_large = hc[1];
@@ -605,11 +658,21 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       n_large = hc[4];
       std::swap(lg, lg2);
     }
+    HIP_OK(hipMemsetAsync(cnt + 3, 0, 4, st));
+    const uint32_t kbits = h == 0 ? 16u : 20u;
+    // groups of L small enough for LDS: tiles straight over L (P still holds L's prefix)
+    if (h > 0) {
+      const uint32_t ntiles = ceil_div(totalL, kWin);
+      HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
+      k_tile_first<<<grid(nL), kT, 0, st>>>(P, nL, first);
+      HIP_OK(hipGetLastError());
+      k_tile_sort<<<ntiles, kT, tile_lds, st>>>(L, nL, P, first, kbits, B, Ln, cnt + 3);
+      HIP_OK(hipGetLastError());
+    }
     read_counters();
     const uint32_t n_small = hc[2];
     const uint32_t n_equal = hc[5];
-    HIP_OK(hipMemsetAsync(cnt + 3, 0, 4, st));
-    if (n_small > 0) {
+    if (n_small > 0) {  // buckets emitted by the digit passes
       k_group_sizes<<<grid(n_small), kT, 0, st>>>(small, n_small, P);
       HIP_OK(hipGetLastError());
       scan_u32(ScanOp::Sum, true, P, P, n_small, cnt + 0, scratch, st);
@@ -619,7 +682,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
       k_tile_first<<<grid(n_small), kT, 0, st>>>(P, n_small, first);
       HIP_OK(hipGetLastError());
-      k_tile_sort<<<ntiles, kT, tile_lds, st>>>(small, n_small, P, first, h == 0 ? 16u : 20u, B, Ln, cnt + 3);
+      k_tile_sort<<<ntiles, kT, tile_lds, st>>>(small, n_small, P, first, kbits, B, Ln, cnt + 3);
       HIP_OK(hipGetLastError());
     }
     if (n_equal > 0) {
