@@ -7,6 +7,9 @@
 // per-table symbol frequencies gathered with LDS atomics; each table's heap Huffman runs on
 // one lane with the reference's exact tie order.  Packing computes every field's bit offset
 // with block-level scans and ORs 32-bit big-endian words into the (zeroed) output.
+#include <cstdio>
+#include <cstdlib>
+
 #include "stages.h"
 #include "scan.h"
 
@@ -18,15 +21,23 @@ constexpr int kT = 256;
 struct CodeLds {
   uint32_t rfreq[kNGroups][kMaxAlpha];
   uint32_t code[kNGroups][kMaxAlpha];
-  int32_t hweight[kNGroups][kMaxAlpha * 2];
-  int32_t hparent[kNGroups][kMaxAlpha * 2];
-  int32_t hheap[kNGroups][kMaxAlpha + 4];
+  uint32_t lenp[2][kMaxAlpha];  // code lengths of tables 0-2 / 3-5 packed in 10-bit fields
+  union {
+    struct {
+      int32_t weight[kNGroups][kMaxAlpha * 2];
+      int32_t parent[kNGroups][kMaxAlpha * 2];
+      int32_t heap[kNGroups][kMaxAlpha + 4];
+    } h;                                     // Huffman construction
+    uint16_t chunk[kT * kGroupSize + 8];     // MTF values of kT consecutive selector groups
+  } u;
   uint8_t len[kNGroups][kMaxAlpha + 2];
   uint8_t sel[kMaxSelectors + 4];
   uint32_t freq[kMaxAlpha];
   uint32_t sh[8];
   uint32_t misc[16];
 };
+
+static_assert(2 * sizeof(CodeLds) <= 160 * 1024, "two table workgroups must fit one CU's LDS");
 
 // BZ2_hbMakeCodeLengths (huffman.c:63-148) on one lane: leaf weight = max(freq,1) << 8 | 0,
 // merge = sum of weights | (1 + max depth); heap moves use strict '<'; rescale with
@@ -102,9 +113,22 @@ __global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv
                                                const uint32_t* __restrict__ ninuse, const uint32_t* __restrict__ inuse,
                                                uint8_t* __restrict__ lens_g, uint32_t* __restrict__ codes_g,
                                                uint8_t* __restrict__ sel_g, uint8_t* __restrict__ selmtf_g,
-                                               uint16_t* __restrict__ gbits_g, uint32_t* __restrict__ info_g) {
+                                               uint16_t* __restrict__ gbits_g, uint32_t* __restrict__ info_g,
+                                               uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   CodeLds& S = *reinterpret_cast<CodeLds*>(smem);
+  uint64_t t_last = stamps ? __builtin_amdgcn_s_memtime() : 0;
+  // diagnostic phase stamps (BZG_DEBUG): s_memtime ticks summed over workgroups
+  auto stamp = [&](int k) {
+    if (stamps) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        atomicAdd((unsigned long long*)&stamps[k], (unsigned long long)(now - t_last));
+        t_last = now;
+      }
+    }
+  };
   const uint32_t b = blockIdx.x;
   const uint32_t nmtf = nmtf_g[b];
   const uint16_t* mv = mtfv + mtf_off[b];
@@ -113,7 +137,9 @@ __global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv
   const uint32_t nsel = ceil_div(nmtf, kGroupSize);
   for (int i = threadIdx.x; i < kMaxAlpha; i += kT) S.freq[i] = freq_g[(size_t)b * kMaxAlpha + i];
   __syncthreads();
-  // initial tables (compress.c:276-319)
+  // initial tables (compress.c:276-319); tables >= ng stay all-zero so packed sums cannot overflow
+  for (int i = threadIdx.x; i < kNGroups * (kMaxAlpha + 2); i += kT) (&S.len[0][0])[i] = 0;
+  __syncthreads();
   if (threadIdx.x == 0) {
     for (int t = 0; t < ng; t++)
       for (int v = 0; v < alpha; v++) S.len[t][v] = 15;
@@ -130,18 +156,38 @@ __global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv
     }
   }
   __syncthreads();
+  // Visit every selector group with its six table costs (50 lengths <= 17: sums < 1024).
+  // Symbols are staged through LDS kT groups at a time; lane l owns group g0 + l.
+  auto for_groups = [&](auto&& f) {
+    for (int v = threadIdx.x; v < kMaxAlpha; v += kT) {
+      S.lenp[0][v] = S.len[0][v] | ((uint32_t)S.len[1][v] << 10) | ((uint32_t)S.len[2][v] << 20);
+      S.lenp[1][v] = S.len[3][v] | ((uint32_t)S.len[4][v] << 10) | ((uint32_t)S.len[5][v] << 20);
+    }
+    for (uint32_t g0 = 0; g0 < nsel; g0 += kT) {
+      const uint32_t lo = g0 * kGroupSize, hi = min((g0 + kT) * kGroupSize, nmtf);
+      for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) S.u.chunk[i - lo] = mv[i];
+      __syncthreads();
+      const uint32_t g = g0 + threadIdx.x;
+      if (g < nsel) {
+        const uint16_t* c = S.u.chunk + threadIdx.x * kGroupSize;
+        const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
+        uint32_t a = 0, bsum = 0;
+        for (uint32_t i = 0; i < n; i++) {
+          const uint32_t v = c[i];
+          a += S.lenp[0][v];
+          bsum += S.lenp[1][v];
+        }
+        const uint32_t cost[kNGroups] = {a & 1023u, (a >> 10) & 1023u, a >> 20, bsum & 1023u, (bsum >> 10) & 1023u, bsum >> 20};
+        f(g, c, n, cost);
+      }
+      __syncthreads();
+    }
+  };
   for (int it = 0; it < kIters; it++) {
     for (int i = threadIdx.x; i < kNGroups * kMaxAlpha; i += kT) (&S.rfreq[0][0])[i] = 0;
     __syncthreads();
-    for (uint32_t g = threadIdx.x; g < nsel; g += kT) {
-      const uint32_t gs = g * kGroupSize, ge = min(gs + kGroupSize, nmtf);
-      uint32_t cost[kNGroups] = {0, 0, 0, 0, 0, 0};
-      for (uint32_t i = gs; i < ge; i++) {
-        const uint32_t v = mv[i];
-#pragma unroll
-        for (int t = 0; t < kNGroups; t++) cost[t] += S.len[t][v];
-      }
-      int bt = 0;
+    for_groups([&](uint32_t g, const uint16_t* c, uint32_t n, const uint32_t* cost) {
+      int bt = 0;  // lowest index wins ties (compress.c:416-420)
       uint32_t bc = cost[0];
       for (int t = 1; t < ng; t++)
         if (cost[t] < bc) {
@@ -149,14 +195,15 @@ __global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv
           bt = t;
         }
       S.sel[g] = (uint8_t)bt;
-      for (uint32_t i = gs; i < ge; i++) atomicAdd(&S.rfreq[bt][mv[i]], 1u);
-    }
-    __syncthreads();
+      for (uint32_t i = 0; i < n; i++) atomicAdd(&S.rfreq[bt][c[i]], 1u);
+    });
+    stamp(0);
     if (threadIdx.x < (unsigned)ng) {
       const int t = threadIdx.x;
-      hb_code_lengths(S.len[t], S.rfreq[t], alpha, kMaxCodeLen, S.hheap[t], S.hweight[t], S.hparent[t]);
+      hb_code_lengths(S.len[t], S.rfreq[t], alpha, kMaxCodeLen, S.u.h.heap[t], S.u.h.weight[t], S.u.h.parent[t]);
     }
     __syncthreads();
+    stamp(1);
   }
   // selector table ids out
   uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
@@ -180,31 +227,48 @@ __global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv
   // payload bits per group
   uint32_t mybits = 0;
   uint16_t* gb = gbits_g + (size_t)b * kMaxSelectors;
-  for (uint32_t g = threadIdx.x; g < nsel; g += kT) {
-    const uint32_t gs = g * kGroupSize, ge = min(gs + kGroupSize, nmtf);
-    const int t = S.sel[g];
-    uint32_t bits = 0;
-    for (uint32_t i = gs; i < ge; i++) bits += S.len[t][mv[i]];
+  for_groups([&](uint32_t g, const uint16_t*, uint32_t, const uint32_t* cost) {
+    const uint32_t bits = cost[S.sel[g]];
     gb[g] = (uint16_t)bits;
     mybits += bits;
-  }
+  });
   uint32_t data_bits;
   block_incl_sum(mybits, S.sh, &data_bits);
-  // selector MTF (compress.c:573-631): lane 0, sequential
+  stamp(2);
+  // selector MTF (compress.c:573-631) in parallel: the MTF index of selector s at g is the
+  // number of tables used more recently than s, where the initial order 0..5 counts as
+  // uses at times -1..-6.  Thread k owns a contiguous run of selectors; the last use of
+  // every table before the run comes from a block max-scan.
   uint8_t* smo = selmtf_g + (size_t)b * kMaxSelectors;
-  if (threadIdx.x == 0) {
-    uint8_t order[kNGroups] = {0, 1, 2, 3, 4, 5};
-    uint32_t sbits = 0;
-    for (uint32_t g = 0; g < nsel; g++) {
-      const uint8_t s = S.sel[g];
-      int j = 0;
-      while (order[j] != s) j++;
-      for (int k = j; k > 0; k--) order[k] = order[k - 1];
-      order[0] = s;
-      smo[g] = (uint8_t)j;
-      sbits += (uint32_t)j + 1;
+  {
+    const uint32_t per = ceil_div(nsel, (uint32_t)kT);
+    const uint32_t g_lo = min(nsel, threadIdx.x * per), g_hi = min(nsel, g_lo + per);
+    int32_t mine[kNGroups] = {-1, -1, -1, -1, -1, -1};  // last use inside my run (+1), 0 = none
+    for (uint32_t g = g_lo; g < g_hi; g++) mine[S.sel[g]] = (int32_t)g + 1;
+    int32_t last[kNGroups];
+#pragma unroll
+    for (int t = 0; t < kNGroups; t++) {
+      const uint32_t m = mine[t] < 0 ? 0u : (uint32_t)mine[t];
+      const uint32_t incl = block_incl_max(m, S.sh);
+      uint32_t ex = __shfl_up(incl, 1);
+      if (__lane_id() == 0) ex = threadIdx.x >= 64 ? S.sh[(threadIdx.x >> 6) - 1] : 0u;
+      __syncthreads();
+      last[t] = ex ? (int32_t)ex - 1 : -1 - t;
     }
-    S.misc[0] = sbits;
+    uint32_t sbits = 0;
+    for (uint32_t g = g_lo; g < g_hi; g++) {
+      const int s = S.sel[g];
+      const int32_t ls = last[s];
+      uint32_t j = 0;
+#pragma unroll
+      for (int t = 0; t < kNGroups; t++) j += last[t] > ls;
+      last[s] = (int32_t)g;
+      smo[g] = (uint8_t)j;
+      sbits += j + 1;
+    }
+    uint32_t tot;
+    block_incl_sum(sbits, S.sh, &tot);
+    if (threadIdx.x == 0) S.misc[0] = tot;
   }
   // code-length table bits (compress.c:694-706)
   if (threadIdx.x < (unsigned)ng) {
@@ -245,6 +309,7 @@ __global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv
     info[5] = tbits;
     info[6] = data_bits;
   }
+  stamp(3);
 }
 
 // Bit offsets of every block, the combined CRC, the trailer position.
@@ -458,10 +523,20 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
     HIP_OK(hipFuncSetAttribute((const void*)k_tables, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(CodeLds)));
     attr = true;
   }
+  static const bool debug = getenv("BZG_DEBUG") != nullptr;
+  uint64_t* stamps = (uint64_t*)ws.u32("code_stamps", 16);
+  if (debug) HIP_OK(hipMemsetAsync(stamps, 0, 64, st));
   if (nb > 0) {
     k_tables<<<nb, kT, sizeof(CodeLds), st>>>(m.mtfv, m.mtf_off, m.nmtf, m.freq, r.ninuse, r.inuse, lens, codes, sel,
-                                               selmtf, gbits, info);
+                                               selmtf, gbits, info, debug ? stamps : nullptr);
     HIP_OK(hipGetLastError());
+    if (debug) {
+      uint64_t hs[4];
+      HIP_OK(hipMemcpyAsync(hs, stamps, 32, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      fprintf(stderr, "[bzg tables stamps] blocks=%u | cost+freq %lu  huffman %lu  codes+bits %lu  selmtf+out %lu\n", nb,
+              hs[0], hs[1], hs[2], hs[3]);
+    }
   }
   const bool header = !carry.header_done;
   const uint64_t start_bit = carry.carry_bits + (header ? 32 : 0);

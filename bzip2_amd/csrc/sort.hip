@@ -88,12 +88,19 @@ __global__ void k_init_sa(const Grp* __restrict__ L, const uint32_t* __restrict_
   sa[G.start + off] = off;
 }
 
+// Element -> group map: gmap[P[g]] = g on a zeroed array, then an inclusive max-scan.
+__global__ void k_mark_groups(const uint32_t* __restrict__ P, uint32_t nL, uint32_t* __restrict__ gmap) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < nL) gmap[P[g]] = g;
+}
+
 // key[s] for every member of every group in L.
 __global__ void __launch_bounds__(kT) k_gather(const Grp* __restrict__ L, const uint32_t* __restrict__ P,
-                                               uint32_t nL, uint32_t total, uint32_t h, SortBufs B) {
+                                               const uint32_t* __restrict__ gmap, uint32_t total, uint32_t h,
+                                               SortBufs B) {
   uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= total) return;
-  uint32_t g = upper_idx(P, nL, x);
+  const uint32_t g = gmap[x];
   const Grp G = L[g];
   const uint32_t s = G.start + (x - P[g]);
   const Unit U = B.units[G.unit];
@@ -241,17 +248,19 @@ __global__ void __launch_bounds__(kT) k_dsingle(const Grp* __restrict__ G, uint3
 }
 
 // ---------------------------------------------------------------- small groups (LDS)
-// tile index of item i = P[i] / kWin; mark the first item of each tile.
-__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_t* __restrict__ first) {
+// tile index of item i = P[i] / kWin; mark the first item of each tile and one past its last.
+__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_t* __restrict__ first,
+                             uint32_t* __restrict__ last) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t t = P[i] / kWin;
   if (i == 0 || P[i - 1] / kWin != t) first[t] = i;
+  if (i == n - 1 || P[i + 1] / kWin != t) last[t] = i + 1;
 }
 
 struct TileLds {
   uint32_t keyA[kTileCap], valA[kTileCap], keyB[kTileCap], valB[kTileCap];
-  uint32_t hist[4][256];
+  uint16_t hist[4][256];  // per-wave digit counts / bases (<= kTileCap)
   // items start inside a kWin window and hold >= 2 elements: at most kWin / 2 per tile
   uint32_t ioff[kWin / 2 + 8];  // tile-local offset of each item (+ end)
   uint32_t istart[kWin / 2 + 8];
@@ -269,7 +278,7 @@ __device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*
   uint32_t* vout = S.valB;
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   for (uint32_t shift = 0; shift < nbits; shift += 8) {
-    for (int i = threadIdx.x; i < 4 * 256; i += kT) (&S.hist[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 4 * 256 / 2; i += kT) reinterpret_cast<uint32_t*>(&S.hist[0][0])[i] = 0;
     __syncthreads();
     uint32_t dig[16], loc[16];
 #pragma unroll
@@ -282,7 +291,7 @@ __device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*
       const uint32_t rank = __popcll(peers & lanemask_lt());
       uint32_t old = act ? S.hist[w][d] : 0u;
       const bool leader = act && ((peers & lanemask_lt()) == 0);
-      if (leader) S.hist[w][d] = old + (uint32_t)__popcll(peers);
+      if (leader) S.hist[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
       dig[j] = d;
       loc[j] = old + rank;
     }
@@ -293,10 +302,10 @@ __device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*
       uint32_t tot = c0 + c1 + c2 + c3;
       uint32_t incl = block_incl_sum(tot, S.sh, (uint32_t*)nullptr);
       uint32_t b = incl - tot;
-      S.hist[0][d] = b;
-      S.hist[1][d] = b + c0;
-      S.hist[2][d] = b + c0 + c1;
-      S.hist[3][d] = b + c0 + c1 + c2;
+      S.hist[0][d] = (uint16_t)b;
+      S.hist[1][d] = (uint16_t)(b + c0);
+      S.hist[2][d] = (uint16_t)(b + c0 + c1);
+      S.hist[3][d] = (uint16_t)(b + c0 + c1 + c2);
     }
     __syncthreads();
 #pragma unroll
@@ -317,40 +326,47 @@ __device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*
   vals = vin;
 }
 
+// Diagnostic stamps (BZG_DEBUG builds only): phase durations summed over workgroups.
+#define STAMP(k)                                                                    \
+  if constexpr (kStamp) {                                                           \
+    __syncthreads();                                                                \
+    if (threadIdx.x == 0) {                                                         \
+      const uint64_t now = __builtin_amdgcn_s_memtime();                            \
+      atomicAdd((unsigned long long*)&stamps[k], (unsigned long long)(now - t_last)); \
+      t_last = now;                                                                 \
+    }                                                                               \
+  }
+
+template <bool kStamp>
 __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small, uint32_t n_small,
-                                                  const uint32_t* __restrict__ P, const uint32_t* __restrict__ first,
+                                                  const uint32_t* __restrict__ first, const uint32_t* __restrict__ last,
                                                   uint32_t key_bits, SortBufs B, Grp* __restrict__ next,
-                                                  uint32_t* __restrict__ n_next) {
+                                                  uint32_t* __restrict__ n_next, bool isa_valid,
+                                                  uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   TileLds& S = *reinterpret_cast<TileLds*>(smem);
   const uint32_t t = blockIdx.x;
   const uint32_t i0 = first[t];
   if (i0 == 0xffffffffu) return;
-  // items of this tile: i0 .. i1-1 with P[i]/kWin == t
-  if (threadIdx.x == 0) S.misc[0] = n_small;
-  __syncthreads();
-  for (uint32_t i = i0 + threadIdx.x; i < n_small && i < i0 + kWin / 2 + 1; i += kT)
-    if (P[i] / kWin != t) atomicMin(&S.misc[0], i);
-  __syncthreads();
-  const uint32_t i1 = min(S.misc[0], i0 + kWin / 2);
+  uint64_t t_last = kStamp ? __builtin_amdgcn_s_memtime() : 0;
+  // items of this tile: i0 .. i1-1 with P[i]/kWin == t (at most kWin/2: items hold >= 2 elements)
+  const uint32_t i1 = min(last[t], i0 + kWin / 2);
   const uint32_t ni = i1 - i0;
   // Items larger than kSmall (sorted by the digit passes) are compacted away: their
   // tile-local size is 0.  Offsets are recomputed over the kept items.
-  if (threadIdx.x == 0) S.misc[2] = 0;
+  for (uint32_t j = threadIdx.x; j < ni; j += kT) {
+    const Grp g = small[i0 + j];
+    S.istart[j] = g.start;
+    S.iunit[j] = g.unit | ((g.flags & 1u) << 31);
+    S.ioff[j] = g.size <= kSmall ? g.size : 0u;
+  }
   __syncthreads();
   uint32_t my_sz[kWin / 2 / kT + 1];
   uint32_t my_sum = 0;
 #pragma unroll
   for (int q = 0; q < (int)(kWin / 2 / kT + 1); q++) {
     const uint32_t j = threadIdx.x * (kWin / 2 / kT + 1) + q;
-    uint32_t sz = 0;
-    if (j < ni) {
-      const Grp g = small[i0 + j];
-      sz = g.size <= kSmall ? g.size : 0u;
-      S.istart[j] = g.start;
-      S.iunit[j] = g.unit | ((g.flags & 1u) << 31);
-      if (g.size > kSmall) atomicMax(&S.misc[2], 1u);
-    }
+    const uint32_t sz = j < ni ? S.ioff[j] : 0u;
     my_sz[q] = sz;
     my_sum += sz;
   }
@@ -369,15 +385,35 @@ __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small,
   __syncthreads();
   const uint32_t n = S.ioff[ni];
   if (n == 0) return;
+  STAMP(0);
   const uint32_t kmask = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
+  {  // owner map: item index of every element (mark item starts, then a block max-scan)
+    uint32_t* owner = S.keyB;
+    uint4* o4 = reinterpret_cast<uint4*>(owner);
+    for (uint32_t i = threadIdx.x; i < kTileCap / 4; i += kT) o4[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < ni; j += kT)
+      if (S.ioff[j + 1] > S.ioff[j]) owner[S.ioff[j]] = j;
+    __syncthreads();
+    uint4 a = o4[threadIdx.x * 4], b = o4[threadIdx.x * 4 + 1], c = o4[threadIdx.x * 4 + 2], d = o4[threadIdx.x * 4 + 3];
+    uint32_t m = max(max(max(a.x, a.y), max(a.z, a.w)), max(max(b.x, b.y), max(b.z, b.w)));
+    m = max(m, max(max(max(c.x, c.y), max(c.z, c.w)), max(max(d.x, d.y), max(d.z, d.w))));
+    const uint32_t incl = block_incl_max(m, S.sh);
+    uint32_t run = __shfl_up(incl, 1);
+    if (__lane_id() == 0) run = threadIdx.x >= 64 ? S.sh[(threadIdx.x >> 6) - 1] : 0u;
+    if (threadIdx.x == 0) run = 0;
+#define BZG_RUNMAX(v) v = run = max(run, v)
+    BZG_RUNMAX(a.x); BZG_RUNMAX(a.y); BZG_RUNMAX(a.z); BZG_RUNMAX(a.w);
+    BZG_RUNMAX(b.x); BZG_RUNMAX(b.y); BZG_RUNMAX(b.z); BZG_RUNMAX(b.w);
+    BZG_RUNMAX(c.x); BZG_RUNMAX(c.y); BZG_RUNMAX(c.z); BZG_RUNMAX(c.w);
+    BZG_RUNMAX(d.x); BZG_RUNMAX(d.y); BZG_RUNMAX(d.z); BZG_RUNMAX(d.w);
+#undef BZG_RUNMAX
+    __syncthreads();
+    o4[threadIdx.x * 4] = a; o4[threadIdx.x * 4 + 1] = b; o4[threadIdx.x * 4 + 2] = c; o4[threadIdx.x * 4 + 3] = d;
+    __syncthreads();
+  }
   for (uint32_t e = threadIdx.x; e < n; e += kT) {
-    // item of element e
-    uint32_t lo = 0, hi = ni;
-    while (hi - lo > 1) {
-      uint32_t mid = (lo + hi) >> 1;
-      if (S.ioff[mid] <= e) lo = mid;
-      else hi = mid;
-    }
+    const uint32_t lo = S.keyB[e];
     const uint32_t s = S.istart[lo] + (e - S.ioff[lo]);
     const bool alt = S.iunit[lo] >> 31;
     const uint32_t k = alt ? B.key2[s] : B.key[s];
@@ -386,6 +422,7 @@ __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small,
     S.valA[e] = v;
   }
   __syncthreads();
+  STAMP(1);
   const uint32_t item_bits = 32 - __builtin_clz(ni);  // ni >= 1
   // largest item in the tile decides the method
   {
@@ -414,76 +451,90 @@ __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small,
     __syncthreads();
     keys = S.keyB;
     vals = S.valB;
+    STAMP(2);
   } else {
     lds_radix_sort(S, n, key_bits + item_bits, keys, vals);
+    STAMP(3);
   }
   // group detection over the sorted composite keys; thread t owns [16t, 16t+16)
-  uint32_t starts = 0;
   const uint32_t e0 = threadIdx.x * 16;
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const uint32_t e = e0 + q;
-    if (e < n && (e == 0 || keys[e] != keys[e - 1])) starts++;
-  }
-  uint32_t ngroups;
-  uint32_t incl = block_incl_sum(starts, S.sh, &ngroups);
-  // gpos[o] = first element of group o, stored in the free B/A buffer (not keys/vals)
-  uint32_t* gpos = (keys == S.keyA) ? S.keyB : S.keyA;
+  uint32_t kq[16];
   {
-    uint32_t o = incl - starts;
+    const uint4* k4 = reinterpret_cast<const uint4*>(keys + e0);
+    const uint4 a = k4[0], b = k4[1], c = k4[2], d = k4[3];
+    kq[0] = a.x; kq[1] = a.y; kq[2] = a.z; kq[3] = a.w; kq[4] = b.x; kq[5] = b.y; kq[6] = b.z; kq[7] = b.w;
+    kq[8] = c.x; kq[9] = c.y; kq[10] = c.z; kq[11] = c.w; kq[12] = d.x; kq[13] = d.y; kq[14] = d.z; kq[15] = d.w;
+  }
+  uint32_t smask = 0;  // bit q: element e0 + q starts a group
+  {
+    uint32_t prev = (e0 > 0 && e0 <= n) ? keys[e0 - 1] : 0u;
+#pragma unroll
     for (int q = 0; q < 16; q++) {
       const uint32_t e = e0 + q;
-      if (e < n && (e == 0 || keys[e] != keys[e - 1])) gpos[o++] = e;
+      if (e < n && (e == 0 || kq[q] != prev)) smask |= 1u << q;
+      prev = kq[q];
     }
+  }
+  const uint32_t starts = __popc(smask);
+  uint32_t ngroups;
+  const uint32_t incl = block_incl_sum(starts, S.sh, &ngroups);
+  // gpos[o] = first element of group o (free key buffer); gid[e] = group of e (free val buffer)
+  uint32_t* gpos = (keys == S.keyA) ? S.keyB : S.keyA;
+  uint32_t* gid = (vals == S.valA) ? S.valB : S.valA;
+  {
+    uint32_t o = incl - starts;
+    uint32_t gq[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      if ((smask >> q) & 1u) gpos[o++] = e0 + q;
+      gq[q] = o - 1;  // unused for e >= n
+    }
+    uint4* g4 = reinterpret_cast<uint4*>(gid + e0);
+    g4[0] = make_uint4(gq[0], gq[1], gq[2], gq[3]);
+    g4[1] = make_uint4(gq[4], gq[5], gq[6], gq[7]);
+    g4[2] = make_uint4(gq[8], gq[9], gq[10], gq[11]);
+    g4[3] = make_uint4(gq[12], gq[13], gq[14], gq[15]);
   }
   if (threadIdx.x == 0) gpos[ngroups] = n;
   __syncthreads();
+  STAMP(4);
   // groups of size >= 2 go to the next iteration
   uint32_t nnew = 0;
   {
     uint32_t o = incl - starts;
-    for (int q = 0; q < 16; q++) {
-      const uint32_t e = e0 + q;
-      if (e < n && (e == 0 || keys[e] != keys[e - 1])) {
-        if (gpos[o + 1] - e >= 2) nnew++;
-        o++;
+    for (uint32_t m = smask; m; m &= m - 1, o++) nnew += (gpos[o + 1] - (e0 + __builtin_ctz(m)) >= 2);
+  }
+  uint32_t tot_new;
+  const uint32_t incl_new = block_incl_sum(nnew, S.sh, &tot_new);
+  if (threadIdx.x == 0) S.misc[1] = tot_new ? atomicAdd(n_next, tot_new) : 0;
+  __syncthreads();
+  if (nnew) {
+    uint32_t wpos = S.misc[1] + incl_new - nnew;
+    uint32_t o = incl - starts;
+    for (uint32_t m = smask; m; m &= m - 1, o++) {
+      const uint32_t e = e0 + __builtin_ctz(m);
+      const uint32_t sz = gpos[o + 1] - e;
+      if (sz >= 2) {
+        const uint32_t item = kq[__builtin_ctz(m)] >> key_bits;
+        next[wpos++] = Grp{S.istart[item] - S.ioff[item] + e, sz, S.iunit[item] & 0x7fffffffu, 0};
       }
     }
   }
-  uint32_t tot_new;
-  uint32_t incl_new = block_incl_sum(nnew, S.sh, &tot_new);
-  if (threadIdx.x == 0) S.misc[1] = tot_new ? atomicAdd(n_next, tot_new) : 0;
-  __syncthreads();
-  uint32_t wpos = S.misc[1] + incl_new - nnew;
-  uint32_t o = incl - starts;
-  uint32_t gstart = 0;
-  // group start for the first element of this thread: the last start <= e0
-  if (e0 < n) {
-    uint32_t lo = 0, hi = ngroups;  // largest o with gpos[o] <= e0
-    while (hi - lo > 1) {
-      uint32_t mid = (lo + hi) >> 1;
-      if (gpos[mid] <= e0) lo = mid;
-      else hi = mid;
-    }
-    gstart = gpos[lo];
-  }
-  for (int q = 0; q < 16; q++) {
-    const uint32_t e = e0 + q;
-    if (e >= n) break;
-    const bool st = (e == 0 || keys[e] != keys[e - 1]);
-    if (st) gstart = e;
+  // element-parallel output: SA in slot order (coalesced); an ISA entry is rewritten only
+  // when the rank changes (isa_valid: every member's ISA already holds its item's start)
+  for (uint32_t e = threadIdx.x; e < n; e += kT) {
     const uint32_t item = keys[e] >> key_bits;
-    const uint32_t base = S.istart[item] - S.ioff[item];
-    const uint32_t unit = S.iunit[item] & 0x7fffffffu;
+    const uint32_t istart = S.istart[item];
+    const uint32_t base = istart - S.ioff[item];
     const uint32_t v = vals[e];
-    const uint32_t slot = base + e, gslot = base + gstart;
-    B.sa[slot] = v;
-    B.isa[B.units[unit].sbase + v] = gslot;
-    if (st) {
-      const uint32_t sz = gpos[o + 1] - e;
-      if (sz >= 2) next[wpos++] = Grp{gslot, sz, unit, 0};
-      o++;
-    }
+    B.sa[base + e] = v;
+    const uint32_t gslot = base + gpos[gid[e]];
+    if (!isa_valid || gslot != istart) B.isa[B.units[S.iunit[item] & 0x7fffffffu].sbase + v] = gslot;
+  }
+  STAMP(5);
+  if constexpr (kStamp) {
+    if (threadIdx.x == 0) atomicAdd((unsigned long long*)&stamps[6], 1ull);
+    if (threadIdx.x == 0) atomicAdd((unsigned long long*)&stamps[7], (unsigned long long)n);
   }
 }
 
@@ -567,11 +618,13 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* P = ws.u32("sort_P", lcap + 16);
   uint32_t* TP = ws.u32("sort_TP", bigcap + S / kDTile + 64);
   uint32_t* first = ws.u32("sort_first", S / kWin + 64);
+  uint32_t* last = ws.u32("sort_last", S / kWin + 64);
+  uint32_t* gmap = ws.u32("sort_gmap", S + 16);
   const size_t max_dtiles = S / kDTile + bigcap + 16;
   uint32_t* hist = ws.u32("sort_hist", max_dtiles * 256);
   uint32_t* tot = ws.u32("sort_tot", bigcap * 256);
   uint32_t* cnt = ws.u32("sort_cnt", 64);  // device counters
-  uint32_t* scratch = ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(lcap, max_dtiles)) + 64);
+  uint32_t* scratch = ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(lcap, max_dtiles), S + 16)) + 64);
   // counters: 0 total(scan), 1 n_large, 2 n_small, 3 n_next(L'), 4 n_large2, 5 n_equal, 6 tiles
   uint32_t hc[8];
   auto read_counters = [&]() {
@@ -589,11 +642,15 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   HIP_OK(hipGetLastError());
 
   static const bool debug = getenv("BZG_DEBUG") != nullptr;
+  uint64_t* stamps = (uint64_t*)ws.u32("sort_stamps", 32);
+  if (debug) HIP_OK(hipMemsetAsync(stamps, 0, 128, st));
   std::vector<uint32_t> hsz;  // debug: sizes of the groups in L
   const size_t tile_lds = sizeof(TileLds);
+  static_assert(2 * sizeof(TileLds) <= 160 * 1024, "two tile-sort workgroups must fit one CU's LDS");
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_OK(hipFuncSetAttribute((const void*)k_tile_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
+    HIP_OK(hipFuncSetAttribute((const void*)k_tile_sort<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
+    HIP_OK(hipFuncSetAttribute((const void*)k_tile_sort<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
     attr_set = true;
   }
   uint32_t h = 0;
@@ -626,7 +683,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
               "33-256:%lu 257-2k:%lu >2k:%lu | groups >2k:%lu\n", h, nL, totalL, bins[0], bins[1], bins[2], bins[3],
               bins[4], bins[5], bins[6], gb[6]);
     }
-    k_gather<<<grid(totalL), kT, 0, st>>>(L, P, nL, totalL, h, B);
+    HIP_OK(hipMemsetAsync(gmap, 0, (size_t)totalL * 4, st));
+    k_mark_groups<<<grid(nL), kT, 0, st>>>(P, nL, gmap);
+    HIP_OK(hipGetLastError());
+    scan_u32(ScanOp::Max, false, gmap, gmap, totalL, cnt + 7, scratch, st);
+    k_gather<<<grid(totalL), kT, 0, st>>>(L, P, gmap, totalL, h, B);
     HIP_OK(hipGetLastError());
     k_extract_large<<<grid(nL), kT, 0, st>>>(L, nL, h == 0 ? 1 : 0, large, cnt + 1);
     HIP_OK(hipGetLastError());
@@ -664,9 +725,10 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     if (h > 0) {
       const uint32_t ntiles = ceil_div(totalL, kWin);
       HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
-      k_tile_first<<<grid(nL), kT, 0, st>>>(P, nL, first);
+      k_tile_first<<<grid(nL), kT, 0, st>>>(P, nL, first, last);
       HIP_OK(hipGetLastError());
-      k_tile_sort<<<ntiles, kT, tile_lds, st>>>(L, nL, P, first, kbits, B, Ln, cnt + 3);
+      if (debug) k_tile_sort<true><<<ntiles, kT, tile_lds, st>>>(L, nL, first, last, kbits, B, Ln, cnt + 3, true, stamps);
+      else k_tile_sort<false><<<ntiles, kT, tile_lds, st>>>(L, nL, first, last, kbits, B, Ln, cnt + 3, true, stamps);
       HIP_OK(hipGetLastError());
     }
     read_counters();
@@ -680,9 +742,10 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       const uint32_t tot_small = hc[0];
       const uint32_t ntiles = ceil_div(tot_small, kWin);
       HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
-      k_tile_first<<<grid(n_small), kT, 0, st>>>(P, n_small, first);
+      k_tile_first<<<grid(n_small), kT, 0, st>>>(P, n_small, first, last);
       HIP_OK(hipGetLastError());
-      k_tile_sort<<<ntiles, kT, tile_lds, st>>>(small, n_small, P, first, kbits, B, Ln, cnt + 3);
+      if (debug) k_tile_sort<true><<<ntiles, kT, tile_lds, st>>>(small, n_small, first, last, kbits, B, Ln, cnt + 3, false, stamps);
+      else k_tile_sort<false><<<ntiles, kT, tile_lds, st>>>(small, n_small, first, last, kbits, B, Ln, cnt + 3, false, stamps);
       HIP_OK(hipGetLastError());
     }
     if (n_equal > 0) {
@@ -698,6 +761,13 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     std::swap(L, Ln);
     h = h == 0 ? 4 : h * 2;
     if (iters > 40) throw HipFailure(hipErrorUnknown);  // cannot happen for aperiodic roots
+  }
+  if (debug) {
+    uint64_t hs[8];
+    HIP_OK(hipMemcpyAsync(hs, stamps, 64, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    fprintf(stderr, "[bzg tile_sort stamps] tiles=%lu elems=%lu | load %lu  elems %lu  rank %lu  radix %lu  groups %lu  "
+            "output %lu (s_memtime ticks summed over workgroups)\n", hs[6], hs[7], hs[0], hs[1], hs[2], hs[3], hs[4], hs[5]);
   }
   k_bwt_out<<<grid(h_boff[nb]), kT, 0, st>>>(r.boff, nb, units, B.sa, r.blk, h_boff[nb], bwt);
   HIP_OK(hipGetLastError());
