@@ -109,6 +109,16 @@ __device__ __forceinline__ T block_incl_max(T v, T* sh) {
   return x > pre ? x : pre;
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2).  Map the
+// hardware workgroup index to a logical one so that every XCD walks a contiguous logical
+// range: neighbouring data stays in one L2.
+constexpr uint32_t kNumXcd = 8;
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
+  const uint32_t per = nwg / kNumXcd, rem = nwg % kNumXcd;
+  const uint32_t xcd = bid % kNumXcd, j = bid / kNumXcd;
+  return xcd < rem ? xcd * (per + 1) + j : rem * (per + 1) + (xcd - rem) * per + j;
+}
+
 // Lanes of the wave whose 8-bit value equals this lane's (among active lanes).
 __device__ __forceinline__ uint64_t match_byte(uint32_t d, uint64_t active) {
   uint64_t m = active;

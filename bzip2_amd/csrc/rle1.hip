@@ -284,12 +284,22 @@ __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x,
                                                   const uint32_t* __restrict__ crc_table_g,
                                                   const uint32_t* __restrict__ xp2_g,
                                                   uint32_t* __restrict__ bcrc) {
-  __shared__ uint32_t tab[256];
+  // slicing-by-8 tables for the MSB-first CRC: tab[k][b] = tab[0][b] advanced by k zero bytes
+  __shared__ uint32_t tab[8][256];
   __shared__ uint32_t xp2[48];
   __shared__ uint32_t part[kT];
   __shared__ uint64_t plen[kT];
   const int b = blockIdx.x;
-  tab[threadIdx.x] = crc_table_g[threadIdx.x];
+  {
+    uint32_t v = crc_table_g[threadIdx.x];
+    tab[0][threadIdx.x] = v;
+    __syncthreads();
+#pragma unroll
+    for (int k = 1; k < 8; k++) {
+      v = (v << 8) ^ tab[0][v >> 24];
+      tab[k][threadIdx.x] = v;
+    }
+  }
   if (threadIdx.x < 48) xp2[threadIdx.x] = xp2_g[threadIdx.x];
   __syncthreads();
   const uint64_t lo = binst[b], hi = binst[b + 1], len = hi - lo;
@@ -298,7 +308,15 @@ __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x,
   if (s > hi) s = hi;
   if (e > hi) e = hi;
   uint32_t c = 0;
-  for (uint64_t i = s; i < e; i++) c = (c << 8) ^ tab[(c >> 24) ^ x[i]];
+  uint64_t i = s;
+  for (; i < e && (i & 7); i++) c = (c << 8) ^ tab[0][(c >> 24) ^ x[i]];
+  for (; i + 8 <= e; i += 8) {
+    const uint2 w = *reinterpret_cast<const uint2*>(x + i);
+    const uint32_t a = c ^ bswap32(w.x), d = bswap32(w.y);
+    c = tab[7][a >> 24] ^ tab[6][(a >> 16) & 255u] ^ tab[5][(a >> 8) & 255u] ^ tab[4][a & 255u] ^
+        tab[3][d >> 24] ^ tab[2][(d >> 16) & 255u] ^ tab[1][(d >> 8) & 255u] ^ tab[0][d & 255u];
+  }
+  for (; i < e; i++) c = (c << 8) ^ tab[0][(c >> 24) ^ x[i]];
   part[threadIdx.x] = c;
   plen[threadIdx.x] = e - s;
   __syncthreads();

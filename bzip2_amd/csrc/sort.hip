@@ -28,9 +28,12 @@ namespace bzg {
 namespace {
 
 constexpr int kT = 256;
-constexpr uint32_t kSmall = 2048;   // max group size sorted in LDS
-constexpr uint32_t kWin = 2048;     // nominal tile window (tile <= kWin + kSmall - 1 elements)
-constexpr uint32_t kTileCap = 4096;
+constexpr uint32_t kSmall = 1024;   // max group size sorted in LDS
+constexpr uint32_t kWin = 1008;     // nominal tile window (tile <= kWin + kSmall - 1 elements)
+constexpr uint32_t kTileCap = 2048;
+constexpr uint32_t kPer = kTileCap / kT;  // tile elements per thread
+constexpr uint32_t kWaveSpan = kTileCap / (kT / 64);  // tile elements per wave in the radix
+static_assert(kWin + kSmall - 1 <= kTileCap && kPer % 4 == 0, "tile shape");
 constexpr uint32_t kDTile = 4096;   // elements per tile of a digit pass
 constexpr uint32_t kRankMax = 48;   // tiles whose groups are all this small sort by rank counting
 
@@ -262,15 +265,15 @@ struct TileLds {
   uint32_t keyA[kTileCap], valA[kTileCap], keyB[kTileCap], valB[kTileCap];
   uint16_t hist[4][256];  // per-wave digit counts / bases (<= kTileCap)
   // items start inside a kWin window and hold >= 2 elements: at most kWin / 2 per tile
-  uint32_t ioff[kWin / 2 + 8];  // tile-local offset of each item (+ end)
-  uint32_t istart[kWin / 2 + 8];
-  uint32_t iunit[kWin / 2 + 8];
-  uint32_t sh[8];
-  uint32_t misc[8];
+  uint32_t ioff[kWin / 2 + 1];  // tile-local offset of each item (+ end)
+  uint32_t istart[kWin / 2];
+  uint32_t iunit[kWin / 2];
+  uint32_t sh[kT / 64];
+  uint32_t misc[4];
 };
 
 // Stable LSD radix sort of n (<= kTileCap) (key, val) pairs in LDS over bits [0, nbits).
-// 4 waves; wave w owns elements [w*1024, w*1024+1024), visited 64 at a time in order.
+// 4 waves; wave w owns elements [w*kWaveSpan, (w+1)*kWaveSpan), visited 64 at a time in order.
 __device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*& keys, uint32_t*& vals) {
   uint32_t* kin = S.keyA;
   uint32_t* vin = S.valA;
@@ -280,10 +283,10 @@ __device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*
   for (uint32_t shift = 0; shift < nbits; shift += 8) {
     for (int i = threadIdx.x; i < 4 * 256 / 2; i += kT) reinterpret_cast<uint32_t*>(&S.hist[0][0])[i] = 0;
     __syncthreads();
-    uint32_t dig[16], loc[16];
+    uint32_t dig[kWaveSpan / 64], loc[kWaveSpan / 64];
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const uint32_t e = w * 1024 + j * 64 + lane;
+    for (int j = 0; j < (int)(kWaveSpan / 64); j++) {
+      const uint32_t e = w * kWaveSpan + j * 64 + lane;
       const bool act = e < n;
       const uint64_t amask = __ballot(act);
       uint32_t d = act ? (kin[e] >> shift) & 255u : 0u;
@@ -309,8 +312,8 @@ __device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const uint32_t e = w * 1024 + j * 64 + lane;
+    for (int j = 0; j < (int)(kWaveSpan / 64); j++) {
+      const uint32_t e = w * kWaveSpan + j * 64 + lane;
       if (e < n) {
         const uint32_t dst = S.hist[w][dig[j]] + loc[j];
         kout[dst] = kin[e];
@@ -395,21 +398,26 @@ __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small,
     for (uint32_t j = threadIdx.x; j < ni; j += kT)
       if (S.ioff[j + 1] > S.ioff[j]) owner[S.ioff[j]] = j;
     __syncthreads();
-    uint4 a = o4[threadIdx.x * 4], b = o4[threadIdx.x * 4 + 1], c = o4[threadIdx.x * 4 + 2], d = o4[threadIdx.x * 4 + 3];
-    uint32_t m = max(max(max(a.x, a.y), max(a.z, a.w)), max(max(b.x, b.y), max(b.z, b.w)));
-    m = max(m, max(max(max(c.x, c.y), max(c.z, c.w)), max(max(d.x, d.y), max(d.z, d.w))));
+    uint4 q4[kPer / 4];
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < (int)(kPer / 4); q++) {
+      q4[q] = o4[threadIdx.x * (kPer / 4) + q];
+      m = max(m, max(max(q4[q].x, q4[q].y), max(q4[q].z, q4[q].w)));
+    }
     const uint32_t incl = block_incl_max(m, S.sh);
     uint32_t run = __shfl_up(incl, 1);
     if (__lane_id() == 0) run = threadIdx.x >= 64 ? S.sh[(threadIdx.x >> 6) - 1] : 0u;
     if (threadIdx.x == 0) run = 0;
-#define BZG_RUNMAX(v) v = run = max(run, v)
-    BZG_RUNMAX(a.x); BZG_RUNMAX(a.y); BZG_RUNMAX(a.z); BZG_RUNMAX(a.w);
-    BZG_RUNMAX(b.x); BZG_RUNMAX(b.y); BZG_RUNMAX(b.z); BZG_RUNMAX(b.w);
-    BZG_RUNMAX(c.x); BZG_RUNMAX(c.y); BZG_RUNMAX(c.z); BZG_RUNMAX(c.w);
-    BZG_RUNMAX(d.x); BZG_RUNMAX(d.y); BZG_RUNMAX(d.z); BZG_RUNMAX(d.w);
-#undef BZG_RUNMAX
     __syncthreads();
-    o4[threadIdx.x * 4] = a; o4[threadIdx.x * 4 + 1] = b; o4[threadIdx.x * 4 + 2] = c; o4[threadIdx.x * 4 + 3] = d;
+#pragma unroll
+    for (int q = 0; q < (int)(kPer / 4); q++) {
+      q4[q].x = run = max(run, q4[q].x);
+      q4[q].y = run = max(run, q4[q].y);
+      q4[q].z = run = max(run, q4[q].z);
+      q4[q].w = run = max(run, q4[q].w);
+      o4[threadIdx.x * (kPer / 4) + q] = q4[q];
+    }
     __syncthreads();
   }
   for (uint32_t e = threadIdx.x; e < n; e += kT) {
@@ -456,20 +464,19 @@ __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small,
     lds_radix_sort(S, n, key_bits + item_bits, keys, vals);
     STAMP(3);
   }
-  // group detection over the sorted composite keys; thread t owns [16t, 16t+16)
-  const uint32_t e0 = threadIdx.x * 16;
-  uint32_t kq[16];
-  {
-    const uint4* k4 = reinterpret_cast<const uint4*>(keys + e0);
-    const uint4 a = k4[0], b = k4[1], c = k4[2], d = k4[3];
-    kq[0] = a.x; kq[1] = a.y; kq[2] = a.z; kq[3] = a.w; kq[4] = b.x; kq[5] = b.y; kq[6] = b.z; kq[7] = b.w;
-    kq[8] = c.x; kq[9] = c.y; kq[10] = c.z; kq[11] = c.w; kq[12] = d.x; kq[13] = d.y; kq[14] = d.z; kq[15] = d.w;
+  // group detection over the sorted composite keys; thread t owns [kPer*t, kPer*t + kPer)
+  const uint32_t e0 = threadIdx.x * kPer;
+  uint32_t kq[kPer];
+#pragma unroll
+  for (int q = 0; q < (int)(kPer / 4); q++) {
+    const uint4 a = reinterpret_cast<const uint4*>(keys + e0)[q];
+    kq[4 * q] = a.x; kq[4 * q + 1] = a.y; kq[4 * q + 2] = a.z; kq[4 * q + 3] = a.w;
   }
   uint32_t smask = 0;  // bit q: element e0 + q starts a group
   {
     uint32_t prev = (e0 > 0 && e0 <= n) ? keys[e0 - 1] : 0u;
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
+    for (int q = 0; q < (int)kPer; q++) {
       const uint32_t e = e0 + q;
       if (e < n && (e == 0 || kq[q] != prev)) smask |= 1u << q;
       prev = kq[q];
@@ -483,17 +490,15 @@ __global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small,
   uint32_t* gid = (vals == S.valA) ? S.valB : S.valA;
   {
     uint32_t o = incl - starts;
-    uint32_t gq[16];
+    uint32_t gq[kPer];
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
+    for (int q = 0; q < (int)kPer; q++) {
       if ((smask >> q) & 1u) gpos[o++] = e0 + q;
       gq[q] = o - 1;  // unused for e >= n
     }
-    uint4* g4 = reinterpret_cast<uint4*>(gid + e0);
-    g4[0] = make_uint4(gq[0], gq[1], gq[2], gq[3]);
-    g4[1] = make_uint4(gq[4], gq[5], gq[6], gq[7]);
-    g4[2] = make_uint4(gq[8], gq[9], gq[10], gq[11]);
-    g4[3] = make_uint4(gq[12], gq[13], gq[14], gq[15]);
+#pragma unroll
+    for (int q = 0; q < (int)(kPer / 4); q++)
+      reinterpret_cast<uint4*>(gid + e0)[q] = make_uint4(gq[4 * q], gq[4 * q + 1], gq[4 * q + 2], gq[4 * q + 3]);
   }
   if (threadIdx.x == 0) gpos[ngroups] = n;
   __syncthreads();
@@ -558,18 +563,29 @@ __global__ void __launch_bounds__(kT) k_equal(const Grp* __restrict__ G, uint32_
 
 // ---------------------------------------------------------------- output
 // bwt[boff[b] + q] = root[(SA[sbase + q / k] - 1) mod p] for q < n_b, k = n_b / p.
-__global__ void k_bwt_out(const uint32_t* __restrict__ boff, uint32_t nb, const Unit* __restrict__ units,
-                          const uint32_t* __restrict__ sa, const uint8_t* __restrict__ text, uint32_t total,
-                          uint8_t* __restrict__ bwt) {
-  uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= total) return;
-  uint32_t b = upper_idx(boff, nb, x);
-  const Unit U = units[b];
-  const uint32_t nbytes = boff[b + 1] - boff[b];
-  const uint32_t k = nbytes / U.len;
-  const uint32_t q = x - boff[b];
-  const uint32_t v = sa[U.sbase + q / k];
-  bwt[x] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
+// Last column: bwt[x] = text[SA[x / k] - 1] (cyclically) for the k-fold repeated root.
+// Four output bytes per thread; XCD-aware so that each L2 serves a few blocks' text.
+__global__ void __launch_bounds__(kT) k_bwt_out(const uint32_t* __restrict__ boff, uint32_t nb,
+                                                const Unit* __restrict__ units, const uint32_t* __restrict__ sa,
+                                                const uint8_t* __restrict__ text, uint32_t total,
+                                                uint8_t* __restrict__ bwt) {
+  const uint32_t wg = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t x0 = (wg * kT + threadIdx.x) * 4;
+  if (x0 >= total) return;
+  uint32_t b = upper_idx(boff, nb, x0);
+  uint32_t out = 0;
+  const uint32_t xe = min(x0 + 4, total);
+  for (uint32_t x = x0; x < xe; x++) {
+    while (x >= boff[b + 1]) b++;
+    const Unit U = units[b];
+    const uint32_t k = (boff[b + 1] - boff[b]) / U.len;
+    const uint32_t q = x - boff[b];
+    const uint32_t v = sa[U.sbase + (k == 1 ? q : q / k)];
+    out |= (uint32_t)text[U.toff + (v == 0 ? U.len - 1 : v - 1)] << (8 * (x - x0));
+  }
+  if (xe - x0 == 4) *reinterpret_cast<uint32_t*>(bwt + x0) = out;
+  else
+    for (uint32_t x = x0; x < xe; x++) bwt[x] = (uint8_t)(out >> (8 * (x - x0)));
 }
 
 __global__ void k_rank0(const Unit* __restrict__ units, uint32_t nb, const uint32_t* __restrict__ isa,
@@ -646,7 +662,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   if (debug) HIP_OK(hipMemsetAsync(stamps, 0, 128, st));
   std::vector<uint32_t> hsz;  // debug: sizes of the groups in L
   const size_t tile_lds = sizeof(TileLds);
-  static_assert(2 * sizeof(TileLds) <= 160 * 1024, "two tile-sort workgroups must fit one CU's LDS");
+  static_assert(4 * sizeof(TileLds) <= 160 * 1024, "four tile-sort workgroups must fit one CU's LDS");
   static bool attr_set = false;
   if (!attr_set) {
     HIP_OK(hipFuncSetAttribute((const void*)k_tile_sort<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
@@ -769,7 +785,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     fprintf(stderr, "[bzg tile_sort stamps] tiles=%lu elems=%lu | load %lu  elems %lu  rank %lu  radix %lu  groups %lu  "
             "output %lu (s_memtime ticks summed over workgroups)\n", hs[6], hs[7], hs[0], hs[1], hs[2], hs[3], hs[4], hs[5]);
   }
-  k_bwt_out<<<grid(h_boff[nb]), kT, 0, st>>>(r.boff, nb, units, B.sa, r.blk, h_boff[nb], bwt);
+  k_bwt_out<<<grid(ceil_div64(h_boff[nb], 4)), kT, 0, st>>>(r.boff, nb, units, B.sa, r.blk, h_boff[nb], bwt);
   HIP_OK(hipGetLastError());
   k_rank0<<<grid(nb), kT, 0, st>>>(units, nb, B.isa, rank0);
   HIP_OK(hipGetLastError());
