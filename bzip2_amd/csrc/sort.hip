@@ -3,595 +3,658 @@
 // Replaces the reference's divsufsort (blocksort.c:1503-1545).  For an aperiodic block all
 // rotations are distinct, so any correct sort yields the reference's last column and
 // origPtr (parity fact 3).  Periodic blocks (w^k) are reduced to their
-// primitive root w here; the tie rank among the k identical copies of rotation 0 is resolved
-// on the host (resolver.cpp, A5).
+// primitive root w; the tie rank among the k identical copies of rotation 0 is resolved on
+// the host (resolver.cpp, A5).
 //
-// Algorithm: prefix doubling (Manber-Myers / Larsson-Sadakane) over the rotations of every
-// unit at once, with a segmented sort specialised by group size:
-//   * every slot s of unit u holds SA[s] (a rotation start) and ISA[sbase_u + i] holds the
-//     slot of the first member of i's group ("rank"), a refinement consistent with the true
-//     order of rotations at depth >= h;
-//   * iteration h: for every member of an unsorted group, key = rank(i + h) (h = 0: the first
-//     four bytes); groups larger than kSmall are split by global MSD counting passes on key
-//     digits; groups/buckets of <= kSmall elements are packed into LDS tiles and finished by
-//     an in-LDS stable LSD radix sort on (item, key);
-//   * new groups of size >= 2 form the next iteration's list; h doubles.
-// All keys of an iteration are gathered before any rank is rewritten.
+// The sort is a string sort keyed directly by the block text (read through L2: a block is
+// <= 900 kB and the workgroups of an XCD walk the blocks in order), not by rank arrays that
+// would have to be gathered from HBM:
+//   S1  MSD byte passes: every block is split into buckets by its leading characters (one
+//       counting pass per character over the buckets still larger than kBig).  Buckets are
+//       emitted into size-class lists (2-8, 9-16, 17-32, 33-64, 65-128, 129-256) at offsets
+//       from one class-major scan per pass.
+//   S2  every class is sorted by one wave per 64 / kSeg buckets: the next 8 characters of
+//       each rotation are gathered, a bitonic network in registers sorts the segment by
+//       (run start, key, index), unique rotations write SA / BWT byte / origPtr, and tied
+//       runs repeat with the next 8 characters (2-8: rank counting on 16 characters).
+//   S3  groups still equal after kDWave characters (long repeats) or S1 buckets still larger
+//       than kBig after kDBig characters go to prefix doubling (sortdbl.hip) over ISA ranks
+//       built for the affected blocks only.
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "scan.h"
-#include "stages.h"
+#include "sort_common.h"
 
 namespace bzg {
 
 namespace {
 
 constexpr int kT = 256;
-constexpr uint32_t kSmall = 1024;   // max group size sorted in LDS
-constexpr uint32_t kWin = 1008;     // nominal tile window (tile <= kWin + kSmall - 1 elements)
-constexpr uint32_t kTileCap = 2048;
-constexpr uint32_t kPer = kTileCap / kT;  // tile elements per thread
-constexpr uint32_t kWaveSpan = kTileCap / (kT / 64);  // tile elements per wave in the radix
-static_assert(kWin + kSmall - 1 <= kTileCap && kPer % 4 == 0, "tile shape");
-constexpr uint32_t kDTile = 4096;   // elements per tile of a digit pass
-constexpr uint32_t kRankMax = 48;   // tiles whose groups are all this small sort by rank counting
+constexpr uint32_t kBig = 256;        // buckets larger than this are split by S1 byte passes
+constexpr uint32_t kDTile = 4096;     // rotations per workgroup in an S1 pass
+constexpr uint32_t kPerT = kDTile / kT;
+constexpr uint32_t kDBig = 16;        // S1 byte passes stop at this depth (then doubling)
+constexpr uint32_t kDWave = 1024;     // S2 rounds stop at this depth (then doubling)
+constexpr int kNCls = 7;              // size classes 0..5 (S2) and 6 (next S1 pass)
+constexpr uint32_t kClsMax[6] = {8, 16, 32, 64, 128, 256};
 
-struct Unit {
-  uint32_t sbase, len, toff, pad;
-};
-struct Grp {
-  uint32_t start, size, unit, flags;  // flags bit0: data lives in the alt (sa2/key2) buffers
-};
+__host__ __device__ __forceinline__ uint32_t size_cls(uint32_t n) {
+  return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= 256 ? 5u : 6u;
+}
 
-struct SortBufs {
-  uint32_t *sa, *isa, *key, *sa2, *key2;
-  const uint8_t* text;
-  const Unit* units;
+struct SortOut {
+  uint8_t* bwt;      // last column of aperiodic units, same offsets as the blocks
+  uint32_t* rank0;   // slot of rotation 0 relative to its unit
+  Grp* deep;         // groups left for the doubling fallback
+  uint32_t* n_deep;
 };
 
-// ---------------------------------------------------------------------------------
-// Binary search: largest g with P[g] <= x (P is an exclusive prefix, P[0] = 0).
-__device__ __forceinline__ uint32_t upper_idx(const uint32_t* __restrict__ P, uint32_t n, uint32_t x) {
-  uint32_t lo = 0, hi = n;  // answer in [lo, hi)
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (P[mid] <= x) lo = mid;
-    else hi = mid;
+struct ClsLists {
+  Grp* l[kNCls];
+  uint32_t base[kNCls];  // entries already in each list before this pass
+};
+
+// ---------------------------------------------------------------- text access
+// (v + d) mod len for v < len.
+__device__ __forceinline__ uint32_t cyc_pos(uint32_t v, uint32_t d, uint32_t len) {
+  uint32_t q = v + d;
+  if (q >= len) {
+    q -= len;
+    if (q >= len) q %= len;
   }
-  return lo;
+  return q;
 }
 
-__global__ void k_units_to_groups(const Unit* __restrict__ units, uint32_t nu, Grp* __restrict__ L,
-                                  uint32_t* __restrict__ sizes) {
-  uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= nu) return;
-  L[u] = Grp{units[u].sbase, units[u].len, u, 0};
-  sizes[u] = units[u].len;
+// Big-endian 4 bytes at p (any alignment; every text buffer has >= 16 bytes of padding).
+__device__ __forceinline__ uint32_t ld_be4(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  return __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u)));
 }
 
-__global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ sizes) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) sizes[g] = L[g].size;
+// The 4 characters of the cyclic unit text t[0..len) starting at q (< len).
+__device__ __forceinline__ uint32_t text_key4(const uint8_t* t, uint32_t len, uint32_t q) {
+  if (q + 4 <= len) return ld_be4(t + q);
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < 4; i++) k = (k << 8) | t[(q + i) % len];
+  return k;
+}
+
+// The 16 characters starting at q, as four big-endian words.
+__device__ __forceinline__ void text_key16(const uint8_t* t, uint32_t len, uint32_t q, uint32_t (&k)[4]) {
+  if (q + 16 <= len) {
+    const uintptr_t a = (uintptr_t)(t + q);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3u);  // byte shift
+    const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+    k[0] = __builtin_bswap32(__builtin_amdgcn_alignbyte(x1, x0, sh));
+    k[1] = __builtin_bswap32(__builtin_amdgcn_alignbyte(x2, x1, sh));
+    k[2] = __builtin_bswap32(__builtin_amdgcn_alignbyte(x3, x2, sh));
+    k[3] = __builtin_bswap32(__builtin_amdgcn_alignbyte(x4, x3, sh));
+    return;
+  }
+  for (int w = 0; w < 4; w++) {
+    uint32_t x = 0;
+    for (uint32_t i = 0; i < 4; i++) x = (x << 8) | t[(q + 4 * w + i) % len];
+    k[w] = x;
+  }
+}
+
+// A rotation v of `unit` is fully ordered at global slot `slot`: SA, BWT byte, origPtr.
+__device__ __forceinline__ void emit_final(const SortBufs& B, const SortOut& O, const Unit& U, uint32_t unit,
+                                           uint32_t slot, uint32_t v, bool write_sa) {
+  if (write_sa) B.sa[slot] = v;
+  const uint32_t r = slot - U.sbase;
+  if (U.k == 1) O.bwt[U.toff + r] = B.text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
+  if (v == 0) O.rank0[unit] = r;
+}
+
+// ---------------------------------------------------------------- setup
+// Units of one rotation are done; the others are classed by size: <= kBig rotations go
+// straight to S2, larger ones to the S1 byte passes.  (Few units: one atomic per wave.)
+__global__ void k_init_units(const Unit* __restrict__ units, uint32_t nu, SortBufs B, SortOut O, ClsLists C,
+                             uint32_t* __restrict__ ccount) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = u < nu;
+  Unit U{0, 0, 0, 1};
+  if (valid) U = units[u];
+  if (valid && U.len == 1) emit_final(B, O, U, u, U.sbase, 0, true);
+  const uint32_t c = (valid && U.len >= 2) ? size_cls(U.len) : 0xffu;
+  for (int k = 0; k < kNCls; k++) {
+    const uint32_t pos = wave_append(ccount + k, c == (uint32_t)k);
+    if (c == (uint32_t)k) C.l[k][pos] = Grp{U.sbase, U.len, u, kGrpIdent};
+  }
 }
 
 __global__ void k_group_tiles(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ cnt) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n) cnt[g] = ceil_div(L[g].size, kDTile);
 }
 
-// SA[s] = s - sbase for every slot (identity order before sorting).
-__global__ void k_init_sa(const Grp* __restrict__ L, const uint32_t* __restrict__ P, uint32_t nL,
-                          uint32_t total, uint32_t* __restrict__ sa) {
-  uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= total) return;
-  uint32_t g = upper_idx(P, nL, x);
-  Grp G = L[g];
-  uint32_t off = x - P[g];
-  sa[G.start + off] = off;
-}
-
-// Element -> group map: gmap[P[g]] = g on a zeroed array, then an inclusive max-scan.
-__global__ void k_mark_groups(const uint32_t* __restrict__ P, uint32_t nL, uint32_t* __restrict__ gmap) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < nL) gmap[P[g]] = g;
-}
-
-// key[s] for every member of every group in L.
-__global__ void __launch_bounds__(kT) k_gather(const Grp* __restrict__ L, const uint32_t* __restrict__ P,
-                                               const uint32_t* __restrict__ gmap, uint32_t total, uint32_t h,
-                                               SortBufs B) {
-  uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= total) return;
-  const uint32_t g = gmap[x];
-  const Grp G = L[g];
-  const uint32_t s = G.start + (x - P[g]);
-  const Unit U = B.units[G.unit];
-  const uint32_t i = B.sa[s];
-  uint32_t k;
-  if (h == 0) {
-    const uint8_t* t = B.text + U.toff;
-    uint32_t i1 = i + 1 >= U.len ? i + 1 - U.len : i + 1;
-    uint32_t i2 = i1 + 1 >= U.len ? i1 + 1 - U.len : i1 + 1;
-    uint32_t i3 = i2 + 1 >= U.len ? i2 + 1 - U.len : i2 + 1;
-    k = ((uint32_t)t[i] << 24) | ((uint32_t)t[i1] << 16) | ((uint32_t)t[i2] << 8) | (uint32_t)t[i3];
-  } else {
-    uint32_t hh = h % U.len;
-    uint32_t j = i + hh;
-    if (j >= U.len) j -= U.len;
-    k = B.isa[U.sbase + j] - U.sbase;
+// ---------------------------------------------------------------- S1 byte passes
+// Every workgroup takes kDTile rotations of one group; loads are issued kPerT at a time.
+__device__ __forceinline__ void s1_load(const SortBufs& B, const Grp& gr, const Unit& U, uint32_t lo, uint32_t hi,
+                                        uint32_t (&vv)[kPerT], uint32_t (&dd)[kPerT]) {
+  const uint32_t* src = (gr.flags & kGrpAlt) ? B.sa2 : B.sa;
+  const bool ident = gr.flags & kGrpIdent;
+  const uint32_t depth = grp_depth(gr);
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++) {
+    const uint32_t e = lo + i * kT + threadIdx.x;
+    vv[i] = e < hi ? (ident ? e : src[gr.start + e]) : 0u;
   }
-  B.key[s] = k;
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++) {
+    const uint32_t e = lo + i * kT + threadIdx.x;
+    dd[i] = e < hi ? (uint32_t)B.text[U.toff + cyc_pos(vv[i], depth, U.len)] : 0u;
+  }
 }
 
-// Groups too large for an LDS tile go to the digit passes; the rest are tile-sorted in place
-// from L (the tiles skip the large ones).  Large groups are rare, so appends are cheap.
-__global__ void k_extract_large(const Grp* __restrict__ L, uint32_t nL, int force_all, Grp* __restrict__ large,
-                                uint32_t* __restrict__ n_large) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = g < nL;
-  Grp G{0, 0, 0, 0};
-  if (valid) G = L[g];
-  const bool big = valid && (force_all || G.size > kSmall);
-  const uint32_t pl = wave_append(n_large, big);
-  if (big) large[pl] = G;
-}
-
-// ---------------------------------------------------------------- digit passes (large)
-__global__ void __launch_bounds__(kT) k_dhist(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
-                                              uint32_t shift, SortBufs B, uint32_t* __restrict__ hist) {
+__global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+                                                SortBufs B, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[256];
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const uint32_t g = upper_idx(TP, nG, t);
   const Grp gr = G[g];
-  const uint32_t c = t - TP[g];
-  const uint32_t lo = c * kDTile, hi = min(gr.size, lo + kDTile);
-  const uint32_t* kk = (gr.flags & 1) ? B.key2 : B.key;
+  const Unit U = B.units[gr.unit];
+  const uint32_t lo = (t - TP[g]) * kDTile, hi = min(gr.size, lo + kDTile);
   h[threadIdx.x] = 0;
+  uint32_t vv[kPerT], dd[kPerT];
+  s1_load(B, gr, U, lo, hi, vv, dd);
   __syncthreads();
-  for (uint32_t e = lo + threadIdx.x; e < hi; e += kT) atomicAdd(&h[(kk[gr.start + e] >> shift) & 255u], 1u);
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++)
+    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[dd[i]], 1u);
   __syncthreads();
   hist[(size_t)t * 256 + threadIdx.x] = h[threadIdx.x];
 }
 
-// One workgroup per large group: bucket bases, per-tile offsets, bucket emission.
-// mode 0: emit small buckets to `small`, large to `next`;  mode 1 (forced): all to `next`;
-// mode 2 (last digit): small to `small`, large to `equal`.
-__global__ void __launch_bounds__(kT) k_doff(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
-                                             uint32_t* __restrict__ hist, uint32_t* __restrict__ tot, int mode,
-                                             Grp* __restrict__ small, uint32_t* __restrict__ n_small,
-                                             Grp* __restrict__ next, uint32_t* __restrict__ n_next,
-                                             Grp* __restrict__ equal, uint32_t* __restrict__ n_equal) {
+__device__ __forceinline__ uint32_t bucket_cls(uint32_t total, uint32_t depth) {
+  if (total < 2) return 0xffu;
+  const uint32_t c = size_cls(total);
+  return (c == 6 && depth >= kDBig) ? 7u : c;  // 7: still big after kDBig characters
+}
+
+// One workgroup per group: bucket totals and bases, per-tile offsets, and the number of
+// buckets of every size class (class-major: ccnt[c * nG + g]).
+__global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+                                               uint32_t* __restrict__ hist, uint32_t* __restrict__ tot,
+                                               uint32_t* __restrict__ ccnt, Grp* __restrict__ deep,
+                                               uint32_t* __restrict__ n_deep) {
   __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t cc[kNCls + 1];
   const uint32_t g = blockIdx.x;
   const Grp gr = G[g];
   const uint32_t t0 = TP[g], t1 = t0 + ceil_div(gr.size, kDTile);
   const uint32_t d = threadIdx.x;
+  if (d <= (uint32_t)kNCls) cc[d] = 0;
   uint32_t total = 0;
   for (uint32_t t = t0; t < t1; t++) total += hist[(size_t)t * 256 + d];
-  uint32_t incl = block_incl_sum(total, sh, (uint32_t*)nullptr);
-  uint32_t base = gr.start + incl - total;
+  const uint32_t incl = block_incl_sum(total, sh, (uint32_t*)nullptr);
+  const uint32_t base = gr.start + incl - total;
   tot[(size_t)g * 256 + d] = total;
   uint32_t run = base;
   for (uint32_t t = t0; t < t1; t++) {
-    uint32_t c = hist[(size_t)t * 256 + d];
+    const uint32_t c = hist[(size_t)t * 256 + d];
     hist[(size_t)t * 256 + d] = run;
     run += c;
   }
-  const Grp nb{base, total, gr.unit, gr.flags ^ 1u};
-  const bool emit = total >= 2;
-  const bool to_next = emit && (mode == 1 || (total > kSmall && mode == 0));
-  const bool to_small = emit && !to_next && total <= kSmall;
-  const bool to_equal = emit && !to_next && !to_small;
-  const uint32_t pn = wave_append(n_next, to_next);
-  const uint32_t ps = wave_append(n_small, to_small);
-  const uint32_t pe = wave_append(n_equal, to_equal);
-  if (to_next) next[pn] = nb;
-  if (to_small) small[ps] = nb;
-  if (to_equal) equal[pe] = nb;
+  const uint32_t depth = grp_depth(gr) + 1;
+  const uint32_t cl = bucket_cls(total, depth);
+#pragma unroll
+  for (int k = 0; k < kNCls; k++) {
+    const uint32_t n = (uint32_t)__popcll(__ballot(cl == (uint32_t)k));
+    if (__lane_id() == 0 && n) atomicAdd(&cc[k], n);
+  }
+  if (cl == 7u) {  // rare: a bucket still larger than kBig after kDBig characters
+    const uint32_t dst_alt = (gr.flags & kGrpIdent) ? 0u : ((gr.flags & kGrpAlt) ^ 1u);
+    deep[atomicAdd(n_deep, 1u)] = Grp{base, total, gr.unit, dst_alt | (depth << 2)};
+  }
+  __syncthreads();
+  if (d < (uint32_t)kNCls) ccnt[(size_t)d * nG + g] = cc[d];
 }
 
-__global__ void __launch_bounds__(kT) k_dscatter(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
-                                                 uint32_t shift, SortBufs B, const uint32_t* __restrict__ off,
-                                                 const uint32_t* __restrict__ tot) {
+// Scatter of one tile into the bucket order; the first tile of a group also emits the
+// group's buckets into the class lists (cscan: exclusive scan of ccnt).
+__global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+                                                   SortBufs B, SortOut O, const uint32_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ tot, const uint32_t* __restrict__ cscan,
+                                                   ClsLists C) {
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t base[256];
   __shared__ uint32_t single[256];
-  const uint32_t t = blockIdx.x;
+  __shared__ uint32_t wc[kT / 64][kNCls + 1];
+  const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const uint32_t g = upper_idx(TP, nG, t);
   const Grp gr = G[g];
-  const uint32_t c = t - TP[g];
-  const uint32_t lo = c * kDTile, hi = min(gr.size, lo + kDTile);
-  const bool alt = gr.flags & 1;
-  const uint32_t* ks = alt ? B.key2 : B.key;
-  const uint32_t* vs = alt ? B.sa2 : B.sa;
-  uint32_t* kd = alt ? B.key : B.key2;
-  uint32_t* vd = alt ? B.sa : B.sa2;
-  cnt[threadIdx.x] = 0;
-  base[threadIdx.x] = off[(size_t)t * 256 + threadIdx.x];
-  single[threadIdx.x] = tot[(size_t)g * 256 + threadIdx.x] == 1;
+  const Unit U = B.units[gr.unit];
+  const uint32_t lo = (t - TP[g]) * kDTile, hi = min(gr.size, lo + kDTile);
+  const bool dst_alt = !(gr.flags & kGrpIdent) && !(gr.flags & kGrpAlt);
+  uint32_t* dst = dst_alt ? B.sa2 : B.sa;
+  const uint32_t d = threadIdx.x;
+  const uint32_t total = tot[(size_t)g * 256 + d];
+  cnt[d] = 0;
+  base[d] = off[(size_t)t * 256 + d];
+  single[d] = total == 1;
+  uint32_t vv[kPerT], dd[kPerT];
+  s1_load(B, gr, U, lo, hi, vv, dd);
   __syncthreads();
-  const uint32_t sb = B.units[gr.unit].sbase;
-  for (uint32_t e = lo + threadIdx.x; e < hi; e += kT) {
-    const uint32_t k = ks[gr.start + e], v = vs[gr.start + e];
-    const uint32_t d = (k >> shift) & 255u;
-    const uint32_t pos = base[d] + atomicAdd(&cnt[d], 1u);
-    kd[pos] = k;
-    vd[pos] = v;
-    if (single[d]) B.isa[sb + v] = pos;  // a bucket of one: its rotation is now fully ordered
-  }
-}
-
-// Singletons scattered into the alt buffers move to the primary SA.  (Writing them to the
-// primary SA inside k_dscatter would race with other workgroups still reading it.)
-__global__ void __launch_bounds__(kT) k_dsingle(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
-                                                SortBufs B, const uint32_t* __restrict__ tot) {
-  __shared__ uint32_t base[257];
-  __shared__ uint32_t sh[kT / 64];
-  const uint32_t t = blockIdx.x;
-  const uint32_t g = upper_idx(TP, nG, t);
-  const Grp gr = G[g];
-  if (gr.flags & 1) return;  // data came from alt: singletons already landed in the primary SA
-  const uint32_t c = t - TP[g];
-  const uint32_t lo = c * kDTile, hi = min(gr.size, lo + kDTile);
-  const uint32_t tv = tot[(size_t)g * 256 + threadIdx.x];
-  const uint32_t incl = block_incl_sum(tv, sh, (uint32_t*)nullptr);
-  base[threadIdx.x] = incl - tv;
-  if (threadIdx.x == kT - 1) base[256] = incl;
-  __syncthreads();
-  for (uint32_t e = lo + threadIdx.x; e < hi; e += kT) {
-    uint32_t a = 0, b = 256;  // bucket d with base[d] <= e < base[d+1]
-    while (b - a > 1) {
-      const uint32_t m = (a + b) >> 1;
-      if (base[m] <= e) a = m;
-      else b = m;
+  uint32_t pos[kPerT];
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++)
+    pos[i] = (lo + i * kT + threadIdx.x < hi) ? base[dd[i]] + atomicAdd(&cnt[dd[i]], 1u) : 0u;
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++) {
+    if (lo + i * kT + threadIdx.x < hi) {
+      dst[pos[i]] = vv[i];
+      // a bucket of one: this rotation is ordered (its primary-SA copy is made by
+      // k_s1_single, since other workgroups may still read the primary SA in this pass)
+      if (single[dd[i]]) emit_final(B, O, U, gr.unit, pos[i], vv[i], !dst_alt);
     }
-    if (base[a + 1] - base[a] == 1) B.sa[gr.start + e] = B.sa2[gr.start + e];
+  }
+  if (t != TP[g]) return;
+  // ---- bucket emission (digit order within the group)
+  const uint32_t depth = grp_depth(gr) + 1;
+  const uint32_t cl = bucket_cls(total, depth);
+  const uint32_t w = d >> 6;
+  uint32_t rank = 0;
+#pragma unroll
+  for (int k = 0; k < kNCls; k++) {
+    const uint64_t m = __ballot(cl == (uint32_t)k);
+    if (cl == (uint32_t)k) rank = (uint32_t)__popcll(m & lanemask_lt());
+    if (__lane_id() == 0) wc[w][k] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (cl < (uint32_t)kNCls) {
+    for (uint32_t x = 0; x < w; x++) rank += wc[x][cl];
+    const uint32_t p = C.base[cl] + cscan[(size_t)cl * nG + g] - cscan[(size_t)cl * nG] + rank;
+    C.l[cl][p] = Grp{base[d], total, gr.unit, (dst_alt ? kGrpAlt : 0u) | (depth << 2)};
   }
 }
 
-// ---------------------------------------------------------------- small groups (LDS)
-// tile index of item i = P[i] / kWin; mark the first item of each tile and one past its last.
-__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_t* __restrict__ first,
-                             uint32_t* __restrict__ last) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t t = P[i] / kWin;
-  if (i == 0 || P[i - 1] / kWin != t) first[t] = i;
-  if (i == n - 1 || P[i + 1] / kWin != t) last[t] = i + 1;
+__global__ void __launch_bounds__(kT) k_s1_single(const Grp* __restrict__ G, SortBufs B, const uint32_t* __restrict__ tot) {
+  __shared__ uint32_t sh[kT / 64];
+  const Grp gr = G[blockIdx.x];
+  if ((gr.flags & kGrpIdent) || (gr.flags & kGrpAlt)) return;  // pass wrote the primary SA
+  const uint32_t total = tot[(size_t)blockIdx.x * 256 + threadIdx.x];
+  const uint32_t incl = block_incl_sum(total, sh, (uint32_t*)nullptr);
+  const uint32_t s = gr.start + incl - total;
+  if (total == 1) B.sa[s] = B.sa2[s];
 }
 
-struct TileLds {
-  uint32_t keyA[kTileCap], valA[kTileCap], keyB[kTileCap], valB[kTileCap];
-  uint16_t hist[4][256];  // per-wave digit counts / bases (<= kTileCap)
-  // items start inside a kWin window and hold >= 2 elements: at most kWin / 2 per tile
-  uint32_t ioff[kWin / 2 + 1];  // tile-local offset of each item (+ end)
-  uint32_t istart[kWin / 2];
-  uint32_t iunit[kWin / 2];
-  uint32_t sh[kT / 64];
-  uint32_t misc[4];
+// out[c] = start of class c in the class-major scan (c < kNCls), out[kNCls] = total.
+__global__ void k_cls_bounds(const uint32_t* __restrict__ cscan, uint32_t nG, const uint32_t* __restrict__ total,
+                             uint32_t* __restrict__ out) {
+  const uint32_t c = threadIdx.x;
+  if (c < (uint32_t)kNCls) out[c] = cscan[(size_t)c * nG];
+  if (c == (uint32_t)kNCls) out[c] = *total;
+}
+
+// ---------------------------------------------------------------- S2
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// The 8 characters starting at q (< len) as two big-endian words.
+__device__ __forceinline__ void text_key8(const uint8_t* t, uint32_t len, uint32_t q, uint32_t& hi, uint32_t& lo) {
+  if (q + 8 <= len) {
+    const uintptr_t a = (uintptr_t)(t + q);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3u);
+    const uint32_t x0 = w[0], x1 = w[1], x2 = w[2];
+    hi = __builtin_bswap32(__builtin_amdgcn_alignbyte(x1, x0, sh));
+    lo = __builtin_bswap32(__builtin_amdgcn_alignbyte(x2, x1, sh));
+    return;
+  }
+  uint32_t x = 0, y = 0;
+  for (uint32_t i = 0; i < 4; i++) x = (x << 8) | t[(q + i) % len];
+  for (uint32_t i = 4; i < 8; i++) y = (y << 8) | t[(q + i) % len];
+  hi = x;
+  lo = y;
+}
+
+// ---- tiny buckets: lane l takes rotation l % 8 of bucket 8 * wave + l / 8.  Every step
+// compares the next 16 characters with the rotations of its bucket still tied with it
+// (same class, named by its first lane) and adds the smaller ones to its position.
+__global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint32_t n_tiny, SortBufs B, SortOut O) {
+  const uint32_t lane = __lane_id();
+  const uint32_t wv = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+  const uint32_t bi = wv * 8 + lane / 8, el = lane % 8;
+  bool act = false;
+  uint32_t s0 = 0, d = 0, v = 0, unit = 0;
+  if (bi < n_tiny) {
+    const Grp g = tiny[bi];
+    if (el < g.size) {
+      act = true;
+      s0 = g.start;
+      d = grp_depth(g);
+      unit = g.unit;
+      v = (g.flags & kGrpIdent) ? el : ((g.flags & kGrpAlt) ? B.sa2 : B.sa)[s0 + el];
+    }
+  }
+  if (!__ballot(act)) return;
+  Unit U{0, 1, 0, 1};
+  if (act) U = B.units[unit];
+  const uint8_t* t = B.text + U.toff;
+  uint8_t lastc = 0;  // BWT byte of this rotation, loaded with the first key
+  if (act) lastc = t[v == 0 ? U.len - 1 : v - 1];
+  bool done = !act;
+  uint32_t cls = act ? (lane & ~7u) : 0xffffffffu;
+  uint32_t pos = 0;
+  const int base = (int)(lane & ~7u);
+  for (;;) {
+    const uint64_t live = __ballot(!done);
+    if (live == 0) break;
+    if (d >= kDWave) {  // still tied after kDWave characters: leave to the doubling fallback
+      if (!done) {
+        const uint64_t mates = match_byte(cls, live);
+        const uint32_t r = (uint32_t)__popcll(mates & lanemask_lt());
+        B.sa[s0 + pos + r] = v;
+        if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, (uint32_t)__popcll(mates), unit, d << 2};
+      }
+      break;
+    }
+    uint32_t k[4] = {0u, 0u, 0u, 0u};
+    if (!done) text_key16(t, U.len, cyc_pos(v, d, U.len), k);
+    const uint64_t khi = ((uint64_t)k[0] << 32) | k[1], klo = ((uint64_t)k[2] << 32) | k[3];
+    uint32_t lt = 0, eq = 0, rep = lane;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int src = base + j;
+      const uint32_t cj = (uint32_t)__shfl((int)cls, src, 64);
+      const uint64_t hj = __shfl(khi, src, 64);
+      const uint64_t lj = __shfl(klo, src, 64);
+      if (cj == cls) {
+        lt += (hj < khi) || (hj == khi && lj < klo);
+        if (hj == khi && lj == klo) {
+          if (eq == 0) rep = (uint32_t)src;
+          eq++;
+        }
+      }
+    }
+    if (!done) {
+      pos += lt;
+      cls = rep;
+      if (eq == 1) {
+        done = true;
+        cls = 0xffffffffu;
+        const uint32_t slot = s0 + pos;
+        B.sa[slot] = v;
+        const uint32_t r = slot - U.sbase;
+        if (U.k == 1) O.bwt[U.toff + r] = lastc;
+        if (v == 0) O.rank0[unit] = r;
+      }
+    }
+    d += 16;
+  }
+}
+
+// ---- buckets of 9..256 rotations: one segment of kSeg lanes x kPer registers per bucket
+// (64 / kSeg buckets per wave).  Element (lane, r) sits at position p = (lane % kSeg) * kPer
+// + r of its segment.  Sort key: (run start, 8 characters, element index); pads sort last.
+// Round 1 sorts by the first 8 characters after the bucket's depth; every later round
+// re-keys only the runs still tied, 8 characters deeper, and re-sorts (positions of unique
+// elements never move since their run start is their own position).
+struct BsortKey {
+  uint32_t w0;  // run start << 16 | element index (pads: 0xffff << 16)
+  uint32_t hi, lo;
 };
 
-// Stable LSD radix sort of n (<= kTileCap) (key, val) pairs in LDS over bits [0, nbits).
-// 4 waves; wave w owns elements [w*kWaveSpan, (w+1)*kWaveSpan), visited 64 at a time in order.
-__device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*& keys, uint32_t*& vals) {
-  uint32_t* kin = S.keyA;
-  uint32_t* vin = S.valA;
-  uint32_t* kout = S.keyB;
-  uint32_t* vout = S.valB;
+__device__ __forceinline__ bool key_less(const BsortKey& a, const BsortKey& b) {
+  const uint32_t ra = a.w0 >> 16, rb = b.w0 >> 16;
+  if (ra != rb) return ra < rb;
+  const uint64_t ka = ((uint64_t)a.hi << 32) | a.lo, kb = ((uint64_t)b.hi << 32) | b.lo;
+  if (ka != kb) return ka < kb;
+  return (a.w0 & 0xffffu) < (b.w0 & 0xffffu);
+}
+
+template <int kSeg, int kPer>
+__device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
+  constexpr int kN = kSeg * kPer;
+  const uint32_t sl = __lane_id() % kSeg;
+#pragma unroll
+  for (int k = 2; k <= kN; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < kPer) {  // partner in another register of this lane
+#pragma unroll
+        for (int r = 0; r < kPer; r++) {
+          const int r2 = r ^ j;
+          if (r2 > r) {
+            const uint32_t p = sl * kPer + r;
+            const bool asc = (p & k) == 0;
+            const bool sw = asc ? key_less(K[r2], K[r]) : key_less(K[r], K[r2]);
+            if (sw) {
+              const BsortKey x = K[r];
+              K[r] = K[r2];
+              K[r2] = x;
+            }
+          }
+        }
+      } else {  // partner in lane ^ (j / kPer), same register
+        const int jl = j / kPer;
+#pragma unroll
+        for (int r = 0; r < kPer; r++) {
+          BsortKey o;
+          o.w0 = (uint32_t)__shfl_xor((int)K[r].w0, jl, 64);
+          o.hi = (uint32_t)__shfl_xor((int)K[r].hi, jl, 64);
+          o.lo = (uint32_t)__shfl_xor((int)K[r].lo, jl, 64);
+          const uint32_t p = sl * kPer + r;
+          const bool keep_min = ((p & j) == 0) == ((p & k) == 0);
+          const bool o_less = key_less(o, K[r]);
+          if (keep_min == o_less) K[r] = o;
+        }
+      }
+    }
+  }
+}
+
+template <int kSeg, int kPer>
+__global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_t nL, SortBufs B, SortOut O) {
+  constexpr int kBPW = 64 / kSeg;
+  constexpr int kE = 64 * kPer;  // elements per wave
+  __shared__ uint32_t Lv[kT / 64][kE];
+  __shared__ uint8_t Lc[kT / 64][kE];
+  __shared__ uint32_t Lk[kT / 64][kE];
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
-  for (uint32_t shift = 0; shift < nbits; shift += 8) {
-    for (int i = threadIdx.x; i < 4 * 256 / 2; i += kT) reinterpret_cast<uint32_t*>(&S.hist[0][0])[i] = 0;
-    __syncthreads();
-    uint32_t dig[kWaveSpan / 64], loc[kWaveSpan / 64];
+  const uint32_t sl = lane % kSeg;
+  const uint32_t bi = (blockIdx.x * (kT / 64) + w) * kBPW + lane / kSeg;
+  const bool has = bi < nL;
+  if (__ballot(has) == 0) return;
+  Grp g{0, 0, 0, 0};
+  if (has) g = L[bi];
+  Unit U{0, 1, 0, 1};
+  if (has) U = B.units[g.unit];
+  const uint8_t* t = B.text + U.toff;
+  const uint32_t m = g.size;
+  uint32_t depth = grp_depth(g);
+  const uint32_t* src = (g.flags & kGrpAlt) ? B.sa2 : B.sa;
+  BsortKey K[kPer];
+  uint32_t vq[kPer];
 #pragma unroll
-    for (int j = 0; j < (int)(kWaveSpan / 64); j++) {
-      const uint32_t e = w * kWaveSpan + j * 64 + lane;
-      const bool act = e < n;
-      const uint64_t amask = __ballot(act);
-      uint32_t d = act ? (kin[e] >> shift) & 255u : 0u;
-      const uint64_t peers = match_byte(d, amask);
-      const uint32_t rank = __popcll(peers & lanemask_lt());
-      uint32_t old = act ? S.hist[w][d] : 0u;
-      const bool leader = act && ((peers & lanemask_lt()) == 0);
-      if (leader) S.hist[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
-      dig[j] = d;
-      loc[j] = old + rank;
-    }
-    __syncthreads();
-    {  // digit bases: exclusive over (digit, wave)
-      const uint32_t d = threadIdx.x;
-      uint32_t c0 = S.hist[0][d], c1 = S.hist[1][d], c2 = S.hist[2][d], c3 = S.hist[3][d];
-      uint32_t tot = c0 + c1 + c2 + c3;
-      uint32_t incl = block_incl_sum(tot, S.sh, (uint32_t*)nullptr);
-      uint32_t b = incl - tot;
-      S.hist[0][d] = (uint16_t)b;
-      S.hist[1][d] = (uint16_t)(b + c0);
-      S.hist[2][d] = (uint16_t)(b + c0 + c1);
-      S.hist[3][d] = (uint16_t)(b + c0 + c1 + c2);
-    }
-    __syncthreads();
+  for (int r = 0; r < kPer; r++) {
+    const uint32_t p = sl * kPer + r;
+    vq[r] = p < m ? ((g.flags & kGrpIdent) ? p : src[g.start + p]) : 0u;
+  }
 #pragma unroll
-    for (int j = 0; j < (int)(kWaveSpan / 64); j++) {
-      const uint32_t e = w * kWaveSpan + j * 64 + lane;
-      if (e < n) {
-        const uint32_t dst = S.hist[w][dig[j]] + loc[j];
-        kout[dst] = kin[e];
-        vout[dst] = vin[e];
+  for (int r = 0; r < kPer; r++) {
+    const uint32_t p = sl * kPer + r, idx = lane * kPer + r;
+    const bool valid = p < m;
+    uint32_t hi = 0xffffffffu, lo = 0xffffffffu;
+    uint8_t c = 0;
+    if (valid) {
+      text_key8(t, U.len, cyc_pos(vq[r], depth, U.len), hi, lo);
+      c = t[vq[r] == 0 ? U.len - 1 : vq[r] - 1];
+    }
+    Lv[w][idx] = vq[r];
+    Lc[w][idx] = c;
+    K[r].w0 = (valid ? 0u : 0xffff0000u) | idx;
+    K[r].hi = hi;
+    K[r].lo = lo;
+  }
+  bool done[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; r++) done[r] = false;
+  for (;;) {
+    bitonic<kSeg, kPer>(K);
+    // ties with the previous / next position of the segment (same run start and key)
+    bool tp[kPer], tn[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      BsortKey q;
+      if (r > 0) {
+        q = K[r - 1];
+      } else {
+        q.w0 = (uint32_t)__shfl_up((int)K[kPer - 1].w0, 1, 64);
+        q.hi = (uint32_t)__shfl_up((int)K[kPer - 1].hi, 1, 64);
+        q.lo = (uint32_t)__shfl_up((int)K[kPer - 1].lo, 1, 64);
+        if (sl == 0) q.w0 = 0xfffe0000u;  // no previous element
+      }
+      tp[r] = (K[r].w0 >> 16) != 0xffffu && (q.w0 >> 16) == (K[r].w0 >> 16) && q.hi == K[r].hi && q.lo == K[r].lo;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      if (r + 1 < kPer) {
+        tn[r] = tp[r + 1];
+      } else {
+        bool x = __shfl_down((int)tp[0], 1, 64) != 0;
+        if (sl == kSeg - 1) x = false;
+        tn[r] = x;
       }
     }
-    __syncthreads();
-    uint32_t* t;
-    t = kin; kin = kout; kout = t;
-    t = vin; vin = vout; vout = t;
-  }
-  keys = kin;
-  vals = vin;
-}
-
-// Diagnostic stamps (BZG_DEBUG builds only): phase durations summed over workgroups.
-#define STAMP(k)                                                                    \
-  if constexpr (kStamp) {                                                           \
-    __syncthreads();                                                                \
-    if (threadIdx.x == 0) {                                                         \
-      const uint64_t now = __builtin_amdgcn_s_memtime();                            \
-      atomicAdd((unsigned long long*)&stamps[k], (unsigned long long)(now - t_last)); \
-      t_last = now;                                                                 \
-    }                                                                               \
-  }
-
-template <bool kStamp>
-__global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small, uint32_t n_small,
-                                                  const uint32_t* __restrict__ first, const uint32_t* __restrict__ last,
-                                                  uint32_t key_bits, SortBufs B, Grp* __restrict__ next,
-                                                  uint32_t* __restrict__ n_next, bool isa_valid,
-                                                  uint64_t* __restrict__ stamps) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  TileLds& S = *reinterpret_cast<TileLds*>(smem);
-  const uint32_t t = blockIdx.x;
-  const uint32_t i0 = first[t];
-  if (i0 == 0xffffffffu) return;
-  uint64_t t_last = kStamp ? __builtin_amdgcn_s_memtime() : 0;
-  // items of this tile: i0 .. i1-1 with P[i]/kWin == t (at most kWin/2: items hold >= 2 elements)
-  const uint32_t i1 = min(last[t], i0 + kWin / 2);
-  const uint32_t ni = i1 - i0;
-  // Items larger than kSmall (sorted by the digit passes) are compacted away: their
-  // tile-local size is 0.  Offsets are recomputed over the kept items.
-  for (uint32_t j = threadIdx.x; j < ni; j += kT) {
-    const Grp g = small[i0 + j];
-    S.istart[j] = g.start;
-    S.iunit[j] = g.unit | ((g.flags & 1u) << 31);
-    S.ioff[j] = g.size <= kSmall ? g.size : 0u;
-  }
-  __syncthreads();
-  uint32_t my_sz[kWin / 2 / kT + 1];
-  uint32_t my_sum = 0;
-#pragma unroll
-  for (int q = 0; q < (int)(kWin / 2 / kT + 1); q++) {
-    const uint32_t j = threadIdx.x * (kWin / 2 / kT + 1) + q;
-    const uint32_t sz = j < ni ? S.ioff[j] : 0u;
-    my_sz[q] = sz;
-    my_sum += sz;
-  }
-  {
-    uint32_t tot_e;
-    const uint32_t incl = block_incl_sum(my_sum, S.sh, &tot_e);
-    uint32_t o = incl - my_sum;
-#pragma unroll
-    for (int q = 0; q < (int)(kWin / 2 / kT + 1); q++) {
-      const uint32_t j = threadIdx.x * (kWin / 2 / kT + 1) + q;
-      if (j < ni) S.ioff[j] = o;
-      o += my_sz[q];
-    }
-    if (threadIdx.x == 0) S.ioff[ni] = tot_e;
-  }
-  __syncthreads();
-  const uint32_t n = S.ioff[ni];
-  if (n == 0) return;
-  STAMP(0);
-  const uint32_t kmask = key_bits >= 32 ? 0xffffffffu : ((1u << key_bits) - 1u);
-  {  // owner map: item index of every element (mark item starts, then a block max-scan)
-    uint32_t* owner = S.keyB;
-    uint4* o4 = reinterpret_cast<uint4*>(owner);
-    for (uint32_t i = threadIdx.x; i < kTileCap / 4; i += kT) o4[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < ni; j += kT)
-      if (S.ioff[j + 1] > S.ioff[j]) owner[S.ioff[j]] = j;
-    __syncthreads();
-    uint4 q4[kPer / 4];
-    uint32_t m = 0;
-#pragma unroll
-    for (int q = 0; q < (int)(kPer / 4); q++) {
-      q4[q] = o4[threadIdx.x * (kPer / 4) + q];
-      m = max(m, max(max(q4[q].x, q4[q].y), max(q4[q].z, q4[q].w)));
-    }
-    const uint32_t incl = block_incl_max(m, S.sh);
-    uint32_t run = __shfl_up(incl, 1);
-    if (__lane_id() == 0) run = threadIdx.x >= 64 ? S.sh[(threadIdx.x >> 6) - 1] : 0u;
-    if (threadIdx.x == 0) run = 0;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < (int)(kPer / 4); q++) {
-      q4[q].x = run = max(run, q4[q].x);
-      q4[q].y = run = max(run, q4[q].y);
-      q4[q].z = run = max(run, q4[q].z);
-      q4[q].w = run = max(run, q4[q].w);
-      o4[threadIdx.x * (kPer / 4) + q] = q4[q];
-    }
-    __syncthreads();
-  }
-  for (uint32_t e = threadIdx.x; e < n; e += kT) {
-    const uint32_t lo = S.keyB[e];
-    const uint32_t s = S.istart[lo] + (e - S.ioff[lo]);
-    const bool alt = S.iunit[lo] >> 31;
-    const uint32_t k = alt ? B.key2[s] : B.key[s];
-    const uint32_t v = alt ? B.sa2[s] : B.sa[s];
-    S.keyA[e] = (lo << key_bits) | (k & kmask);
-    S.valA[e] = v;
-  }
-  __syncthreads();
-  STAMP(1);
-  const uint32_t item_bits = 32 - __builtin_clz(ni);  // ni >= 1
-  // largest item in the tile decides the method
-  {
+    // positions (sorted order); new run starts: p if it starts a run, else inherited
+    uint32_t rsn[kPer];
     uint32_t mx = 0;
-    for (uint32_t j = threadIdx.x; j < ni; j += kT) mx = max(mx, S.ioff[j + 1] - S.ioff[j]);
-    mx = block_incl_max(mx, S.sh);
-    if (threadIdx.x == kT - 1) S.misc[3] = mx;
-    __syncthreads();
-  }
-  uint32_t *keys, *vals;
-  if (S.misc[3] <= kRankMax) {
-    // rank counting: element e goes to ioff[item] + #{f in item : (key_f, f) < (key_e, e)};
-    // lanes of one item read the same key at each step (LDS broadcast)
-    for (uint32_t e = threadIdx.x; e < n; e += kT) {
-      const uint32_t ke = S.keyA[e];
-      const uint32_t item = ke >> key_bits;
-      const uint32_t lo = S.ioff[item], hi = S.ioff[item + 1];
-      uint32_t r = 0;
-      for (uint32_t f = lo; f < hi; f++) {
-        const uint32_t kf = S.keyA[f];
-        r += (kf < ke) | ((kf == ke) & (f < e));
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const uint32_t p = sl * kPer + r;
+      mx = max(mx, tp[r] ? 0u : p);
+      rsn[r] = mx;
+    }
+    uint32_t pre = mx;
+#pragma unroll
+    for (int o = 1; o < kSeg; o <<= 1) {
+      const uint32_t x = (uint32_t)__shfl_up((int)pre, o, 64);
+      if (sl >= (uint32_t)o) pre = max(pre, x);
+    }
+    pre = (uint32_t)__shfl_up((int)pre, 1, 64);
+    if (sl == 0) pre = 0;
+    bool any_tied = false;
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      rsn[r] = max(rsn[r], pre);
+      const uint32_t idx = K[r].w0 & 0xffffu;
+      const bool valid = (K[r].w0 >> 16) != 0xffffu;
+      const bool tied = valid && (tp[r] || tn[r]);
+      const uint32_t p = sl * kPer + r;
+      if (valid && !tied && !done[r]) {
+        // unique: final position
+        const uint32_t slot = g.start + p;
+        const uint32_t v = Lv[w][idx];
+        B.sa[slot] = v;
+        const uint32_t rr = slot - U.sbase;
+        if (U.k == 1) O.bwt[U.toff + rr] = Lc[w][idx];
+        if (v == 0) O.rank0[g.unit] = rr;
       }
-      S.keyB[lo + r] = ke;
-      S.valB[lo + r] = S.valA[e];
+      done[r] = valid && !tied;
+      any_tied |= tied;
     }
-    __syncthreads();
-    keys = S.keyB;
-    vals = S.valB;
-    STAMP(2);
-  } else {
-    lds_radix_sort(S, n, key_bits + item_bits, keys, vals);
-    STAMP(3);
-  }
-  // group detection over the sorted composite keys; thread t owns [kPer*t, kPer*t + kPer)
-  const uint32_t e0 = threadIdx.x * kPer;
-  uint32_t kq[kPer];
+    if (__ballot(any_tied) == 0) break;
+    depth += 8;
+    if (depth >= kDWave) {  // still tied after kDWave characters: leave to the doubling fallback
+      const uint32_t sbase = (lane / kSeg) * (kSeg * kPer);  // this segment's counters
 #pragma unroll
-  for (int q = 0; q < (int)(kPer / 4); q++) {
-    const uint4 a = reinterpret_cast<const uint4*>(keys + e0)[q];
-    kq[4 * q] = a.x; kq[4 * q + 1] = a.y; kq[4 * q + 2] = a.z; kq[4 * q + 3] = a.w;
-  }
-  uint32_t smask = 0;  // bit q: element e0 + q starts a group
-  {
-    uint32_t prev = (e0 > 0 && e0 <= n) ? keys[e0 - 1] : 0u;
+      for (int r = 0; r < kPer; r++) Lk[w][lane * kPer + r] = 0;
+      wave_sync();
 #pragma unroll
-    for (int q = 0; q < (int)kPer; q++) {
-      const uint32_t e = e0 + q;
-      if (e < n && (e == 0 || kq[q] != prev)) smask |= 1u << q;
-      prev = kq[q];
+      for (int r = 0; r < kPer; r++)
+        if (!done[r] && (K[r].w0 >> 16) != 0xffffu) {
+          B.sa[g.start + sl * kPer + r] = Lv[w][K[r].w0 & 0xffffu];
+          atomicAdd(&Lk[w][sbase + rsn[r]], 1u);
+        }
+      wave_sync();
+#pragma unroll
+      for (int r = 0; r < kPer; r++) {
+        const uint32_t p = sl * kPer + r;
+        if (!done[r] && (K[r].w0 >> 16) != 0xffffu && rsn[r] == p)
+          O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + p, Lk[w][sbase + p], g.unit, depth << 2};
+      }
+      break;
     }
-  }
-  const uint32_t starts = __popc(smask);
-  uint32_t ngroups;
-  const uint32_t incl = block_incl_sum(starts, S.sh, &ngroups);
-  // gpos[o] = first element of group o (free key buffer); gid[e] = group of e (free val buffer)
-  uint32_t* gpos = (keys == S.keyA) ? S.keyB : S.keyA;
-  uint32_t* gid = (vals == S.valA) ? S.valB : S.valA;
-  {
-    uint32_t o = incl - starts;
-    uint32_t gq[kPer];
+    // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
 #pragma unroll
-    for (int q = 0; q < (int)kPer; q++) {
-      if ((smask >> q) & 1u) gpos[o++] = e0 + q;
-      gq[q] = o - 1;  // unused for e >= n
-    }
-#pragma unroll
-    for (int q = 0; q < (int)(kPer / 4); q++)
-      reinterpret_cast<uint4*>(gid + e0)[q] = make_uint4(gq[4 * q], gq[4 * q + 1], gq[4 * q + 2], gq[4 * q + 3]);
-  }
-  if (threadIdx.x == 0) gpos[ngroups] = n;
-  __syncthreads();
-  STAMP(4);
-  // groups of size >= 2 go to the next iteration
-  uint32_t nnew = 0;
-  {
-    uint32_t o = incl - starts;
-    for (uint32_t m = smask; m; m &= m - 1, o++) nnew += (gpos[o + 1] - (e0 + __builtin_ctz(m)) >= 2);
-  }
-  uint32_t tot_new;
-  const uint32_t incl_new = block_incl_sum(nnew, S.sh, &tot_new);
-  if (threadIdx.x == 0) S.misc[1] = tot_new ? atomicAdd(n_next, tot_new) : 0;
-  __syncthreads();
-  if (nnew) {
-    uint32_t wpos = S.misc[1] + incl_new - nnew;
-    uint32_t o = incl - starts;
-    for (uint32_t m = smask; m; m &= m - 1, o++) {
-      const uint32_t e = e0 + __builtin_ctz(m);
-      const uint32_t sz = gpos[o + 1] - e;
-      if (sz >= 2) {
-        const uint32_t item = kq[__builtin_ctz(m)] >> key_bits;
-        next[wpos++] = Grp{S.istart[item] - S.ioff[item] + e, sz, S.iunit[item] & 0x7fffffffu, 0};
+    for (int r = 0; r < kPer; r++) {
+      const uint32_t idx = K[r].w0 & 0xffffu;
+      const bool valid = (K[r].w0 >> 16) != 0xffffu;
+      if (!valid) continue;
+      const uint32_t p = sl * kPer + r;
+      if (done[r]) {
+        K[r].w0 = (p << 16) | idx;
+        K[r].hi = K[r].lo = 0;
+      } else {
+        uint32_t hi, lo;
+        text_key8(t, U.len, cyc_pos(Lv[w][idx], depth, U.len), hi, lo);
+        K[r].w0 = (rsn[r] << 16) | idx;
+        K[r].hi = hi;
+        K[r].lo = lo;
       }
     }
-  }
-  // element-parallel output: SA in slot order (coalesced); an ISA entry is rewritten only
-  // when the rank changes (isa_valid: every member's ISA already holds its item's start)
-  for (uint32_t e = threadIdx.x; e < n; e += kT) {
-    const uint32_t item = keys[e] >> key_bits;
-    const uint32_t istart = S.istart[item];
-    const uint32_t base = istart - S.ioff[item];
-    const uint32_t v = vals[e];
-    B.sa[base + e] = v;
-    const uint32_t gslot = base + gpos[gid[e]];
-    if (!isa_valid || gslot != istart) B.isa[B.units[S.iunit[item] & 0x7fffffffu].sbase + v] = gslot;
-  }
-  STAMP(5);
-  if constexpr (kStamp) {
-    if (threadIdx.x == 0) atomicAdd((unsigned long long*)&stamps[6], 1ull);
-    if (threadIdx.x == 0) atomicAdd((unsigned long long*)&stamps[7], (unsigned long long)n);
   }
 }
 
-// Equal-key groups larger than kSmall: everyone gets the bucket start as rank.
-__global__ void __launch_bounds__(kT) k_equal(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
-                                              SortBufs B, Grp* __restrict__ next, uint32_t* __restrict__ n_next) {
-  const uint32_t t = blockIdx.x;
-  const uint32_t g = upper_idx(TP, nG, t);
-  const Grp gr = G[g];
-  const uint32_t c = t - TP[g];
-  const uint32_t lo = c * kDTile, hi = min(gr.size, lo + kDTile);
+// ---------------------------------------------------------------- fallback glue
+__global__ void k_fb_flag(const Grp* __restrict__ D, uint32_t n, uint32_t* __restrict__ uflag, uint32_t* __restrict__ mind) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const Grp gr = D[g];
+  uflag[gr.unit] = 1;
+  atomicMin(mind, grp_depth(gr));
+}
+
+// Deep groups whose data is in the alternate buffer move to the primary SA; the doubling
+// list gets the groups with their flags reset.  One workgroup per group.
+__global__ void __launch_bounds__(kT) k_fb_copy(const Grp* __restrict__ D, Grp* __restrict__ L0, SortBufs B) {
+  const Grp gr = D[blockIdx.x];
+  if (gr.flags & kGrpAlt)
+    for (uint32_t e = threadIdx.x; e < gr.size; e += kT) B.sa[gr.start + e] = B.sa2[gr.start + e];
+  if (threadIdx.x == 0) L0[blockIdx.x] = Grp{gr.start, gr.size, gr.unit, 0};
+}
+
+// Members of a deep group take the group's first slot as rank (after k_fb_isa_all).
+__global__ void __launch_bounds__(kT) k_fb_group_isa(const Grp* __restrict__ L0, SortBufs B) {
+  const Grp gr = L0[blockIdx.x];
   const uint32_t sb = B.units[gr.unit].sbase;
-  const uint32_t* vs = (gr.flags & 1) ? B.sa2 : B.sa;
-  for (uint32_t e = lo + threadIdx.x; e < hi; e += kT) {
-    const uint32_t v = vs[gr.start + e];
-    B.sa[gr.start + e] = v;
-    B.isa[sb + v] = gr.start;
-  }
-  if (c == 0 && threadIdx.x == 0) next[atomicAdd(n_next, 1u)] = Grp{gr.start, gr.size, gr.unit, 0};
+  for (uint32_t e = threadIdx.x; e < gr.size; e += kT) B.isa[sb + B.sa[gr.start + e]] = gr.start;
 }
 
-// ---------------------------------------------------------------- output
-// bwt[boff[b] + q] = root[(SA[sbase + q / k] - 1) mod p] for q < n_b, k = n_b / p.
-// Last column: bwt[x] = text[SA[x / k] - 1] (cyclically) for the k-fold repeated root.
-// Four output bytes per thread; XCD-aware so that each L2 serves a few blocks' text.
-__global__ void __launch_bounds__(kT) k_bwt_out(const uint32_t* __restrict__ boff, uint32_t nb,
-                                                const Unit* __restrict__ units, const uint32_t* __restrict__ sa,
-                                                const uint8_t* __restrict__ text, uint32_t total,
-                                                uint8_t* __restrict__ bwt) {
-  const uint32_t wg = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t x0 = (wg * kT + threadIdx.x) * 4;
-  if (x0 >= total) return;
-  uint32_t b = upper_idx(boff, nb, x0);
-  uint32_t out = 0;
-  const uint32_t xe = min(x0 + 4, total);
-  for (uint32_t x = x0; x < xe; x++) {
-    while (x >= boff[b + 1]) b++;
-    const Unit U = units[b];
-    const uint32_t k = (boff[b + 1] - boff[b]) / U.len;
-    const uint32_t q = x - boff[b];
-    const uint32_t v = sa[U.sbase + (k == 1 ? q : q / k)];
-    out |= (uint32_t)text[U.toff + (v == 0 ? U.len - 1 : v - 1)] << (8 * (x - x0));
-  }
-  if (xe - x0 == 4) *reinterpret_cast<uint32_t*>(bwt + x0) = out;
-  else
-    for (uint32_t x = x0; x < xe; x++) bwt[x] = (uint8_t)(out >> (8 * (x - x0)));
+// ISA of every slot of the listed units from the (complete, primary) SA: every rotation's own
+// slot; deep groups' members are overwritten afterwards by k_fb_group_isa.
+__global__ void __launch_bounds__(kT) k_fb_isa_all(const uint32_t* __restrict__ ulist, const Unit* __restrict__ units,
+                                                   SortBufs B) {
+  const Unit U = units[ulist[blockIdx.y]];
+  const uint32_t q = blockIdx.x * kT + threadIdx.x;
+  if (q >= U.len) return;
+  const uint32_t v = B.sa[U.sbase + q];
+  B.isa[U.sbase + v] = U.sbase + q;
 }
 
-__global__ void k_rank0(const Unit* __restrict__ units, uint32_t nb, const uint32_t* __restrict__ isa,
-                        uint32_t* __restrict__ rank0) {
-  uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < nb) rank0[b] = isa[units[b].sbase] - units[b].sbase;
+// Last column of the listed units from the SA (periodic roots repeated k times).
+__global__ void __launch_bounds__(kT) k_unit_out(const uint32_t* __restrict__ ulist, const Unit* __restrict__ units,
+                                                 const uint32_t* __restrict__ sa, const uint8_t* __restrict__ text,
+                                                 uint8_t* __restrict__ bwt) {
+  const Unit U = units[ulist[blockIdx.y]];
+  const uint32_t x = blockIdx.x * kT + threadIdx.x;
+  if (x >= U.len * U.k) return;
+  const uint32_t v = sa[U.sbase + (U.k == 1 ? x : x / U.k)];
+  bwt[U.toff + x] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
+}
+
+__global__ void k_rank0_isa(const uint32_t* __restrict__ ulist, uint32_t n, const Unit* __restrict__ units,
+                            const uint32_t* __restrict__ isa, uint32_t* __restrict__ rank0) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t u = ulist[i];
+  rank0[u] = isa[units[u].sbase] - units[u].sbase;
 }
 
 }  // namespace
@@ -602,196 +665,163 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
                hipStream_t st) {
   const uint32_t nb = r.nblocks;
   if (nb == 0) return;
-  // Units: one per block, the primitive root of the block.
+  if (nb > 0xffffu) throw HipFailure(hipErrorInvalidValue);  // S2 keys carry 16-bit unit ids
   std::vector<Unit> hu(nb);
   uint64_t S = 0;
+  uint32_t maxlen = 0;
+  std::vector<uint32_t> periodic;
   for (uint32_t b = 0; b < nb; b++) {
-    hu[b] = Unit{(uint32_t)S, h_period[b], h_boff[b], 0};
+    const uint32_t n_b = h_boff[b + 1] - h_boff[b];
+    hu[b] = Unit{(uint32_t)S, h_period[b], h_boff[b], n_b / h_period[b]};
+    if (hu[b].k > 1) periodic.push_back(b);
     S += h_period[b];
+    maxlen = std::max(maxlen, n_b);
   }
   Unit* units = ws.typed<Unit>("sort_units", nb);
   HIP_OK(hipMemcpyAsync(units, hu.data(), sizeof(Unit) * nb, hipMemcpyHostToDevice, st));
 
-  SortBufs B;
+  SortBufs B{};
   B.sa = ws.u32("sort_sa", S + 16);
-  B.isa = ws.u32("sort_isa", S + 16);
-  B.key = ws.u32("sort_key", S + 16);
   B.sa2 = ws.u32("sort_sa2", S + 16);
-  B.key2 = ws.u32("sort_key2", S + 16);
   B.text = r.blk;
   B.units = units;
-
-  const size_t lcap = S / 2 + nb + 16;        // groups of >= 2 members
-  // large-list entries: groups larger than kSmall, plus (first pass at h = 0) every bucket
-  // of >= 2 members of every unit
-  const size_t bigcap = S / kSmall + std::min<uint64_t>(256ull * nb, S / 2) + nb + 16;
-  Grp* L = ws.typed<Grp>("sort_L", lcap);
-  Grp* Ln = ws.typed<Grp>("sort_Ln", lcap);
-  Grp* small = ws.typed<Grp>("sort_small", lcap);
-  Grp* large = ws.typed<Grp>("sort_large", bigcap);
-  Grp* large2 = ws.typed<Grp>("sort_large2", bigcap);
-  Grp* equal = ws.typed<Grp>("sort_equal", bigcap);
-  uint32_t* P = ws.u32("sort_P", lcap + 16);
-  uint32_t* TP = ws.u32("sort_TP", bigcap + S / kDTile + 64);
-  uint32_t* first = ws.u32("sort_first", S / kWin + 64);
-  uint32_t* last = ws.u32("sort_last", S / kWin + 64);
-  uint32_t* gmap = ws.u32("sort_gmap", S + 16);
-  const size_t max_dtiles = S / kDTile + bigcap + 16;
-  uint32_t* hist = ws.u32("sort_hist", max_dtiles * 256);
-  uint32_t* tot = ws.u32("sort_tot", bigcap * 256);
-  uint32_t* cnt = ws.u32("sort_cnt", 64);  // device counters
-  uint32_t* scratch = ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(lcap, max_dtiles), S + 16)) + 64);
-  // counters: 0 total(scan), 1 n_large, 2 n_small, 3 n_next(L'), 4 n_large2, 5 n_equal, 6 tiles
-  uint32_t hc[8];
+  // class lists: a class-c bucket holds more than kClsMax[c-1] rotations
+  ClsLists C{};
+  size_t ccap[kNCls];
+  for (int c = 0; c < kNCls; c++) {
+    const uint64_t minsz = c == 0 ? 2 : (uint64_t)kClsMax[c - 1] + 1;
+    ccap[c] = S / minsz + nb + 16;
+    C.l[c] = ws.typed<Grp>("sort_cls" + std::to_string(c), ccap[c]);
+  }
+  Grp* next = ws.typed<Grp>("sort_next", ccap[6]);
+  SortOut O{};
+  O.bwt = bwt;
+  O.rank0 = rank0;
+  O.deep = ws.typed<Grp>("sort_deep", S / 2 + nb + 16);
+  uint32_t* cnt = ws.u32("sort_cnt", 64);  // 0..6 class counts (init), 8..15 class bounds, 16 n_deep, 17 tiles, 18 min depth
+  O.n_deep = cnt + 16;
+  const size_t max_tiles = S / kDTile + ccap[6] + 16;
+  uint32_t* TP = ws.u32("sort_TP", max_tiles + 16);
+  uint32_t* hist = ws.u32("sort_hist", max_tiles * 256);
+  uint32_t* tot = ws.u32("sort_tot", ccap[6] * 256);
+  uint32_t* ccnt = ws.u32("sort_ccnt", kNCls * ccap[6] + 16);
+  uint32_t* scratch = ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(kNCls * ccap[6], max_tiles)) + 64);
+  uint32_t hc[24];
   auto read_counters = [&]() {
     HIP_OK(hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
   };
   auto grid = [](uint64_t n) { return (unsigned)std::max<uint64_t>(1, ceil_div64(n, kT)); };
-
-  // initial list = units
-  uint32_t nL = nb;
-  k_units_to_groups<<<grid(nb), kT, 0, st>>>(units, nb, L, P);
-  HIP_OK(hipGetLastError());
-  scan_u32(ScanOp::Sum, true, P, P, nL, cnt + 0, scratch, st);
-  k_init_sa<<<grid(S), kT, 0, st>>>(L, P, nL, (uint32_t)S, B.sa);
-  HIP_OK(hipGetLastError());
-
   static const bool debug = getenv("BZG_DEBUG") != nullptr;
-  uint64_t* stamps = (uint64_t*)ws.u32("sort_stamps", 32);
-  if (debug) HIP_OK(hipMemsetAsync(stamps, 0, 128, st));
-  std::vector<uint32_t> hsz;  // debug: sizes of the groups in L
-  const size_t tile_lds = sizeof(TileLds);
-  static_assert(4 * sizeof(TileLds) <= 160 * 1024, "four tile-sort workgroups must fit one CU's LDS");
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_OK(hipFuncSetAttribute((const void*)k_tile_sort<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
-    HIP_OK(hipFuncSetAttribute((const void*)k_tile_sort<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
-    attr_set = true;
-  }
-  uint32_t h = 0;
-  int iters = 0;
-  uint64_t unsorted = 0;
-  while (nL > 0) {
-    ++iters;
-    // element prefix over L (for h == 0 it was computed above)
-    if (h > 0) {
-      k_group_sizes<<<grid(nL), kT, 0, st>>>(L, nL, P);
-      HIP_OK(hipGetLastError());
-      scan_u32(ScanOp::Sum, true, P, P, nL, cnt + 0, scratch, st);
-    }
-    HIP_OK(hipMemsetAsync(cnt + 1, 0, 7 * 4, st));
+
+  HIP_OK(hipMemsetAsync(cnt, 0, 64 * 4, st));
+  k_init_units<<<grid(nb), kT, 0, st>>>(units, nb, B, O, C, cnt);
+  HIP_OK(hipGetLastError());
+  read_counters();
+  uint32_t ncls[kNCls];
+  for (int c = 0; c < kNCls; c++) ncls[c] = hc[c];
+  uint32_t n_big = ncls[6];
+  Grp* big = C.l[6];
+  Grp* nxt = next;
+  int passes = 0;
+  uint64_t s1_elems = 0;
+  // ---- S1: byte passes over the buckets larger than kBig
+  while (n_big > 0) {
+    ++passes;
+    k_group_tiles<<<grid(n_big), kT, 0, st>>>(big, n_big, TP);
+    HIP_OK(hipGetLastError());
+    scan_u32(ScanOp::Sum, true, TP, TP, n_big, cnt + 17, scratch, st);
     read_counters();
-    const uint32_t totalL = hc[0];
-    unsorted += totalL;
+    const uint32_t ntiles = hc[17];
     if (debug) {
-      std::vector<Grp> hg(nL);
-      HIP_OK(hipMemcpy(hg.data(), L, sizeof(Grp) * nL, hipMemcpyDeviceToHost));
-      uint64_t bins[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // elements in groups of size 2,3-4,5-8,9-32,33-256,257-2048,>2048
-      uint64_t gb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (const Grp& g : hg) {
-        const int bi = g.size <= 2 ? 0 : g.size <= 4 ? 1 : g.size <= 8 ? 2 : g.size <= 32 ? 3 : g.size <= 256 ? 4
-                       : g.size <= 2048 ? 5 : 6;
-        bins[bi] += g.size;
-        gb[bi]++;
+      std::vector<Grp> hg(n_big);
+      HIP_OK(hipMemcpy(hg.data(), big, sizeof(Grp) * n_big, hipMemcpyDeviceToHost));
+      uint64_t el = 0;
+      for (const Grp& g : hg) el += g.size;
+      s1_elems += el;
+      fprintf(stderr, "[bzg sort S1] pass %d: groups=%u elems=%lu tiles=%u\n", passes, n_big, el, ntiles);
+    }
+    k_s1_hist<<<ntiles, kT, 0, st>>>(big, n_big, TP, B, hist);
+    HIP_OK(hipGetLastError());
+    k_s1_off<<<n_big, kT, 0, st>>>(big, n_big, TP, hist, tot, ccnt, O.deep, O.n_deep);
+    HIP_OK(hipGetLastError());
+    scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * n_big, cnt + 15, scratch, st);
+    k_cls_bounds<<<1, 64, 0, st>>>(ccnt, n_big, cnt + 15, cnt + 8);
+    HIP_OK(hipGetLastError());
+    ClsLists Cp = C;
+    for (int c = 0; c < 6; c++) Cp.base[c] = ncls[c];
+    Cp.l[6] = nxt;
+    Cp.base[6] = 0;
+    k_s1_scatter<<<ntiles, kT, 0, st>>>(big, n_big, TP, B, O, hist, tot, ccnt, Cp);
+    HIP_OK(hipGetLastError());
+    k_s1_single<<<n_big, kT, 0, st>>>(big, B, tot);
+    HIP_OK(hipGetLastError());
+    read_counters();
+    for (int c = 0; c < 6; c++) ncls[c] += hc[8 + c + 1] - hc[8 + c];
+    n_big = hc[8 + kNCls] - hc[8 + 6];
+    std::swap(big, nxt);
+  }
+  // ---- S2: every size class
+  if (debug)
+    fprintf(stderr, "[bzg sort S2] buckets by class: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", ncls[0],
+            ncls[1], ncls[2], ncls[3], ncls[4], ncls[5]);
+  if (ncls[0]) k_tiny<<<ceil_div(ncls[0], 8 * (kT / 64)), kT, 0, st>>>(C.l[0], ncls[0], B, O);
+  if (ncls[1]) k_bsort<16, 1><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
+  if (ncls[2]) k_bsort<32, 1><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O);
+  if (ncls[3]) k_bsort<64, 1><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O);
+  if (ncls[4]) k_bsort<64, 2><<<ceil_div(ncls[4], kT / 64), kT, 0, st>>>(C.l[4], ncls[4], B, O);
+  if (ncls[5]) k_bsort<64, 4><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O);
+  HIP_OK(hipGetLastError());
+  read_counters();
+  const uint32_t n_deep = hc[16];
+  int dbl_iters = 0;
+  uint64_t dbl_elems = 0;
+  std::vector<uint32_t> fb_units;
+  if (n_deep > 0) {
+    // ---- S3: prefix doubling for the deep groups, over ISA ranks of the affected units
+    B.isa = ws.u32("sort_isa", S + 16);
+    B.key = ws.u32("sort_key", S + 16);
+    B.key2 = ws.u32("sort_key2", S + 16);
+    uint32_t* uflag = ws.u32("sort_uflag", nb + 16);
+    HIP_OK(hipMemsetAsync(uflag, 0, 4 * (size_t)nb, st));
+    HIP_OK(hipMemsetAsync(cnt + 18, 0xff, 4, st));
+    k_fb_flag<<<grid(n_deep), kT, 0, st>>>(O.deep, n_deep, uflag, cnt + 18);
+    HIP_OK(hipGetLastError());
+    std::vector<uint32_t> hf(nb);
+    HIP_OK(hipMemcpyAsync(hf.data(), uflag, 4 * (size_t)nb, hipMemcpyDeviceToHost, st));
+    read_counters();
+    const uint32_t h0 = hc[18];
+    uint32_t flen = 0;
+    for (uint32_t b = 0; b < nb; b++)
+      if (hf[b]) {
+        fb_units.push_back(b);
+        flen = std::max(flen, hu[b].len * hu[b].k);
       }
-      fprintf(stderr, "[bzg sort] h=%u groups=%u elems=%u | elems by group size 2:%lu 3-4:%lu 5-8:%lu 9-32:%lu "
-              "33-256:%lu 257-2k:%lu >2k:%lu | groups >2k:%lu\n", h, nL, totalL, bins[0], bins[1], bins[2], bins[3],
-              bins[4], bins[5], bins[6], gb[6]);
-    }
-    HIP_OK(hipMemsetAsync(gmap, 0, (size_t)totalL * 4, st));
-    k_mark_groups<<<grid(nL), kT, 0, st>>>(P, nL, gmap);
+    uint32_t* ulist = ws.u32("sort_ulist", fb_units.size() + 16);
+    HIP_OK(hipMemcpyAsync(ulist, fb_units.data(), 4 * fb_units.size(), hipMemcpyHostToDevice, st));
+    Grp* L0 = ws.typed<Grp>("sort_L0", n_deep + 16);
+    k_fb_copy<<<n_deep, kT, 0, st>>>(O.deep, L0, B);
     HIP_OK(hipGetLastError());
-    scan_u32(ScanOp::Max, false, gmap, gmap, totalL, cnt + 7, scratch, st);
-    k_gather<<<grid(totalL), kT, 0, st>>>(L, P, gmap, totalL, h, B);
+    k_fb_isa_all<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B);
     HIP_OK(hipGetLastError());
-    k_extract_large<<<grid(nL), kT, 0, st>>>(L, nL, h == 0 ? 1 : 0, large, cnt + 1);
+    k_fb_group_isa<<<n_deep, kT, 0, st>>>(L0, B);
     HIP_OK(hipGetLastError());
-    read_counters();
-    uint32_t n_large = hc[1];
-    static const uint32_t dig0[4] = {24, 16, 8, 0};
-    static const uint32_t digh[3] = {12, 4, 0};
-    const uint32_t* digs = h == 0 ? dig0 : digh;
-    const int ndig = h == 0 ? 4 : 3;
-    Grp* lg = large;
-    Grp* lg2 = large2;
-    for (int di = 0; di < ndig && n_large > 0; di++) {
-      const int mode = (h == 0 && di == 0) ? 1 : (di == ndig - 1 ? 2 : 0);
-      k_group_tiles<<<grid(n_large), kT, 0, st>>>(lg, n_large, TP);
-      HIP_OK(hipGetLastError());
-      scan_u32(ScanOp::Sum, true, TP, TP, n_large, cnt + 6, scratch, st);
-      HIP_OK(hipMemsetAsync(cnt + 4, 0, 4, st));
-      read_counters();
-      const uint32_t ntiles = hc[6];
-      k_dhist<<<ntiles, kT, 0, st>>>(lg, n_large, TP, digs[di], B, hist);
-      HIP_OK(hipGetLastError());
-      k_doff<<<n_large, kT, 0, st>>>(lg, n_large, TP, hist, tot, mode, small, cnt + 2, lg2, cnt + 4, equal, cnt + 5);
-      HIP_OK(hipGetLastError());
-      k_dscatter<<<ntiles, kT, 0, st>>>(lg, n_large, TP, digs[di], B, hist, tot);
-      HIP_OK(hipGetLastError());
-      k_dsingle<<<ntiles, kT, 0, st>>>(lg, n_large, TP, B, tot);
-      HIP_OK(hipGetLastError());
-      read_counters();
-      n_large = hc[4];
-      std::swap(lg, lg2);
-    }
-    HIP_OK(hipMemsetAsync(cnt + 3, 0, 4, st));
-    const uint32_t kbits = h == 0 ? 16u : 20u;
-    // groups of L small enough for LDS: tiles straight over L (P still holds L's prefix)
-    if (h > 0) {
-      const uint32_t ntiles = ceil_div(totalL, kWin);
-      HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
-      k_tile_first<<<grid(nL), kT, 0, st>>>(P, nL, first, last);
-      HIP_OK(hipGetLastError());
-      if (debug) k_tile_sort<true><<<ntiles, kT, tile_lds, st>>>(L, nL, first, last, kbits, B, Ln, cnt + 3, true, stamps);
-      else k_tile_sort<false><<<ntiles, kT, tile_lds, st>>>(L, nL, first, last, kbits, B, Ln, cnt + 3, true, stamps);
-      HIP_OK(hipGetLastError());
-    }
-    read_counters();
-    const uint32_t n_small = hc[2];
-    const uint32_t n_equal = hc[5];
-    if (n_small > 0) {  // buckets emitted by the digit passes
-      k_group_sizes<<<grid(n_small), kT, 0, st>>>(small, n_small, P);
-      HIP_OK(hipGetLastError());
-      scan_u32(ScanOp::Sum, true, P, P, n_small, cnt + 0, scratch, st);
-      read_counters();
-      const uint32_t tot_small = hc[0];
-      const uint32_t ntiles = ceil_div(tot_small, kWin);
-      HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
-      k_tile_first<<<grid(n_small), kT, 0, st>>>(P, n_small, first, last);
-      HIP_OK(hipGetLastError());
-      if (debug) k_tile_sort<true><<<ntiles, kT, tile_lds, st>>>(small, n_small, first, last, kbits, B, Ln, cnt + 3, false, stamps);
-      else k_tile_sort<false><<<ntiles, kT, tile_lds, st>>>(small, n_small, first, last, kbits, B, Ln, cnt + 3, false, stamps);
-      HIP_OK(hipGetLastError());
-    }
-    if (n_equal > 0) {
-      k_group_tiles<<<grid(n_equal), kT, 0, st>>>(equal, n_equal, TP);
-      HIP_OK(hipGetLastError());
-      scan_u32(ScanOp::Sum, true, TP, TP, n_equal, cnt + 6, scratch, st);
-      read_counters();
-      k_equal<<<hc[6], kT, 0, st>>>(equal, n_equal, TP, B, Ln, cnt + 3);
-      HIP_OK(hipGetLastError());
-    }
-    read_counters();
-    nL = hc[3];
-    std::swap(L, Ln);
-    h = h == 0 ? 4 : h * 2;
-    if (iters > 40) throw HipFailure(hipErrorUnknown);  // cannot happen for aperiodic roots
+    if (debug) fprintf(stderr, "[bzg sort S3] deep groups=%u units=%zu h0=%u\n", n_deep, fb_units.size(), h0);
+    doubling_sort(ws, B, L0, n_deep, h0, &dbl_iters, &dbl_elems, st);
+    k_unit_out<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B.sa, r.blk, bwt);
+    HIP_OK(hipGetLastError());
+    k_rank0_isa<<<grid(fb_units.size()), kT, 0, st>>>(ulist, (uint32_t)fb_units.size(), units, B.isa, rank0);
+    HIP_OK(hipGetLastError());
   }
-  if (debug) {
-    uint64_t hs[8];
-    HIP_OK(hipMemcpyAsync(hs, stamps, 64, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    fprintf(stderr, "[bzg tile_sort stamps] tiles=%lu elems=%lu | load %lu  elems %lu  rank %lu  radix %lu  groups %lu  "
-            "output %lu (s_memtime ticks summed over workgroups)\n", hs[6], hs[7], hs[0], hs[1], hs[2], hs[3], hs[4], hs[5]);
+  if (!periodic.empty()) {  // periodic roots: the root's last column repeated k times
+    uint32_t* plist = ws.u32("sort_plist", periodic.size() + 16);
+    HIP_OK(hipMemcpyAsync(plist, periodic.data(), 4 * periodic.size(), hipMemcpyHostToDevice, st));
+    k_unit_out<<<dim3(ceil_div(maxlen, kT), (unsigned)periodic.size()), kT, 0, st>>>(plist, units, B.sa, r.blk, bwt);
+    HIP_OK(hipGetLastError());
   }
-  k_bwt_out<<<grid(ceil_div64(h_boff[nb], 4)), kT, 0, st>>>(r.boff, nb, units, B.sa, r.blk, h_boff[nb], bwt);
-  HIP_OK(hipGetLastError());
-  k_rank0<<<grid(nb), kT, 0, st>>>(units, nb, B.isa, rank0);
-  HIP_OK(hipGetLastError());
   if (stats) {
-    stats->iterations = iters;
-    stats->unsorted_elems = unsorted;
+    stats->iterations = passes + 1 + dbl_iters;
+    stats->unsorted_elems = s1_elems + dbl_elems;
   }
 }
 

@@ -128,6 +128,42 @@ def test_bwt_matches_oracle(case):
         assert orig[b] == o, (case, b, len(blk))
 
 
+def _long_repeat_blocks():
+    """Aperiodic blocks with long repeats: deep string-tile groups (kDWave), deep S1 buckets
+    (kDBig) and big radix-round groups all end in the doubling fallback."""
+    rng = random.Random(11)
+    w = bytes(rng.randrange(256) for _ in range(3000))
+    parts = [
+        w * 50 + b"x",                                   # 50-member groups, LCP up to 147k
+        b"ab" * 40_000 + b"c",                           # two huge S1 buckets, LCP up to 80k
+        (b"abcabcabd" * 9000)[:-1] + b"e",               # near-periodic, period 9
+        bytes(rng.randrange(2) for _ in range(400)) * 200 + b"\x02",  # 200-member groups, binary
+        datagen.text(20_000, 5) * 12 + b"!",             # text repeats, 12-member groups
+        bytes(rng.randrange(4) for _ in range(70_000)),  # small alphabet, no long repeats
+    ]
+    offs = [0]
+    for p_ in parts:
+        offs.append(offs[-1] + len(p_))
+    return b"".join(parts), offs
+
+
+def test_bwt_long_repeats_fallback():
+    blocks, offs = _long_repeat_blocks()
+    bwt, orig = gpu_bwt(blocks, offs)
+    for b in range(len(offs) - 1):
+        blk = blocks[offs[b]:offs[b + 1]]
+        L, o, per = O.orc_bwt(blk)
+        assert per == len(blk), b  # all aperiodic
+        assert bwt[offs[b]:offs[b + 1]] == L, b
+        assert orig[b] == o, b
+
+
+def test_long_repeats_streams():
+    blocks, _ = _long_repeat_blocks()
+    for level in (1, 9):
+        assert B.buff_to_buff_compress(blocks, level) == expected(blocks, level)
+
+
 def test_bwt_single_symbol_blocks():
     blocks = b"a" * 5000 + b"\xfb" * 3 + b"z"
     offs = [0, 5000, 5003, 5004]
