@@ -400,12 +400,63 @@ struct BsortKey {
   uint32_t hi, lo;
 };
 
+// (run start, key, index) order; branch-free: (rs:hi) and (lo:idx) as 48-bit integers.
 __device__ __forceinline__ bool key_less(const BsortKey& a, const BsortKey& b) {
-  const uint32_t ra = a.w0 >> 16, rb = b.w0 >> 16;
-  if (ra != rb) return ra < rb;
-  const uint64_t ka = ((uint64_t)a.hi << 32) | a.lo, kb = ((uint64_t)b.hi << 32) | b.lo;
-  if (ka != kb) return ka < kb;
-  return (a.w0 & 0xffffu) < (b.w0 & 0xffffu);
+  const uint64_t a1 = ((uint64_t)(a.w0 >> 16) << 32) | a.hi, b1 = ((uint64_t)(b.w0 >> 16) << 32) | b.hi;
+  const uint64_t a2 = ((uint64_t)a.lo << 16) | (a.w0 & 0xffffu), b2 = ((uint64_t)b.lo << 16) | (b.w0 & 0xffffu);
+  return (a1 < b1) | ((a1 == b1) & (a2 < b2));
+}
+
+// x from lane ^ J (J < 64): DPP within quads, ds_swizzle within 32 lanes, bpermute across.
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
+  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  else if constexpr (J < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (J << 10) | 0x1F);
+  else return (uint32_t)__shfl_xor((int)x, J, 64);
+}
+
+template <int kSeg, int kPer, int J>
+__device__ __forceinline__ void bitonic_xlane(BsortKey (&K)[kPer], int k, uint32_t sl) {
+  constexpr int jl = J / kPer;
+  BsortKey o[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; r++) {
+    o[r].w0 = xor_lane<jl>(K[r].w0);
+    o[r].hi = xor_lane<jl>(K[r].hi);
+    o[r].lo = xor_lane<jl>(K[r].lo);
+  }
+#pragma unroll
+  for (int r = 0; r < kPer; r++) {
+    const uint32_t p = sl * kPer + r;
+    const bool keep_min = ((p & J) == 0) == ((p & k) == 0);
+    if (keep_min == key_less(o[r], K[r])) K[r] = o[r];
+  }
+}
+
+template <int kSeg, int kPer, int J>
+__device__ __forceinline__ void bitonic_j(BsortKey (&K)[kPer], int k, uint32_t sl) {
+  if constexpr (J >= 1) {
+    if (J <= (k >> 1)) {
+      if constexpr (J < kPer) {  // partner in another register of this lane
+#pragma unroll
+        for (int r = 0; r < kPer; r++) {
+          const int r2 = r ^ J;
+          if (r2 > r) {
+            const uint32_t p = sl * kPer + r;
+            const bool asc = (p & k) == 0;
+            const bool sw = asc ? key_less(K[r2], K[r]) : key_less(K[r], K[r2]);
+            const BsortKey x = K[r], y = K[r2];
+            K[r] = sw ? y : x;
+            K[r2] = sw ? x : y;
+          }
+        }
+      } else {
+        bitonic_xlane<kSeg, kPer, J>(K, k, sl);
+      }
+    }
+    bitonic_j<kSeg, kPer, J / 2>(K, k, sl);
+  }
 }
 
 template <int kSeg, int kPer>
@@ -413,39 +464,99 @@ __device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
   constexpr int kN = kSeg * kPer;
   const uint32_t sl = __lane_id() % kSeg;
 #pragma unroll
-  for (int k = 2; k <= kN; k <<= 1) {
+  for (int k = 2; k <= kN; k <<= 1) bitonic_j<kSeg, kPer, kN / 2>(K, k, sl);
+}
+
+// Runs still tied after kBsRounds bitonic rounds (few rotations, often long repeats) are
+// finished in place: every tied rotation ranks itself among the members of its run that are
+// still tied with it (same class, named by the lowest position of the class) on the next 16
+// characters per step; positions do not move any more, the final slot is run start + rank.
+constexpr int kBsRounds = 2;
+
+template <int kSeg, int kPer>
+__device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, const Unit& U, uint32_t depth,
+                           const BsortKey (&K)[kPer], const bool (&done)[kPer], const uint32_t (&rsn)[kPer],
+                           const uint32_t* Lv, uint32_t* Lk, uint4* TK, uint32_t* TC) {
+  constexpr int kN = kSeg * kPer;
+  const uint32_t lane = __lane_id(), sl = lane % kSeg, sb = (lane / kSeg) * kN;
+  const uint8_t* t = B.text + U.toff;
+  bool live[kPer];
+  uint32_t v[kPer], pos[kPer], cls[kPer], rlen[kPer];
 #pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j < kPer) {  // partner in another register of this lane
+  for (int r = 0; r < kPer; r++) {
+    live[r] = !done[r] && (K[r].w0 >> 16) != 0xffffu;
+    v[r] = live[r] ? Lv[K[r].w0 & 0xffffu] : 0u;
+    pos[r] = rsn[r];
+    cls[r] = rsn[r];
+    Lk[lane * kPer + r] = 0;
+  }
+  wave_sync();
 #pragma unroll
-        for (int r = 0; r < kPer; r++) {
-          const int r2 = r ^ j;
-          if (r2 > r) {
-            const uint32_t p = sl * kPer + r;
-            const bool asc = (p & k) == 0;
-            const bool sw = asc ? key_less(K[r2], K[r]) : key_less(K[r], K[r2]);
-            if (sw) {
-              const BsortKey x = K[r];
-              K[r] = K[r2];
-              K[r2] = x;
-            }
-          }
-        }
-      } else {  // partner in lane ^ (j / kPer), same register
-        const int jl = j / kPer;
+  for (int r = 0; r < kPer; r++)
+    if (live[r]) atomicAdd(&Lk[sb + rsn[r]], 1u);
+  wave_sync();
 #pragma unroll
-        for (int r = 0; r < kPer; r++) {
-          BsortKey o;
-          o.w0 = (uint32_t)__shfl_xor((int)K[r].w0, jl, 64);
-          o.hi = (uint32_t)__shfl_xor((int)K[r].hi, jl, 64);
-          o.lo = (uint32_t)__shfl_xor((int)K[r].lo, jl, 64);
+  for (int r = 0; r < kPer; r++) rlen[r] = live[r] ? Lk[sb + rsn[r]] : 0u;
+  for (;;) {
+    bool any = false;
+#pragma unroll
+    for (int r = 0; r < kPer; r++) any |= live[r];
+    if (__ballot(any) == 0) break;
+    const bool deep = depth >= kDWave;
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const uint32_t wp = sb + sl * kPer + r;
+      uint32_t k[4] = {0u, 0u, 0u, 0u};
+      if (live[r] && !deep) text_key16(t, U.len, cyc_pos(v[r], depth, U.len), k);
+      TK[wp] = make_uint4(k[0], k[1], k[2], k[3]);
+      TC[wp] = live[r] ? cls[r] : 0xffffffffu;
+    }
+    wave_sync();
+    if (deep) {  // still tied after kDWave characters: leave to the doubling fallback
+#pragma unroll
+      for (int r = 0; r < kPer; r++)
+        if (live[r]) {
           const uint32_t p = sl * kPer + r;
-          const bool keep_min = ((p & j) == 0) == ((p & k) == 0);
-          const bool o_less = key_less(o, K[r]);
-          if (keep_min == o_less) K[r] = o;
+          uint32_t rank = 0, cnt = 0;
+          for (uint32_t q = rsn[r]; q < rsn[r] + rlen[r]; q++)
+            if (TC[sb + q] == cls[r]) {
+              cnt++;
+              rank += q < p;
+            }
+          B.sa[g.start + pos[r] + rank] = v[r];
+          if (rank == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + pos[r], cnt, g.unit, depth << 2};
+        }
+      break;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      if (!live[r]) continue;
+      const uint4 me = TK[sb + sl * kPer + r];
+      const uint64_t mh = ((uint64_t)me.x << 32) | me.y, ml = ((uint64_t)me.z << 32) | me.w;
+      uint32_t lt = 0, eq = 0, rep = 0xffffffffu;
+      for (uint32_t q = rsn[r]; q < rsn[r] + rlen[r]; q++) {
+        if (TC[sb + q] != cls[r]) continue;
+        const uint4 o = TK[sb + q];
+        const uint64_t oh = ((uint64_t)o.x << 32) | o.y, ol = ((uint64_t)o.z << 32) | o.w;
+        lt += (oh < mh) || (oh == mh && ol < ml);
+        if (oh == mh && ol == ml) {
+          if (rep == 0xffffffffu) rep = q;
+          eq++;
         }
       }
+      pos[r] += lt;
+      cls[r] = rep;
+      if (eq == 1) {
+        live[r] = false;
+        const uint32_t slot = g.start + pos[r];
+        B.sa[slot] = v[r];
+        const uint32_t rr = slot - U.sbase;
+        if (U.k == 1) O.bwt[U.toff + rr] = t[v[r] == 0 ? U.len - 1 : v[r] - 1];
+        if (v[r] == 0) O.rank0[g.unit] = rr;
+      }
     }
+    wave_sync();
+    depth += 16;
   }
 }
 
@@ -456,6 +567,8 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
   __shared__ uint32_t Lv[kT / 64][kE];
   __shared__ uint8_t Lc[kT / 64][kE];
   __shared__ uint32_t Lk[kT / 64][kE];
+  __shared__ uint4 TK[kT / 64][kE];
+  __shared__ uint32_t TC[kT / 64][kE];
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   const uint32_t sl = lane % kSeg;
   const uint32_t bi = (blockIdx.x * (kT / 64) + w) * kBPW + lane / kSeg;
@@ -495,6 +608,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
   bool done[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; r++) done[r] = false;
+  int round = 0;
   for (;;) {
     bitonic<kSeg, kPer>(K);
     // ties with the previous / next position of the segment (same run start and key)
@@ -560,25 +674,9 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
       any_tied |= tied;
     }
     if (__ballot(any_tied) == 0) break;
-    depth += 8;
-    if (depth >= kDWave) {  // still tied after kDWave characters: leave to the doubling fallback
-      const uint32_t sbase = (lane / kSeg) * (kSeg * kPer);  // this segment's counters
-#pragma unroll
-      for (int r = 0; r < kPer; r++) Lk[w][lane * kPer + r] = 0;
-      wave_sync();
-#pragma unroll
-      for (int r = 0; r < kPer; r++)
-        if (!done[r] && (K[r].w0 >> 16) != 0xffffu) {
-          B.sa[g.start + sl * kPer + r] = Lv[w][K[r].w0 & 0xffffu];
-          atomicAdd(&Lk[w][sbase + rsn[r]], 1u);
-        }
-      wave_sync();
-#pragma unroll
-      for (int r = 0; r < kPer; r++) {
-        const uint32_t p = sl * kPer + r;
-        if (!done[r] && (K[r].w0 >> 16) != 0xffffu && rsn[r] == p)
-          O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + p, Lk[w][sbase + p], g.unit, depth << 2};
-      }
+    depth += 8;  // tied runs are equal to this depth
+    if (++round >= kBsRounds || depth >= kDWave) {
+      bsort_tail<kSeg, kPer>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       break;
     }
     // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
