@@ -37,11 +37,15 @@ constexpr uint32_t kDTile = 4096;     // rotations per workgroup in an S1 pass
 constexpr uint32_t kPerT = kDTile / kT;
 constexpr uint32_t kDBig = 16;        // S1 byte passes stop at this depth (then doubling)
 constexpr uint32_t kDWave = 1024;     // S2 rounds stop at this depth (then doubling)
-constexpr int kNCls = 7;              // size classes 0..5 (S2) and 6 (next S1 pass)
-constexpr uint32_t kClsMax[6] = {8, 16, 32, 64, 128, 256};
+constexpr uint32_t kSG = 2048;        // S1 groups up to this size are packed into shared tiles
+// size classes: 0..5 go to S2 (2-8 .. 129-256), 6 / 7 to the next S1 pass (packed / tiled),
+// 8 (still big after kDBig characters) to the doubling fallback
+constexpr int kNCls = 8;
+constexpr uint32_t kClsMax[7] = {8, 16, 32, 64, 128, 256, kSG};
+constexpr uint32_t kClsDeep = 8;
 
 __host__ __device__ __forceinline__ uint32_t size_cls(uint32_t n) {
-  return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= 256 ? 5u : 6u;
+  return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= 256 ? 5u : n <= kSG ? 6u : 7u;
 }
 
 struct SortOut {
@@ -174,12 +178,12 @@ __global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, uint3
 __device__ __forceinline__ uint32_t bucket_cls(uint32_t total, uint32_t depth) {
   if (total < 2) return 0xffu;
   const uint32_t c = size_cls(total);
-  return (c == 6 && depth >= kDBig) ? 7u : c;  // 7: still big after kDBig characters
+  return (c >= 6 && depth >= kDBig) ? kClsDeep : c;
 }
 
 // One workgroup per group: bucket totals and bases, per-tile offsets, and the number of
 // buckets of every size class (class-major: ccnt[c * nG + g]).
-__global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+__global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32_t nTot, const uint32_t* __restrict__ TP,
                                                uint32_t* __restrict__ hist, uint32_t* __restrict__ tot,
                                                uint32_t* __restrict__ ccnt, Grp* __restrict__ deep,
                                                uint32_t* __restrict__ n_deep) {
@@ -208,12 +212,12 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
     const uint32_t n = (uint32_t)__popcll(__ballot(cl == (uint32_t)k));
     if (__lane_id() == 0 && n) atomicAdd(&cc[k], n);
   }
-  if (cl == 7u) {  // rare: a bucket still larger than kBig after kDBig characters
+  if (cl == kClsDeep) {  // rare: a bucket still larger than kBig after kDBig characters
     const uint32_t dst_alt = (gr.flags & kGrpIdent) ? 0u : ((gr.flags & kGrpAlt) ^ 1u);
     deep[atomicAdd(n_deep, 1u)] = Grp{base, total, gr.unit, dst_alt | (depth << 2)};
   }
   __syncthreads();
-  if (d < (uint32_t)kNCls) ccnt[(size_t)d * nG + g] = cc[d];
+  if (d < (uint32_t)kNCls) ccnt[(size_t)d * nTot + g] = cc[d];
 }
 
 // Scatter of one tile into the bucket order; the first tile of a group also emits the
@@ -221,7 +225,7 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
 __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
                                                    SortBufs B, SortOut O, const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ tot, const uint32_t* __restrict__ cscan,
-                                                   ClsLists C) {
+                                                   uint32_t nTot, ClsLists C) {
   __shared__ uint32_t cnt[256];
   __shared__ uint32_t base[256];
   __shared__ uint32_t single[256];
@@ -269,7 +273,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, ui
   __syncthreads();
   if (cl < (uint32_t)kNCls) {
     for (uint32_t x = 0; x < w; x++) rank += wc[x][cl];
-    const uint32_t p = C.base[cl] + cscan[(size_t)cl * nG + g] - cscan[(size_t)cl * nG] + rank;
+    const uint32_t p = C.base[cl] + cscan[(size_t)cl * nTot + g] - cscan[(size_t)cl * nTot] + rank;
     C.l[cl][p] = Grp{base[d], total, gr.unit, (dst_alt ? kGrpAlt : 0u) | (depth << 2)};
   }
 }
@@ -284,11 +288,197 @@ __global__ void __launch_bounds__(kT) k_s1_single(const Grp* __restrict__ G, Sor
   if (total == 1) B.sa[s] = B.sa2[s];
 }
 
+
+// ---- packed S1 tiles: groups of kBig+1 .. kSG rotations, several per workgroup (all the
+// groups whose element prefix falls in a kSG window; <= kSGrp groups, < 2 kSG rotations).
+// A group lies in one tile, so its counts, bases and scatter stay in LDS, and singletons can
+// write the primary SA directly.  Two kernels per pass: counts of buckets per size class
+// (for the class-major scan), then the scatter and bucket emission; the second reads the
+// digits the first stored (dig, indexed by slot).
+constexpr uint32_t kSGrp = kSG / (kBig + 1) + 2;
+
+// tile index of item i = P[i] / kSG; mark the first item of each tile and one past its last.
+__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_t* __restrict__ first,
+                             uint32_t* __restrict__ last) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t t = P[i] / kSG;
+  if (i == 0 || P[i - 1] / kSG != t) first[t] = i;
+  if (i == n - 1 || P[i + 1] / kSG != t) last[t] = i + 1;
+}
+
+__global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ sizes) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) sizes[g] = L[g].size;
+}
+
+struct S1sLds {
+  uint32_t cnt[kSGrp * 256];   // bucket counts
+  uint32_t cur[kSGrp * 256];   // bucket cursors (tile-relative)
+  uint32_t gstart[kSGrp], goff[kSGrp + 1], gfl[kSGrp], gunit[kSGrp], gtoff[kSGrp], glen[kSGrp];
+  uint32_t sh[kT / 64];
+  uint32_t cc[kNCls + 1];
+};
+
+// Loads the tile's groups; returns the number of groups (0: empty tile).
+__device__ __forceinline__ uint32_t s1s_setup(S1sLds& S, const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+                                              const uint32_t* __restrict__ last, uint32_t t, const SortBufs& B) {
+  const uint32_t i0 = first[t];
+  if (i0 == 0xffffffffu) return 0;
+  const uint32_t ni = min(last[t], i0 + kSGrp) - i0;
+  if (threadIdx.x < ni) {
+    const Grp g = SG[i0 + threadIdx.x];
+    const Unit U = B.units[g.unit];
+    S.gstart[threadIdx.x] = g.start;
+    S.goff[threadIdx.x + 1] = g.size;
+    S.gfl[threadIdx.x] = g.flags;
+    S.gunit[threadIdx.x] = g.unit;
+    S.gtoff[threadIdx.x] = U.toff;
+    S.glen[threadIdx.x] = U.len;
+  }
+  for (uint32_t i = threadIdx.x; i < ni * 256; i += kT) S.cnt[i] = 0;
+  if (threadIdx.x <= (uint32_t)kNCls) S.cc[threadIdx.x] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    S.goff[0] = 0;
+    for (uint32_t j = 1; j <= ni; j++) S.goff[j] += S.goff[j - 1];
+  }
+  __syncthreads();
+  return ni;
+}
+
+__device__ __forceinline__ uint32_t s1s_owner(const S1sLds& S, uint32_t ni, uint32_t e) {
+  uint32_t j = 0;
+#pragma unroll
+  for (uint32_t q = 1; q < kSGrp; q++) j += (q < ni && e >= S.goff[q]);
+  return j;
+}
+
+__global__ void __launch_bounds__(kT) k_s1s_count(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+                                                  const uint32_t* __restrict__ last, SortBufs B, uint8_t* __restrict__ dig,
+                                                  uint32_t* __restrict__ ccnt, uint32_t nTot, uint32_t ibase) {
+  __shared__ S1sLds S;
+  const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t ni = s1s_setup(S, SG, first, last, t, B);
+  if (ni == 0) {
+    if (threadIdx.x < (uint32_t)kNCls) ccnt[(size_t)threadIdx.x * nTot + ibase + t] = 0;
+    return;
+  }
+  const uint32_t n = S.goff[ni];
+  uint32_t vv[kPerT], jj[kPerT];
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++) {
+    const uint32_t e = i * kT + threadIdx.x;
+    jj[i] = s1s_owner(S, ni, e);
+    vv[i] = 0;
+    if (e < n) {
+      const uint32_t j = jj[i], o = e - S.goff[j], fl = S.gfl[j];
+      vv[i] = (fl & kGrpIdent) ? o : ((fl & kGrpAlt) ? B.sa2 : B.sa)[S.gstart[j] + o];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++) {
+    const uint32_t e = i * kT + threadIdx.x;
+    if (e < n) {
+      const uint32_t j = jj[i];
+      const uint32_t d = B.text[S.gtoff[j] + cyc_pos(vv[i], grp_depth(Grp{0, 0, 0, S.gfl[j]}), S.glen[j])];
+      dig[S.gstart[j] + e - S.goff[j]] = (uint8_t)d;
+      atomicAdd(&S.cnt[j * 256 + d], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < ni * 256; b += kT) {
+    const uint32_t j = b >> 8;
+    const uint32_t cl = bucket_cls(S.cnt[b], grp_depth(Grp{0, 0, 0, S.gfl[j]}) + 1);
+    if (cl < (uint32_t)kNCls) atomicAdd(&S.cc[cl], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < (uint32_t)kNCls) ccnt[(size_t)threadIdx.x * nTot + ibase + t] = S.cc[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(kT) k_s1s_scatter(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+                                                    const uint32_t* __restrict__ last, SortBufs B, SortOut O,
+                                                    const uint8_t* __restrict__ dig, const uint32_t* __restrict__ cscan,
+                                                    uint32_t nTot, uint32_t ibase, ClsLists C) {
+  __shared__ S1sLds S;
+  const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t ni = s1s_setup(S, SG, first, last, t, B);
+  if (ni == 0) return;
+  const uint32_t n = S.goff[ni];
+  uint32_t vv[kPerT], pk[kPerT];  // pk: group | digit << 8
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++) {
+    const uint32_t e = i * kT + threadIdx.x;
+    const uint32_t j = s1s_owner(S, ni, e);
+    vv[i] = 0;
+    pk[i] = j;
+    if (e < n) {
+      const uint32_t o = e - S.goff[j], fl = S.gfl[j];
+      vv[i] = (fl & kGrpIdent) ? o : ((fl & kGrpAlt) ? B.sa2 : B.sa)[S.gstart[j] + o];
+      pk[i] |= (uint32_t)dig[S.gstart[j] + o] << 8;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++)
+    if (i * kT + threadIdx.x < n) atomicAdd(&S.cnt[(pk[i] & 255u) * 256 + (pk[i] >> 8)], 1u);
+  __syncthreads();
+  // tile-relative bucket bases: exclusive scan over the (group, digit) bins
+  {
+    constexpr uint32_t kB = kSGrp * 256 / kT;
+    uint32_t c[kB], sum = 0;
+#pragma unroll
+    for (int q = 0; q < (int)kB; q++) {
+      const uint32_t b = threadIdx.x * kB + q;
+      c[q] = b < ni * 256 ? S.cnt[b] : 0u;
+      sum += c[q];
+    }
+    uint32_t run = block_incl_sum(sum, S.sh, (uint32_t*)nullptr) - sum;
+#pragma unroll
+    for (int q = 0; q < (int)kB; q++) {
+      const uint32_t b = threadIdx.x * kB + q;
+      if (b < ni * 256) S.cur[b] = run;
+      run += c[q];
+    }
+  }
+  __syncthreads();
+  // bucket emission (before the cursors move)
+  for (uint32_t b = threadIdx.x; b < ni * 256; b += kT) {
+    const uint32_t j = b >> 8, total = S.cnt[b];
+    const uint32_t fl = S.gfl[j];
+    const uint32_t depth = grp_depth(Grp{0, 0, 0, fl}) + 1;
+    const uint32_t cl = bucket_cls(total, depth);
+    if (cl == 0xffu) continue;
+    const uint32_t dst_alt = (fl & kGrpIdent) ? 0u : ((fl & kGrpAlt) ^ 1u);
+    const Grp nb{S.gstart[j] + S.cur[b] - S.goff[j], total, S.gunit[j], dst_alt | (depth << 2)};
+    if (cl == kClsDeep) {
+      O.deep[atomicAdd(O.n_deep, 1u)] = nb;
+    } else {
+      const uint32_t r = atomicAdd(&S.cc[cl], 1u);
+      C.l[cl][C.base[cl] + cscan[(size_t)cl * nTot + ibase + t] - cscan[(size_t)cl * nTot] + r] = nb;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++) {
+    if (i * kT + threadIdx.x < n) {
+      const uint32_t j = pk[i] & 255u, d = pk[i] >> 8;
+      const uint32_t fl = S.gfl[j];
+      const uint32_t slot = S.gstart[j] + atomicAdd(&S.cur[j * 256 + d], 1u) - S.goff[j];
+      const bool dst_alt = !(fl & kGrpIdent) && !(fl & kGrpAlt);
+      (dst_alt ? B.sa2 : B.sa)[slot] = vv[i];
+      if (S.cnt[j * 256 + d] == 1) {
+        // a bucket of one: ordered (the group lies in this tile, so the primary SA is free)
+        emit_final(B, O, B.units[S.gunit[j]], S.gunit[j], slot, vv[i], true);
+      }
+    }
+  }
+}
+
 // out[c] = start of class c in the class-major scan (c < kNCls), out[kNCls] = total.
-__global__ void k_cls_bounds(const uint32_t* __restrict__ cscan, uint32_t nG, const uint32_t* __restrict__ total,
+__global__ void k_cls_bounds(const uint32_t* __restrict__ cscan, uint32_t nTot, const uint32_t* __restrict__ total,
                              uint32_t* __restrict__ out) {
   const uint32_t c = threadIdx.x;
-  if (c < (uint32_t)kNCls) out[c] = cscan[(size_t)c * nG];
+  if (c < (uint32_t)kNCls) out[c] = cscan[(size_t)c * nTot];
   if (c == (uint32_t)kNCls) out[c] = *total;
 }
 
@@ -395,16 +585,25 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
 // Round 1 sorts by the first 8 characters after the bucket's depth; every later round
 // re-keys only the runs still tied, 8 characters deeper, and re-sorts (positions of unique
 // elements never move since their run start is their own position).
+// The 96-bit key (run start:16, hi:32, lo:32, element index:16) in three words, so that
+// the order is the lexicographic order of (d0:d1 as 64 bits, d2).  Pads: run start 0xffff.
 struct BsortKey {
-  uint32_t w0;  // run start << 16 | element index (pads: 0xffff << 16)
-  uint32_t hi, lo;
+  uint32_t d0, d1, d2;
 };
 
-// (run start, key, index) order; branch-free: (rs:hi) and (lo:idx) as 48-bit integers.
+__device__ __forceinline__ BsortKey make_key(uint32_t rs, uint32_t hi, uint32_t lo, uint32_t idx) {
+  return BsortKey{(rs << 16) | (hi >> 16), (hi << 16) | (lo >> 16), (lo << 16) | idx};
+}
+__device__ __forceinline__ uint32_t key_rs(const BsortKey& k) { return k.d0 >> 16; }
+__device__ __forceinline__ uint32_t key_idx(const BsortKey& k) { return k.d2 & 0xffffu; }
+// same run start and characters (index ignored)
+__device__ __forceinline__ bool key_tied(const BsortKey& a, const BsortKey& b) {
+  return a.d0 == b.d0 && a.d1 == b.d1 && (a.d2 >> 16) == (b.d2 >> 16);
+}
+
 __device__ __forceinline__ bool key_less(const BsortKey& a, const BsortKey& b) {
-  const uint64_t a1 = ((uint64_t)(a.w0 >> 16) << 32) | a.hi, b1 = ((uint64_t)(b.w0 >> 16) << 32) | b.hi;
-  const uint64_t a2 = ((uint64_t)a.lo << 16) | (a.w0 & 0xffffu), b2 = ((uint64_t)b.lo << 16) | (b.w0 & 0xffffu);
-  return (a1 < b1) | ((a1 == b1) & (a2 < b2));
+  const uint64_t a1 = ((uint64_t)a.d0 << 32) | a.d1, b1 = ((uint64_t)b.d0 << 32) | b.d1;
+  return (a1 < b1) | ((a1 == b1) & (a.d2 < b.d2));
 }
 
 // x from lane ^ J (J < 64): DPP within quads, ds_swizzle within 32 lanes, bpermute across.
@@ -422,9 +621,9 @@ __device__ __forceinline__ void bitonic_xlane(BsortKey (&K)[kPer], int k, uint32
   BsortKey o[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; r++) {
-    o[r].w0 = xor_lane<jl>(K[r].w0);
-    o[r].hi = xor_lane<jl>(K[r].hi);
-    o[r].lo = xor_lane<jl>(K[r].lo);
+    o[r].d0 = xor_lane<jl>(K[r].d0);
+    o[r].d1 = xor_lane<jl>(K[r].d1);
+    o[r].d2 = xor_lane<jl>(K[r].d2);
   }
 #pragma unroll
   for (int r = 0; r < kPer; r++) {
@@ -484,8 +683,8 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
   uint32_t v[kPer], pos[kPer], cls[kPer], rlen[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; r++) {
-    live[r] = !done[r] && (K[r].w0 >> 16) != 0xffffu;
-    v[r] = live[r] ? Lv[K[r].w0 & 0xffffu] : 0u;
+    live[r] = !done[r] && key_rs(K[r]) != 0xffffu;
+    v[r] = live[r] ? Lv[key_idx(K[r])] : 0u;
     pos[r] = rsn[r];
     cls[r] = rsn[r];
     Lk[lane * kPer + r] = 0;
@@ -601,9 +800,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     }
     Lv[w][idx] = vq[r];
     Lc[w][idx] = c;
-    K[r].w0 = (valid ? 0u : 0xffff0000u) | idx;
-    K[r].hi = hi;
-    K[r].lo = lo;
+    K[r] = make_key(valid ? 0u : 0xffffu, hi, lo, idx);
   }
   bool done[kPer];
 #pragma unroll
@@ -619,12 +816,12 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
       if (r > 0) {
         q = K[r - 1];
       } else {
-        q.w0 = (uint32_t)__shfl_up((int)K[kPer - 1].w0, 1, 64);
-        q.hi = (uint32_t)__shfl_up((int)K[kPer - 1].hi, 1, 64);
-        q.lo = (uint32_t)__shfl_up((int)K[kPer - 1].lo, 1, 64);
-        if (sl == 0) q.w0 = 0xfffe0000u;  // no previous element
+        q.d0 = (uint32_t)__shfl_up((int)K[kPer - 1].d0, 1, 64);
+        q.d1 = (uint32_t)__shfl_up((int)K[kPer - 1].d1, 1, 64);
+        q.d2 = (uint32_t)__shfl_up((int)K[kPer - 1].d2, 1, 64);
+        if (sl == 0) q.d0 = 0xfffe0000u;  // no previous element
       }
-      tp[r] = (K[r].w0 >> 16) != 0xffffu && (q.w0 >> 16) == (K[r].w0 >> 16) && q.hi == K[r].hi && q.lo == K[r].lo;
+      tp[r] = key_rs(K[r]) != 0xffffu && key_tied(q, K[r]);
     }
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
@@ -657,8 +854,8 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
       rsn[r] = max(rsn[r], pre);
-      const uint32_t idx = K[r].w0 & 0xffffu;
-      const bool valid = (K[r].w0 >> 16) != 0xffffu;
+      const uint32_t idx = key_idx(K[r]);
+      const bool valid = key_rs(K[r]) != 0xffffu;
       const bool tied = valid && (tp[r] || tn[r]);
       const uint32_t p = sl * kPer + r;
       if (valid && !tied && !done[r]) {
@@ -682,19 +879,16 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
-      const uint32_t idx = K[r].w0 & 0xffffu;
-      const bool valid = (K[r].w0 >> 16) != 0xffffu;
+      const uint32_t idx = key_idx(K[r]);
+      const bool valid = key_rs(K[r]) != 0xffffu;
       if (!valid) continue;
       const uint32_t p = sl * kPer + r;
       if (done[r]) {
-        K[r].w0 = (p << 16) | idx;
-        K[r].hi = K[r].lo = 0;
+        K[r] = make_key(p, 0, 0, idx);
       } else {
         uint32_t hi, lo;
         text_key8(t, U.len, cyc_pos(Lv[w][idx], depth, U.len), hi, lo);
-        K[r].w0 = (rsn[r] << 16) | idx;
-        K[r].hi = hi;
-        K[r].lo = lo;
+        K[r] = make_key(rsn[r], hi, lo, idx);
       }
     }
   }
@@ -791,19 +985,29 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     ccap[c] = S / minsz + nb + 16;
     C.l[c] = ws.typed<Grp>("sort_cls" + std::to_string(c), ccap[c]);
   }
-  Grp* next = ws.typed<Grp>("sort_next", ccap[6]);
+  Grp* nxt6 = ws.typed<Grp>("sort_nxt6", ccap[6]);
+  Grp* nxt7 = ws.typed<Grp>("sort_nxt7", ccap[7]);
   SortOut O{};
   O.bwt = bwt;
   O.rank0 = rank0;
   O.deep = ws.typed<Grp>("sort_deep", S / 2 + nb + 16);
-  uint32_t* cnt = ws.u32("sort_cnt", 64);  // 0..6 class counts (init), 8..15 class bounds, 16 n_deep, 17 tiles, 18 min depth
-  O.n_deep = cnt + 16;
-  const size_t max_tiles = S / kDTile + ccap[6] + 16;
+  // counters: 0..7 class counts (init), 8..16 class bounds + total, 17 tiles, 18 packed total,
+  // 19 n_deep, 20 min depth
+  uint32_t* cnt = ws.u32("sort_cnt", 64);
+  O.n_deep = cnt + 19;
+  const size_t max_tiles = S / kDTile + ccap[7] + 16;
+  const size_t max_ptiles = S / kSG + 64;
+  const size_t max_tot = ccap[7] + max_ptiles;
   uint32_t* TP = ws.u32("sort_TP", max_tiles + 16);
   uint32_t* hist = ws.u32("sort_hist", max_tiles * 256);
-  uint32_t* tot = ws.u32("sort_tot", ccap[6] * 256);
-  uint32_t* ccnt = ws.u32("sort_ccnt", kNCls * ccap[6] + 16);
-  uint32_t* scratch = ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(kNCls * ccap[6], max_tiles)) + 64);
+  uint32_t* tot = ws.u32("sort_tot", ccap[7] * 256);
+  uint32_t* ccnt = ws.u32("sort_ccnt", kNCls * max_tot + 16);
+  uint32_t* P = ws.u32("sort_P", ccap[6] + 16);
+  uint32_t* first = ws.u32("sort_first", max_ptiles);
+  uint32_t* last = ws.u32("sort_last", max_ptiles);
+  uint8_t* dig = ws.u8("sort_dig", S + 16);
+  uint32_t* scratch =
+      ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[6])) + 64);
   uint32_t hc[24];
   auto read_counters = [&]() {
     HIP_OK(hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, st));
@@ -818,46 +1022,70 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   read_counters();
   uint32_t ncls[kNCls];
   for (int c = 0; c < kNCls; c++) ncls[c] = hc[c];
-  uint32_t n_big = ncls[6];
-  Grp* big = C.l[6];
-  Grp* nxt = next;
+  uint32_t n6 = ncls[6], n7 = ncls[7];
+  Grp* cur6 = C.l[6];
+  Grp* cur7 = C.l[7];
   int passes = 0;
   uint64_t s1_elems = 0;
-  // ---- S1: byte passes over the buckets larger than kBig
-  while (n_big > 0) {
+  // ---- S1: byte passes over the buckets larger than kBig (tiled groups > kSG, packed ones <= kSG)
+  while (n6 + n7 > 0) {
     ++passes;
-    k_group_tiles<<<grid(n_big), kT, 0, st>>>(big, n_big, TP);
-    HIP_OK(hipGetLastError());
-    scan_u32(ScanOp::Sum, true, TP, TP, n_big, cnt + 17, scratch, st);
-    read_counters();
-    const uint32_t ntiles = hc[17];
-    if (debug) {
-      std::vector<Grp> hg(n_big);
-      HIP_OK(hipMemcpy(hg.data(), big, sizeof(Grp) * n_big, hipMemcpyDeviceToHost));
-      uint64_t el = 0;
-      for (const Grp& g : hg) el += g.size;
-      s1_elems += el;
-      fprintf(stderr, "[bzg sort S1] pass %d: groups=%u elems=%lu tiles=%u\n", passes, n_big, el, ntiles);
+    if (n7) {
+      k_group_tiles<<<grid(n7), kT, 0, st>>>(cur7, n7, TP);
+      HIP_OK(hipGetLastError());
+      scan_u32(ScanOp::Sum, true, TP, TP, n7, cnt + 17, scratch, st);
     }
-    k_s1_hist<<<ntiles, kT, 0, st>>>(big, n_big, TP, B, hist);
-    HIP_OK(hipGetLastError());
-    k_s1_off<<<n_big, kT, 0, st>>>(big, n_big, TP, hist, tot, ccnt, O.deep, O.n_deep);
-    HIP_OK(hipGetLastError());
-    scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * n_big, cnt + 15, scratch, st);
-    k_cls_bounds<<<1, 64, 0, st>>>(ccnt, n_big, cnt + 15, cnt + 8);
+    if (n6) {
+      k_group_sizes<<<grid(n6), kT, 0, st>>>(cur6, n6, P);
+      HIP_OK(hipGetLastError());
+      scan_u32(ScanOp::Sum, true, P, P, n6, cnt + 18, scratch, st);
+    }
+    read_counters();
+    const uint32_t ntl = n7 ? hc[17] : 0;
+    const uint32_t nT = n6 ? ceil_div(hc[18], kSG) : 0;
+    const uint32_t nTot = n7 + nT;
+    if (debug) {
+      fprintf(stderr, "[bzg sort S1] pass %d: tiled groups=%u tiles=%u | packed groups=%u elems=%u tiles=%u\n", passes,
+              n7, ntl, n6, n6 ? hc[18] : 0, nT);
+      s1_elems += n6 ? hc[18] : 0;
+    }
+    if (nT) {
+      HIP_OK(hipMemsetAsync(first, 0xff, (size_t)nT * 4, st));
+      k_tile_first<<<grid(n6), kT, 0, st>>>(P, n6, first, last);
+      HIP_OK(hipGetLastError());
+      k_s1s_count<<<nT, kT, 0, st>>>(cur6, first, last, B, dig, ccnt, nTot, n7);
+      HIP_OK(hipGetLastError());
+    }
+    if (n7) {
+      k_s1_hist<<<ntl, kT, 0, st>>>(cur7, n7, TP, B, hist);
+      HIP_OK(hipGetLastError());
+      k_s1_off<<<n7, kT, 0, st>>>(cur7, nTot, TP, hist, tot, ccnt, O.deep, O.n_deep);
+      HIP_OK(hipGetLastError());
+    }
+    scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * nTot, cnt + 16, scratch, st);
+    k_cls_bounds<<<1, 64, 0, st>>>(ccnt, nTot, cnt + 16, cnt + 8);
     HIP_OK(hipGetLastError());
     ClsLists Cp = C;
     for (int c = 0; c < 6; c++) Cp.base[c] = ncls[c];
-    Cp.l[6] = nxt;
-    Cp.base[6] = 0;
-    k_s1_scatter<<<ntiles, kT, 0, st>>>(big, n_big, TP, B, O, hist, tot, ccnt, Cp);
-    HIP_OK(hipGetLastError());
-    k_s1_single<<<n_big, kT, 0, st>>>(big, B, tot);
-    HIP_OK(hipGetLastError());
+    Cp.l[6] = nxt6;
+    Cp.l[7] = nxt7;
+    Cp.base[6] = Cp.base[7] = 0;
+    if (n7) {
+      k_s1_scatter<<<ntl, kT, 0, st>>>(cur7, n7, TP, B, O, hist, tot, ccnt, nTot, Cp);
+      HIP_OK(hipGetLastError());
+      k_s1_single<<<n7, kT, 0, st>>>(cur7, B, tot);
+      HIP_OK(hipGetLastError());
+    }
+    if (nT) {
+      k_s1s_scatter<<<nT, kT, 0, st>>>(cur6, first, last, B, O, dig, ccnt, nTot, n7, Cp);
+      HIP_OK(hipGetLastError());
+    }
     read_counters();
     for (int c = 0; c < 6; c++) ncls[c] += hc[8 + c + 1] - hc[8 + c];
-    n_big = hc[8 + kNCls] - hc[8 + 6];
-    std::swap(big, nxt);
+    n6 = hc[8 + 7] - hc[8 + 6];
+    n7 = hc[8 + 8] - hc[8 + 7];
+    std::swap(cur6, nxt6);
+    std::swap(cur7, nxt7);
   }
   // ---- S2: every size class
   if (debug)
@@ -871,7 +1099,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   if (ncls[5]) k_bsort<64, 4><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O);
   HIP_OK(hipGetLastError());
   read_counters();
-  const uint32_t n_deep = hc[16];
+  const uint32_t n_deep = hc[19];
   int dbl_iters = 0;
   uint64_t dbl_elems = 0;
   std::vector<uint32_t> fb_units;
@@ -882,13 +1110,13 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     B.key2 = ws.u32("sort_key2", S + 16);
     uint32_t* uflag = ws.u32("sort_uflag", nb + 16);
     HIP_OK(hipMemsetAsync(uflag, 0, 4 * (size_t)nb, st));
-    HIP_OK(hipMemsetAsync(cnt + 18, 0xff, 4, st));
-    k_fb_flag<<<grid(n_deep), kT, 0, st>>>(O.deep, n_deep, uflag, cnt + 18);
+    HIP_OK(hipMemsetAsync(cnt + 20, 0xff, 4, st));
+    k_fb_flag<<<grid(n_deep), kT, 0, st>>>(O.deep, n_deep, uflag, cnt + 20);
     HIP_OK(hipGetLastError());
     std::vector<uint32_t> hf(nb);
     HIP_OK(hipMemcpyAsync(hf.data(), uflag, 4 * (size_t)nb, hipMemcpyDeviceToHost, st));
     read_counters();
-    const uint32_t h0 = hc[18];
+    const uint32_t h0 = hc[20];
     uint32_t flen = 0;
     for (uint32_t b = 0; b < nb; b++)
       if (hf[b]) {

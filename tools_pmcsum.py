@@ -1,10 +1,21 @@
 """Per-kernel sums of PMC counters from tools_pmc.sh output: python tools_pmcsum.py <dir>"""
-import csv, glob, sys, collections
+import collections
+import csv
+import glob
+import re
+import sys
+
+
+def short(name):
+    m = re.search(r"::(k_\w+)", name)
+    return m.group(1) if m else name[:30]
+
+
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        agg[r["Kernel_Name"][:30]][r["Counter_Name"]] += float(r["Counter_Value"])
+        agg[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
 names = sorted({c for k in agg.values() for c in k})
-print(f'{"kernel":30s} ' + " ".join(f"{n[:14]:>14s}" for n in names))
+print(f'{"kernel":22s} ' + " ".join(f"{n[3:17]:>14s}" for n in names))
 for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1].values()))[:24]:
-    print(f"{k:30s} " + " ".join(f"{v.get(n, 0):14.4g}" for n in names))
+    print(f"{k:22s} " + " ".join(f"{v.get(n, 0):14.4g}" for n in names))
