@@ -18,27 +18,6 @@ namespace bzg {
 namespace {
 constexpr int kT = 256;
 
-struct CodeLds {
-  uint32_t rfreq[kNGroups][kMaxAlpha];
-  uint32_t code[kNGroups][kMaxAlpha];
-  uint32_t lenp[2][kMaxAlpha];  // code lengths of tables 0-2 / 3-5 packed in 10-bit fields
-  union {
-    struct {
-      int32_t weight[kNGroups][kMaxAlpha * 2];
-      int32_t parent[kNGroups][kMaxAlpha * 2];
-      int32_t heap[kNGroups][kMaxAlpha + 4];
-    } h;                                     // Huffman construction
-    uint16_t chunk[kT * kGroupSize + 8];     // MTF values of kT consecutive selector groups
-  } u;
-  uint8_t len[kNGroups][kMaxAlpha + 2];
-  uint8_t sel[kMaxSelectors + 4];
-  uint32_t freq[kMaxAlpha];
-  uint32_t sh[8];
-  uint32_t misc[16];
-};
-
-static_assert(2 * sizeof(CodeLds) <= 160 * 1024, "two table workgroups must fit one CU's LDS");
-
 // BZ2_hbMakeCodeLengths (huffman.c:63-148) on one lane: leaf weight = max(freq,1) << 8 | 0,
 // merge = sum of weights | (1 + max depth); heap moves use strict '<'; rescale with
 // w = 1 + w/2 while any length exceeds max_len.
@@ -105,191 +84,236 @@ __device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, i
   }
 }
 
-// Per-block table optimisation.  Outputs (global, per block b):
-//   lens[b][6][258], codes[b][6][258], sel[b][nsel] (table ids), selmtf[b][nsel],
-//   gbits[b][nsel] (payload bits per 50-group), info[b] = {nGroups, nSel, alpha, bits}
-__global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv, const uint32_t* __restrict__ mtf_off,
-                                               const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ freq_g,
-                                               const uint32_t* __restrict__ ninuse, const uint32_t* __restrict__ inuse,
-                                               uint8_t* __restrict__ lens_g, uint32_t* __restrict__ codes_g,
-                                               uint8_t* __restrict__ sel_g, uint8_t* __restrict__ selmtf_g,
-                                               uint16_t* __restrict__ gbits_g, uint32_t* __restrict__ info_g,
-                                               uint64_t* __restrict__ stamps) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  CodeLds& S = *reinterpret_cast<CodeLds*>(smem);
-  uint64_t t_last = stamps ? __builtin_amdgcn_s_memtime() : 0;
-  // diagnostic phase stamps (BZG_DEBUG): s_memtime ticks summed over workgroups
-  auto stamp = [&](int k) {
-    if (stamps) {
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        const uint64_t now = __builtin_amdgcn_s_memtime();
-        atomicAdd((unsigned long long*)&stamps[k], (unsigned long long)(now - t_last));
-        t_last = now;
+__device__ __forceinline__ int n_groups(uint32_t nmtf) {  // compress.c:266-270
+  return nmtf < 200 ? 2 : nmtf < 600 ? 3 : nmtf < 1200 ? 4 : nmtf < 2400 ? 5 : 6;
+}
+
+// ---- table optimisation (sendMTFValues, compress.c:250-561), one kernel per step:
+//   k_init_tables: the initial contiguous partition (compress.c:276-319);
+//   4 x { k_cf: cost of every 50-symbol group under each table, selection (lowest index wins
+//          ties, compress.c:416-420) and per-table symbol frequencies -- several workgroups
+//          per block, each over a slice of the groups;
+//         k_huff: BZ2_hbMakeCodeLengths for every (block, table), one wave each };
+//   k_cf (final mode): payload bits of every group under the final tables;
+//   k_final: canonical codes, selector MTF, table and header bit counts.
+constexpr uint32_t kCfSlices = 8;  // workgroups per block in k_cf
+
+__global__ void k_init_tables(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ freq_g,
+                              const uint32_t* __restrict__ ninuse, uint8_t* __restrict__ lens_g,
+                              uint32_t* __restrict__ rf_g) {
+  const uint32_t b = blockIdx.x;
+  uint8_t* L = lens_g + (size_t)b * kNGroups * kMaxAlpha;
+  for (int i = threadIdx.x; i < kNGroups * kMaxAlpha; i += blockDim.x) {
+    L[i] = 0;
+    rf_g[(size_t)b * kNGroups * kMaxAlpha + i] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const uint32_t nmtf = nmtf_g[b];
+  const int alpha = (int)ninuse[b] + 2;
+  const int ng = n_groups(nmtf);
+  const uint32_t* freq = freq_g + (size_t)b * kMaxAlpha;
+  for (int t = 0; t < ng; t++)
+    for (int v = 0; v < alpha; v++) L[t * kMaxAlpha + v] = 15;
+  int part = ng, rem = (int)nmtf, gs = 0;
+  while (part > 0) {
+    const int target = rem / part;
+    int ge = gs - 1, acc = 0;
+    while (acc < target && ge < alpha - 1) acc += (int)freq[++ge];
+    if (ge > gs && part != ng && part != 1 && ((ng - part) % 2 == 1)) acc -= (int)freq[ge--];
+    for (int v = gs; v <= ge; v++) L[(part - 1) * kMaxAlpha + v] = 0;
+    part--;
+    gs = ge + 1;
+    rem -= acc;
+  }
+}
+
+struct CfLds {
+  uint32_t lenp[2][kMaxAlpha];       // lengths of tables 0-2 / 3-5 in 10-bit fields
+  uint32_t rfreq[kNGroups][kMaxAlpha];
+  uint16_t chunk[kT * kGroupSize + 8];
+  uint32_t sh[8];
+};
+
+// final == 0: select tables and count frequencies (into rf_g); final == 1: payload bits of
+// every group under its (already chosen) table into gbits_g, their sum into info_g[b*8+6].
+__global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, const uint32_t* __restrict__ mtf_off,
+                                           const uint32_t* __restrict__ nmtf_g, const uint8_t* __restrict__ lens_g,
+                                           uint8_t* __restrict__ sel_g, uint32_t* __restrict__ rf_g,
+                                           uint16_t* __restrict__ gbits_g, uint32_t* __restrict__ info_g, int final) {
+  __shared__ CfLds S;
+  const uint32_t b = blockIdx.y;
+  const uint32_t nmtf = nmtf_g[b];
+  const uint32_t nsel = ceil_div(nmtf, kGroupSize);
+  const uint32_t nch = ceil_div(nsel, kT);
+  const uint32_t cps = ceil_div(nch, kCfSlices);
+  const uint32_t c0 = blockIdx.x * cps, c1 = min(nch, c0 + cps);
+  if (c0 >= c1) return;
+  const int ng = n_groups(nmtf);
+  const uint16_t* mv = mtfv + mtf_off[b];
+  const uint8_t* L = lens_g + (size_t)b * kNGroups * kMaxAlpha;
+  for (int v = threadIdx.x; v < kMaxAlpha; v += kT) {
+    S.lenp[0][v] = L[v] | ((uint32_t)L[kMaxAlpha + v] << 10) | ((uint32_t)L[2 * kMaxAlpha + v] << 20);
+    S.lenp[1][v] = L[3 * kMaxAlpha + v] | ((uint32_t)L[4 * kMaxAlpha + v] << 10) | ((uint32_t)L[5 * kMaxAlpha + v] << 20);
+  }
+  if (!final)
+    for (int i = threadIdx.x; i < kNGroups * kMaxAlpha; i += kT) (&S.rfreq[0][0])[i] = 0;
+  uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
+  uint32_t mybits = 0;
+  for (uint32_t ch = c0; ch < c1; ch++) {
+    const uint32_t g0 = ch * kT;
+    const uint32_t lo = g0 * kGroupSize, hi = min((g0 + kT) * kGroupSize, nmtf);
+    __syncthreads();
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) S.chunk[i - lo] = mv[i];
+    __syncthreads();
+    const uint32_t g = g0 + threadIdx.x;
+    if (g < nsel) {
+      const uint16_t* c = S.chunk + threadIdx.x * kGroupSize;
+      const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
+      uint32_t a = 0, bsum = 0;
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t v = c[i];
+        a += S.lenp[0][v];
+        bsum += S.lenp[1][v];
+      }
+      // 50 lengths <= 17: every 10-bit field sum stays below 1024
+      const uint32_t cost[kNGroups] = {a & 1023u, (a >> 10) & 1023u, a >> 20,
+                                       bsum & 1023u, (bsum >> 10) & 1023u, bsum >> 20};
+      if (final) {
+        const uint32_t bits = cost[selo[g]];
+        gbits_g[(size_t)b * kMaxSelectors + g] = (uint16_t)bits;
+        mybits += bits;
+      } else {
+        int bt = 0;  // lowest index wins ties (compress.c:416-420)
+        uint32_t bc = cost[0];
+        for (int t = 1; t < ng; t++)
+          if (cost[t] < bc) {
+            bc = cost[t];
+            bt = t;
+          }
+        selo[g] = (uint8_t)bt;
+        for (uint32_t i = 0; i < n; i++) atomicAdd(&S.rfreq[bt][c[i]], 1u);
       }
     }
-  };
+  }
+  __syncthreads();
+  if (final) {
+    uint32_t tot;
+    block_incl_sum(mybits, S.sh, &tot);
+    if (threadIdx.x == 0) atomicAdd(&info_g[(size_t)b * 8 + 6], tot);
+  } else {
+    uint32_t* rf = rf_g + (size_t)b * kNGroups * kMaxAlpha;
+    for (int i = threadIdx.x; i < ng * kMaxAlpha; i += kT) {
+      const uint32_t v = (&S.rfreq[0][0])[i];
+      if (v) atomicAdd(&rf[i], v);
+    }
+  }
+}
+
+// BZ2_hbMakeCodeLengths for table t of block b (one wave; the heap work is sequential).
+__global__ void __launch_bounds__(64) k_huff(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
+                                             uint32_t* __restrict__ rf_g, uint8_t* __restrict__ lens_g) {
+  __shared__ int32_t heap[kMaxAlpha + 4];
+  __shared__ int32_t weight[kMaxAlpha * 2];
+  __shared__ int32_t parent[kMaxAlpha * 2];
+  __shared__ uint32_t fq[kMaxAlpha];
+  __shared__ uint8_t len[kMaxAlpha + 2];
+  const uint32_t b = blockIdx.x / kNGroups, t = blockIdx.x % kNGroups;
+  const int ng = n_groups(nmtf_g[b]);
+  if ((int)t >= ng) return;
+  const int alpha = (int)ninuse[b] + 2;
+  uint32_t* rf = rf_g + ((size_t)b * kNGroups + t) * kMaxAlpha;
+  for (int v = threadIdx.x; v < alpha; v += 64) {
+    fq[v] = rf[v];
+    rf[v] = 0;  // ready for the next iteration
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) hb_code_lengths(len, fq, alpha, kMaxCodeLen, heap, weight, parent);
+  __syncthreads();
+  uint8_t* L = lens_g + ((size_t)b * kNGroups + t) * kMaxAlpha;
+  for (int v = threadIdx.x; v < alpha; v += 64) L[v] = len[v];
+}
+
+// Canonical codes (huffman.c:152-166), selector MTF (compress.c:573-631), table bits
+// (compress.c:694-706) and the block's total bit count.  info_g[b*8+6] holds the payload bits.
+__global__ void __launch_bounds__(kT) k_final(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
+                                              const uint32_t* __restrict__ inuse, const uint8_t* __restrict__ lens_g,
+                                              uint32_t* __restrict__ codes_g, const uint8_t* __restrict__ sel_g,
+                                              uint8_t* __restrict__ selmtf_g, uint32_t* __restrict__ info_g) {
+  __shared__ uint8_t len[kNGroups][kMaxAlpha + 2];
+  __shared__ uint8_t sel[kMaxSelectors + 4];
+  __shared__ uint32_t sh[8];
+  __shared__ uint32_t misc[16];
   const uint32_t b = blockIdx.x;
   const uint32_t nmtf = nmtf_g[b];
-  const uint16_t* mv = mtfv + mtf_off[b];
   const int alpha = (int)ninuse[b] + 2;
-  const int ng = nmtf < 200 ? 2 : nmtf < 600 ? 3 : nmtf < 1200 ? 4 : nmtf < 2400 ? 5 : 6;
+  const int ng = n_groups(nmtf);
   const uint32_t nsel = ceil_div(nmtf, kGroupSize);
-  for (int i = threadIdx.x; i < kMaxAlpha; i += kT) S.freq[i] = freq_g[(size_t)b * kMaxAlpha + i];
+  for (int i = threadIdx.x; i < kNGroups * kMaxAlpha; i += kT)
+    len[i / kMaxAlpha][i % kMaxAlpha] = lens_g[(size_t)b * kNGroups * kMaxAlpha + i];
+  for (uint32_t g = threadIdx.x; g < nsel; g += kT) sel[g] = sel_g[(size_t)b * kMaxSelectors + g];
   __syncthreads();
-  // initial tables (compress.c:276-319); tables >= ng stay all-zero so packed sums cannot overflow
-  for (int i = threadIdx.x; i < kNGroups * (kMaxAlpha + 2); i += kT) (&S.len[0][0])[i] = 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int t = 0; t < ng; t++)
-      for (int v = 0; v < alpha; v++) S.len[t][v] = 15;
-    int part = ng, rem = (int)nmtf, gs = 0;
-    while (part > 0) {
-      const int target = rem / part;
-      int ge = gs - 1, acc = 0;
-      while (acc < target && ge < alpha - 1) acc += (int)S.freq[++ge];
-      if (ge > gs && part != ng && part != 1 && ((ng - part) % 2 == 1)) acc -= (int)S.freq[ge--];
-      for (int v = gs; v <= ge; v++) S.len[part - 1][v] = 0;
-      part--;
-      gs = ge + 1;
-      rem -= acc;
-    }
-  }
-  __syncthreads();
-  // Visit every selector group with its six table costs (50 lengths <= 17: sums < 1024).
-  // Symbols are staged through LDS kT groups at a time; lane l owns group g0 + l.
-  auto for_groups = [&](auto&& f) {
-    for (int v = threadIdx.x; v < kMaxAlpha; v += kT) {
-      S.lenp[0][v] = S.len[0][v] | ((uint32_t)S.len[1][v] << 10) | ((uint32_t)S.len[2][v] << 20);
-      S.lenp[1][v] = S.len[3][v] | ((uint32_t)S.len[4][v] << 10) | ((uint32_t)S.len[5][v] << 20);
-    }
-    for (uint32_t g0 = 0; g0 < nsel; g0 += kT) {
-      const uint32_t lo = g0 * kGroupSize, hi = min((g0 + kT) * kGroupSize, nmtf);
-      for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) S.u.chunk[i - lo] = mv[i];
-      __syncthreads();
-      const uint32_t g = g0 + threadIdx.x;
-      if (g < nsel) {
-        const uint16_t* c = S.u.chunk + threadIdx.x * kGroupSize;
-        const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
-        uint32_t a = 0, bsum = 0;
-        for (uint32_t i = 0; i < n; i++) {
-          const uint32_t v = c[i];
-          a += S.lenp[0][v];
-          bsum += S.lenp[1][v];
-        }
-        const uint32_t cost[kNGroups] = {a & 1023u, (a >> 10) & 1023u, a >> 20, bsum & 1023u, (bsum >> 10) & 1023u, bsum >> 20};
-        f(g, c, n, cost);
+  // canonical codes: lane t of wave t
+  if ((threadIdx.x & 63) == 0 && (int)(threadIdx.x >> 6) < ng) {
+    for (int t = threadIdx.x >> 6; t < ng; t += kT / 64) {
+      int mn = 32, mx = 0;
+      for (int v = 0; v < alpha; v++) {
+        mn = min(mn, (int)len[t][v]);
+        mx = max(mx, (int)len[t][v]);
       }
-      __syncthreads();
-    }
-  };
-  for (int it = 0; it < kIters; it++) {
-    for (int i = threadIdx.x; i < kNGroups * kMaxAlpha; i += kT) (&S.rfreq[0][0])[i] = 0;
-    __syncthreads();
-    for_groups([&](uint32_t g, const uint16_t* c, uint32_t n, const uint32_t* cost) {
-      int bt = 0;  // lowest index wins ties (compress.c:416-420)
-      uint32_t bc = cost[0];
-      for (int t = 1; t < ng; t++)
-        if (cost[t] < bc) {
-          bc = cost[t];
-          bt = t;
-        }
-      S.sel[g] = (uint8_t)bt;
-      for (uint32_t i = 0; i < n; i++) atomicAdd(&S.rfreq[bt][c[i]], 1u);
-    });
-    stamp(0);
-    if (threadIdx.x < (unsigned)ng) {
-      const int t = threadIdx.x;
-      hb_code_lengths(S.len[t], S.rfreq[t], alpha, kMaxCodeLen, S.u.h.heap[t], S.u.h.weight[t], S.u.h.parent[t]);
-    }
-    __syncthreads();
-    stamp(1);
-  }
-  // selector table ids out
-  uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
-  for (uint32_t g = threadIdx.x; g < nsel; g += kT) selo[g] = S.sel[g];
-  // canonical codes (huffman.c:152-166)
-  if (threadIdx.x < (unsigned)ng) {
-    const int t = threadIdx.x;
-    int mn = 32, mx = 0;
-    for (int v = 0; v < alpha; v++) {
-      mn = min(mn, (int)S.len[t][v]);
-      mx = max(mx, (int)S.len[t][v]);
-    }
-    uint32_t c = 0;
-    for (int l = mn; l <= mx; l++) {
-      for (int v = 0; v < alpha; v++)
-        if (S.len[t][v] == l) S.code[t][v] = c++;
-      c <<= 1;
+      uint32_t* co = codes_g + ((size_t)b * kNGroups + t) * kMaxAlpha;
+      uint32_t c = 0;
+      for (int l = mn; l <= mx; l++) {
+        for (int v = 0; v < alpha; v++)
+          if (len[t][v] == l) co[v] = c++;
+        c <<= 1;
+      }
+      int cur = len[t][0];
+      uint32_t bits = 5;
+      for (int v = 0; v < alpha; v++) {
+        const int l = len[t][v];
+        bits += 1 + 2 * (uint32_t)(l > cur ? l - cur : cur - l);
+        cur = l;
+      }
+      misc[8 + t] = bits;
     }
   }
-  __syncthreads();
-  // payload bits per group
-  uint32_t mybits = 0;
-  uint16_t* gb = gbits_g + (size_t)b * kMaxSelectors;
-  for_groups([&](uint32_t g, const uint16_t*, uint32_t, const uint32_t* cost) {
-    const uint32_t bits = cost[S.sel[g]];
-    gb[g] = (uint16_t)bits;
-    mybits += bits;
-  });
-  uint32_t data_bits;
-  block_incl_sum(mybits, S.sh, &data_bits);
-  stamp(2);
-  // selector MTF (compress.c:573-631) in parallel: the MTF index of selector s at g is the
-  // number of tables used more recently than s, where the initial order 0..5 counts as
-  // uses at times -1..-6.  Thread k owns a contiguous run of selectors; the last use of
-  // every table before the run comes from a block max-scan.
+  // selector MTF in parallel: the MTF index of selector s at g is the number of tables used
+  // more recently than s, where the initial order 0..5 counts as uses at times -1..-6.
+  // Thread k owns a contiguous run of selectors; the last use of every table before the run
+  // comes from a block max-scan.
   uint8_t* smo = selmtf_g + (size_t)b * kMaxSelectors;
   {
     const uint32_t per = ceil_div(nsel, (uint32_t)kT);
     const uint32_t g_lo = min(nsel, threadIdx.x * per), g_hi = min(nsel, g_lo + per);
     int32_t mine[kNGroups] = {-1, -1, -1, -1, -1, -1};  // last use inside my run (+1), 0 = none
-    for (uint32_t g = g_lo; g < g_hi; g++) mine[S.sel[g]] = (int32_t)g + 1;
-    int32_t last[kNGroups];
+    for (uint32_t g = g_lo; g < g_hi; g++) mine[sel[g]] = (int32_t)g + 1;
+    int32_t lastu[kNGroups];
 #pragma unroll
     for (int t = 0; t < kNGroups; t++) {
       const uint32_t m = mine[t] < 0 ? 0u : (uint32_t)mine[t];
-      const uint32_t incl = block_incl_max(m, S.sh);
+      const uint32_t incl = block_incl_max(m, sh);
       uint32_t ex = __shfl_up(incl, 1);
-      if (__lane_id() == 0) ex = threadIdx.x >= 64 ? S.sh[(threadIdx.x >> 6) - 1] : 0u;
+      if (__lane_id() == 0) ex = threadIdx.x >= 64 ? sh[(threadIdx.x >> 6) - 1] : 0u;
       __syncthreads();
-      last[t] = ex ? (int32_t)ex - 1 : -1 - t;
+      lastu[t] = ex ? (int32_t)ex - 1 : -1 - t;
     }
     uint32_t sbits = 0;
     for (uint32_t g = g_lo; g < g_hi; g++) {
-      const int s = S.sel[g];
-      const int32_t ls = last[s];
+      const int s = sel[g];
+      const int32_t ls = lastu[s];
       uint32_t j = 0;
 #pragma unroll
-      for (int t = 0; t < kNGroups; t++) j += last[t] > ls;
-      last[s] = (int32_t)g;
+      for (int t = 0; t < kNGroups; t++) j += lastu[t] > ls;
+      lastu[s] = (int32_t)g;
       smo[g] = (uint8_t)j;
       sbits += j + 1;
     }
     uint32_t tot;
-    block_incl_sum(sbits, S.sh, &tot);
-    if (threadIdx.x == 0) S.misc[0] = tot;
-  }
-  // code-length table bits (compress.c:694-706)
-  if (threadIdx.x < (unsigned)ng) {
-    const int t = threadIdx.x;
-    int cur = S.len[t][0];
-    uint32_t bits = 5;
-    for (int v = 0; v < alpha; v++) {
-      const int l = S.len[t][v];
-      bits += 1 + 2 * (uint32_t)(l > cur ? l - cur : cur - l);
-      cur = l;
-    }
-    S.misc[8 + t] = bits;
+    block_incl_sum(sbits, sh, &tot);
+    if (threadIdx.x == 0) misc[0] = tot;
   }
   __syncthreads();
-  uint8_t* lo = lens_g + (size_t)b * kNGroups * kMaxAlpha;
-  uint32_t* co = codes_g + (size_t)b * kNGroups * kMaxAlpha;
-  for (int i = threadIdx.x; i < ng * kMaxAlpha; i += kT) {
-    const int t = i / kMaxAlpha, v = i % kMaxAlpha;
-    lo[i] = v < alpha ? S.len[t][v] : 0;
-    co[i] = v < alpha ? S.code[t][v] : 0;
-  }
   if (threadIdx.x == 0) {
     uint32_t used16 = 0;
     for (int i = 0; i < 16; i++) {
@@ -298,18 +322,17 @@ __global__ void __launch_bounds__(kT) k_tables(const uint16_t* __restrict__ mtfv
       if (half) used16++;
     }
     uint32_t tbits = 0;
-    for (int t = 0; t < ng; t++) tbits += S.misc[8 + t];
-    const uint32_t total = 48 + 32 + 1 + 24 + 16 + 16 * used16 + 3 + 15 + S.misc[0] + tbits + data_bits;
+    for (int t = 0; t < ng; t++) tbits += misc[8 + t];
     uint32_t* info = info_g + (size_t)b * 8;
+    const uint32_t data_bits = info[6];
+    const uint32_t total = 48 + 32 + 1 + 24 + 16 + 16 * used16 + 3 + 15 + misc[0] + tbits + data_bits;
     info[0] = (uint32_t)ng;
     info[1] = nsel;
     info[2] = (uint32_t)alpha;
     info[3] = total;
-    info[4] = S.misc[0];
+    info[4] = misc[0];
     info[5] = tbits;
-    info[6] = data_bits;
   }
-  stamp(3);
 }
 
 // Bit offsets of every block, the combined CRC, the trailer position.
@@ -518,25 +541,21 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
   uint32_t* info = ws.u32("code_info", nbx * 8);
   uint64_t* bbits = ws.typed<uint64_t>("code_bbits", nbx + 2);
   uint32_t* comb = ws.u32("code_comb", 4);
-  static bool attr = false;
-  if (!attr) {
-    HIP_OK(hipFuncSetAttribute((const void*)k_tables, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(CodeLds)));
-    attr = true;
-  }
-  static const bool debug = getenv("BZG_DEBUG") != nullptr;
-  uint64_t* stamps = (uint64_t*)ws.u32("code_stamps", 16);
-  if (debug) HIP_OK(hipMemsetAsync(stamps, 0, 64, st));
+  uint32_t* rf = ws.u32("code_rf", nbx * kNGroups * kMaxAlpha);
   if (nb > 0) {
-    k_tables<<<nb, kT, sizeof(CodeLds), st>>>(m.mtfv, m.mtf_off, m.nmtf, m.freq, r.ninuse, r.inuse, lens, codes, sel,
-                                               selmtf, gbits, info, debug ? stamps : nullptr);
+    HIP_OK(hipMemsetAsync(info, 0, nbx * 8 * 4, st));
+    k_init_tables<<<nb, 64, 0, st>>>(m.nmtf, m.freq, r.ninuse, lens, rf);
     HIP_OK(hipGetLastError());
-    if (debug) {
-      uint64_t hs[4];
-      HIP_OK(hipMemcpyAsync(hs, stamps, 32, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      fprintf(stderr, "[bzg tables stamps] blocks=%u | cost+freq %lu  huffman %lu  codes+bits %lu  selmtf+out %lu\n", nb,
-              hs[0], hs[1], hs[2], hs[3]);
+    for (int it = 0; it < kIters; it++) {
+      k_cf<<<dim3(kCfSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, lens, sel, rf, gbits, info, 0);
+      HIP_OK(hipGetLastError());
+      k_huff<<<nb * kNGroups, 64, 0, st>>>(m.nmtf, r.ninuse, rf, lens);
+      HIP_OK(hipGetLastError());
     }
+    k_cf<<<dim3(kCfSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, lens, sel, rf, gbits, info, 1);
+    HIP_OK(hipGetLastError());
+    k_final<<<nb, kT, 0, st>>>(m.nmtf, r.ninuse, r.inuse, lens, codes, sel, selmtf, info);
+    HIP_OK(hipGetLastError());
   }
   const bool header = !carry.header_done;
   const uint64_t start_bit = carry.carry_bits + (header ? 32 : 0);
