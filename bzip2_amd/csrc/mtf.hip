@@ -145,37 +145,59 @@ __global__ void __launch_bounds__(64) k_compose(const uint32_t* __restrict__ bof
   }
 }
 
-// 3. per-chunk MTF from the chunk's initial list.  The thread's list lives in LDS as 64
-// words laid out [word][thread] so that lanes touching the same word index hit distinct
-// banks.  Byte k of word w is list position 4w+k.
+// 3. per-chunk MTF from the chunk's initial list, fused with the chunk's zero-run summary.
+// List positions 0..31 live in eight registers (byte k of word w = position 4w+k; SWAR
+// search and shift, no memory access); positions 32..255 live in LDS as 56 words laid out
+// [word][thread].  Ranks >= 32 are rare (< 0.1% on text), so the LDS part is touched by few
+// steps of a wave.
+constexpr int kRegW = 8;
 __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                                 const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
-                                                uint8_t* __restrict__ ranks) {
-  __shared__ uint32_t lst[64][kT];
+                                                uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
+                                                uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
+  __shared__ uint32_t lst[64 - kRegW][kT];
   const ChunkRef r = chunk_ref(boff, cbase);
   if (!r.valid) return;
   const uint32_t t = threadIdx.x;
   const uint32_t* src = init + (size_t)r.gidx * 64;
-  for (int w = 0; w < 64; w++) lst[w][t] = src[w];
+  uint32_t W[kRegW];
+#pragma unroll
+  for (int w = 0; w < kRegW; w++) W[w] = src[w];
+  for (int w = kRegW; w < 64; w++) lst[w - kRegW][t] = src[w];
   uint32_t racc = 0;  // 4 ranks packed, stored as one word when aligned
+  uint32_t ld = 0, z = 0, cnt = 0;
+  bool seen = false;
   for_bytes<true>(L, r.lo, r.hi, [&](uint32_t i, uint32_t c) {
     const uint32_t pat = c * 0x01010101u;
-    // find word and byte of c
-    uint32_t w = 0, x = 0;
-    for (; w < 64; w++) {  // every block byte is in the list; the bound only keeps a bad input finite
-      x = lst[w][t] ^ pat;
-      const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
-      if (z) {
-        x = z;
-        break;
+    uint32_t fw = kRegW, fz = 0;
+#pragma unroll
+    for (int w = kRegW - 1; w >= 0; w--) {
+      const uint32_t x = W[w] ^ pat;
+      const uint32_t zz = (x - 0x01010101u) & ~x & 0x80808080u;
+      if (zz) {
+        fw = (uint32_t)w;
+        fz = zz;
       }
     }
-    if (w == 64) {
-      w = 63;
-      x = 0x80000000u;
+    uint32_t pos;
+    if (fw < (uint32_t)kRegW) {
+      pos = fw * 4 + ((uint32_t)__builtin_ctz(fz) >> 3);
+    } else {  // beyond position 31: LDS words (every block byte is in the list)
+      uint32_t w = kRegW, x = 0;
+      for (; w < 64; w++) {
+        x = lst[w - kRegW][t] ^ pat;
+        const uint32_t zz = (x - 0x01010101u) & ~x & 0x80808080u;
+        if (zz) {
+          x = zz;
+          break;
+        }
+      }
+      if (w == 64) {  // only a corrupt input; keeps the loop finite
+        w = 63;
+        x = 0x80000000u;
+      }
+      pos = w * 4 + ((uint32_t)__builtin_ctz(x) >> 3);
     }
-    const uint32_t k = (uint32_t)__builtin_ctz(x) >> 3;  // byte within word
-    const uint32_t pos = w * 4 + k;
     racc |= pos << (8 * (i & 3));
     if ((i & 3) == 3 || i + 1 == r.hi) {
       if ((i & 3) == 3 && i >= r.lo + 3) {
@@ -185,40 +207,42 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
       }
       racc = 0;
     }
-    if (pos == 0) return;
-    // shift positions [0, pos) up by one and put c at 0
-    uint32_t carry = c;
-    for (uint32_t q = 0; q < w; q++) {
-      const uint32_t v = lst[q][t];
-      lst[q][t] = (v << 8) | carry;
-      carry = v >> 24;
-    }
-    const uint32_t v = lst[w][t];
-    const uint32_t lowmask = (k == 3) ? 0xffffffffu : ((1u << (8 * (k + 1))) - 1u);  // bytes 0..k
-    lst[w][t] = (v & ~lowmask) | (((v << 8) | carry) & lowmask);
-  });
-}
-
-// 4a. per-chunk zero-run summary
-__global__ void __launch_bounds__(kT) k_rle2_count(const uint8_t* __restrict__ ranks, const uint32_t* __restrict__ boff,
-                                                   const uint32_t* __restrict__ cbase, uint32_t* __restrict__ lead,
-                                                   uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
-  const ChunkRef r = chunk_ref(boff, cbase);
-  if (!r.valid) return;
-  uint32_t ld = 0, z = 0, cnt = 0;
-  bool seen = false;
-  for_bytes<true>(ranks, r.lo, r.hi, [&](uint32_t, uint32_t v) {
-    if (v == 0) {
+    // zero-run summary (RUNA/RUNB symbols of inner runs are counted here)
+    if (pos == 0) {
       z++;
+      return;
+    }
+    if (!seen) {
+      ld = z;
+      seen = true;
     } else {
-      if (!seen) {
-        ld = z;
-        seen = true;
-      } else {
-        cnt += nsym(z);
+      cnt += nsym(z);
+    }
+    z = 0;
+    cnt++;
+    // move c to the front: positions [0, pos) shift up by one byte
+    const uint32_t tw = pos >> 2, tb = pos & 3;
+    uint32_t carry = c;
+#pragma unroll
+    for (int w = 0; w < kRegW; w++) {
+      const uint32_t v = W[w];
+      if ((uint32_t)w < tw) {
+        W[w] = (v << 8) | carry;
+        carry = v >> 24;
+      } else if ((uint32_t)w == tw) {
+        const uint32_t lowmask = (tb == 3) ? 0xffffffffu : ((1u << (8 * (tb + 1))) - 1u);  // bytes 0..tb
+        W[w] = (v & ~lowmask) | (((v << 8) | carry) & lowmask);
       }
-      z = 0;
-      cnt++;
+    }
+    if (tw >= (uint32_t)kRegW) {
+      for (uint32_t w = kRegW; w < tw; w++) {
+        const uint32_t v = lst[w - kRegW][t];
+        lst[w - kRegW][t] = (v << 8) | carry;
+        carry = v >> 24;
+      }
+      const uint32_t v = lst[tw - kRegW][t];
+      const uint32_t lowmask = (tb == 3) ? 0xffffffffu : ((1u << (8 * (tb + 1))) - 1u);
+      lst[tw - kRegW][t] = (v & ~lowmask) | (((v << 8) | carry) & lowmask);
     }
   });
   lead[r.gidx] = seen ? ld : 0xffffffffu;  // all-zero chunk marker
@@ -257,20 +281,86 @@ __global__ void k_rle2_plan(const uint32_t* __restrict__ boff, const uint32_t* _
   (void)ninuse;
 }
 
-// 4c. emission + symbol frequencies
-__global__ void __launch_bounds__(kT) k_rle2_emit(const uint8_t* __restrict__ ranks, const uint32_t* __restrict__ boff,
-                                                  const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ ninuse,
-                                                  const uint32_t* __restrict__ zin, const uint32_t* __restrict__ coff,
-                                                  const uint32_t* __restrict__ finalrun, const uint32_t* __restrict__ mtf_off,
-                                                  uint16_t* __restrict__ mtfv, uint32_t* __restrict__ freq) {
+// 4c. emission + symbol frequencies: one wave per chunk, lane l owns ranks [16l, 16l+16).
+// The zero run that ends at a lane's first nonzero rank started in an earlier lane (or chunk:
+// zin) -- its length comes from a segmented scan over the lanes.  Each lane writes its
+// symbols contiguously at an offset from a wave scan of the per-lane symbol counts.
+constexpr int kEW = 16;  // chunks (waves) per workgroup: one frequency flush per 16 chunks
+__global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restrict__ ranks,
+                                                        const uint32_t* __restrict__ boff,
+                                                        const uint32_t* __restrict__ cbase,
+                                                        const uint32_t* __restrict__ ninuse,
+                                                        const uint32_t* __restrict__ zin,
+                                                        const uint32_t* __restrict__ coff,
+                                                        const uint32_t* __restrict__ finalrun,
+                                                        const uint32_t* __restrict__ mtf_off,
+                                                        uint16_t* __restrict__ mtfv, uint32_t* __restrict__ freq) {
   __shared__ uint32_t hist[kMaxAlpha];
-  for (int i = threadIdx.x; i < kMaxAlpha; i += kT) hist[i] = 0;
+  for (int i = threadIdx.x; i < kMaxAlpha; i += 64 * kEW) hist[i] = 0;
   __syncthreads();
-  const ChunkRef r = chunk_ref(boff, cbase);
-  if (r.valid) {
-    uint16_t* out = mtfv + mtf_off[r.b] + coff[r.gidx];
-    uint32_t z = 0, o = 0;
-    bool seen = false;
+  const uint32_t b = blockIdx.y, lane = __lane_id();
+  const uint32_t c = blockIdx.x * kEW + (threadIdx.x >> 6);
+  const uint32_t n = boff[b + 1] - boff[b];
+  if (c * kChunk < n) {
+    const uint32_t lo = boff[b] + c * kChunk, hi = min(boff[b + 1], lo + kChunk);
+    const uint32_t g = cbase[b] + c;
+    const uint32_t base = lo + lane * 16;
+    uint32_t rk[16];
+    uint32_t nzmask = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      rk[k] = base + k < hi ? ranks[base + k] : 0u;
+      if (base + k < hi && rk[k]) nzmask |= 1u << k;
+    }
+    const uint32_t cnt = base < hi ? min(16u, hi - base) : 0u;
+    const bool has = nzmask != 0;
+    const uint32_t lz = has ? (uint32_t)__builtin_ctz(nzmask) : cnt;
+    const uint32_t last_nz = has ? 31u - (uint32_t)__builtin_clz(nzmask) : 0u;
+    const uint32_t tz = has ? cnt - 1 - last_nz : cnt;
+    // zeros carried into each lane: a scan over the lanes that restarts at lanes with a
+    // nonzero rank (lane value: has ? trailing zeros : all its zeros)
+    uint32_t fl = has ? 1u : 0u, val = has ? tz : cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t pf = (uint32_t)__shfl_up((int)fl, o, 64);
+      const uint32_t pv = (uint32_t)__shfl_up((int)val, o, 64);
+      if (lane >= (uint32_t)o && !fl) {
+        val += pv;
+        fl = pf;
+      }
+    }
+    uint32_t cin = (uint32_t)__shfl_up((int)val, 1, 64);
+    uint32_t cfl = (uint32_t)__shfl_up((int)fl, 1, 64);
+    if (lane == 0) cin = cfl = 0;
+    // the run before the chunk's first nonzero rank is zin (it includes the chunk's leading
+    // zeros, k_rle2_plan); later runs end inside the chunk
+    const uint32_t run0 = cfl ? cin + lz : zin[g];
+    uint32_t ecount = 0;
+    if (has) {
+      ecount += nsym(run0);
+      uint32_t zz = 0;
+      bool first = true;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        if ((uint32_t)k < cnt) {
+          if (rk[k] == 0) {
+            zz++;
+          } else {
+            if (!first) ecount += nsym(zz);
+            first = false;
+            zz = 0;
+            ecount++;
+          }
+        }
+      }
+    }
+    const bool lastchunk = hi == boff[b + 1];
+    const uint32_t fr = finalrun[b];
+    const uint32_t tail = (lastchunk && lane == 63) ? nsym(fr) + 1 : 0u;  // final run + EOB
+    const uint32_t tot = ecount + tail;
+    const uint32_t excl = wave_incl_sum(tot) - tot;
+    uint16_t* out = mtfv + mtf_off[b] + coff[g] + excl;
+    uint32_t o = 0;
     auto put_run = [&](uint32_t zz) {
       while (zz > 0) {
         zz--;
@@ -280,29 +370,34 @@ __global__ void __launch_bounds__(kT) k_rle2_emit(const uint8_t* __restrict__ ra
         zz >>= 1;
       }
     };
-    const uint32_t z_in = zin[r.gidx];
-    for_bytes<true>(ranks, r.lo, r.hi, [&](uint32_t, uint32_t v) {
-      if (v == 0) {
-        z++;
-        return;
+    if (has) {
+      uint32_t zz = 0;
+      bool first = true;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        if ((uint32_t)k < cnt) {
+          if (rk[k] == 0) {
+            zz++;
+          } else {
+            put_run(first ? run0 : zz);
+            first = false;
+            zz = 0;
+            out[o++] = (uint16_t)(rk[k] + 1);
+            atomicAdd(&hist[rk[k] + 1], 1u);
+          }
+        }
       }
-      put_run(seen ? z : z_in);
-      seen = true;
-      z = 0;
-      out[o++] = (uint16_t)(v + 1);
-      atomicAdd(&hist[v + 1], 1u);
-    });
-    const uint32_t n = boff[r.b + 1] - boff[r.b];
-    if ((r.c + 1) * kChunk >= n) {  // last chunk: final run + EOB
-      put_run(finalrun[r.b]);
-      const uint32_t eob = ninuse[r.b] + 1;
+    }
+    if (tail) {
+      put_run(fr);
+      const uint32_t eob = ninuse[b] + 1;
       out[o++] = (uint16_t)eob;
       atomicAdd(&hist[eob], 1u);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kMaxAlpha; i += kT)
-    if (hist[i]) atomicAdd(&freq[(size_t)r.b * kMaxAlpha + i], hist[i]);
+  for (int i = threadIdx.x; i < kMaxAlpha; i += 64 * kEW)
+    if (hist[i]) atomicAdd(&freq[(size_t)b * kMaxAlpha + i], hist[i]);
 }
 
 }  // namespace
@@ -348,14 +443,13 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
   HIP_OK(hipGetLastError());
   k_compose<<<nb, 64, 0, st>>>(r.boff, cbase, r.inuse, sig, siglen, init);
   HIP_OK(hipGetLastError());
-  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, init, ranks);
-  HIP_OK(hipGetLastError());
-  k_rle2_count<<<g2, kT, 0, st>>>(ranks, r.boff, cbase, lead, trail, inner);
+  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, init, ranks, lead, trail, inner);
   HIP_OK(hipGetLastError());
   k_rle2_plan<<<ceil_div(nb, 64), 64, 0, st>>>(r.boff, cbase, nb, r.ninuse, lead, trail, inner, zin, coff, finalrun,
                                                 res.nmtf);
   HIP_OK(hipGetLastError());
-  k_rle2_emit<<<g2, kT, 0, st>>>(ranks, r.boff, cbase, r.ninuse, zin, coff, finalrun, moff, res.mtfv, res.freq);
+  k_rle2_emit<<<dim3(ceil_div(maxch, kEW), nb), 64 * kEW, 0, st>>>(ranks, r.boff, cbase, r.ninuse, zin, coff, finalrun,
+                                                                   moff, res.mtfv, res.freq);
   HIP_OK(hipGetLastError());
 }
 
