@@ -381,6 +381,11 @@ struct BitWriter {
 // nbits up to 32 may overflow the accumulator when nacc > 32 after a put; put() keeps
 // nacc < 32 on exit, so a put of <= 32 bits never loses bits.
 
+struct PackLds {
+  uint16_t chunk[kT * kGroupSize + 8];
+  uint32_t bits[(kT * kGroupSize * kMaxCodeLen + 31) / 32 + 2];  // one step's payload
+};
+
 __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, const uint32_t* __restrict__ mtf_off,
                                              const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ inuse,
                                              const uint32_t* __restrict__ bcrc, const uint32_t* __restrict__ origptr,
@@ -391,6 +396,7 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
   __shared__ uint8_t len[kNGroups][kMaxAlpha + 2];
   __shared__ uint32_t code[kNGroups][kMaxAlpha];
   __shared__ uint32_t sh[8];
+  __shared__ PackLds P;
   const uint32_t b = blockIdx.x;
   const uint32_t* info = info_g + (size_t)b * 8;
   const int ng = (int)info[0];
@@ -485,25 +491,58 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
     }
     w.flush();
   }
-  // payload
+  // payload: kT selector groups per step.  The step's symbols are staged in LDS, every lane
+  // encodes its group into an LDS bit buffer at its group's offset, and the buffer goes out as
+  // whole words (the two boundary words, shared with the neighbouring steps, by atomicOr).
   {
     const uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
     const uint16_t* gb = gbits_g + (size_t)b * kMaxSelectors;
-    const uint32_t per = ceil_div(nsel, kT);
-    const uint32_t lo = min(nsel, threadIdx.x * per), hi = min(nsel, lo + per);
-    uint32_t bits = 0;
-    for (uint32_t g = lo; g < hi; g++) bits += gb[g];
-    const uint32_t incl = block_incl_sum(bits, sh, (uint32_t*)nullptr);
-    BitWriter w(out, p_dat + incl - bits);
-    for (uint32_t g = lo; g < hi; g++) {
-      const int t = selo[g];
-      const uint32_t gs = g * kGroupSize, ge = min(gs + kGroupSize, nmtf);
-      for (uint32_t i = gs; i < ge; i++) {
-        const uint32_t v = mv[i];
-        w.put(len[t][v], code[t][v]);
+    uint64_t pos = p_dat;  // bit position of the step
+    for (uint32_t g0 = 0; g0 < nsel; g0 += kT) {
+      const uint32_t lo = g0 * kGroupSize, hi = min((g0 + kT) * kGroupSize, nmtf);
+      for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) P.chunk[i - lo] = mv[i];
+      const uint32_t g = g0 + threadIdx.x;
+      const uint32_t mybits = g < nsel ? gb[g] : 0u;
+      uint32_t stepbits;
+      const uint32_t gx = block_incl_sum(mybits, sh, &stepbits) - mybits;
+      const uint32_t w0 = (uint32_t)(pos & 31);          // bit offset of the step in its first word
+      const uint32_t nwords = (w0 + stepbits + 31) >> 5;  // words the step touches
+      for (uint32_t i = threadIdx.x; i < nwords; i += kT) P.bits[i] = 0;
+      __syncthreads();
+      if (g < nsel) {
+        const int t = selo[g];
+        const uint16_t* c = P.chunk + threadIdx.x * kGroupSize;
+        const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
+        uint32_t bp = w0 + gx;                    // bit position in P.bits
+        uint64_t acc = 0;                         // left-aligned pending bits
+        uint32_t na = bp & 31;                    // bits in acc, counted from the word start
+        uint32_t wi = bp >> 5;
+        for (uint32_t i = 0; i < n; i++) {
+          const uint32_t v = c[i];
+          const uint32_t l = len[t][v];
+          acc |= ((uint64_t)code[t][v] << (64 - l)) >> na;
+          na += l;
+          if (na >= 32) {
+            atomicOr(&P.bits[wi++], (uint32_t)(acc >> 32));
+            acc <<= 32;
+            na -= 32;
+          }
+        }
+        if (na) atomicOr(&P.bits[wi], (uint32_t)(acc >> 32));
       }
+      __syncthreads();
+      uint32_t* ow = out + (pos >> 5);
+      for (uint32_t i = threadIdx.x; i < nwords; i += kT) {
+        const uint32_t v = bswap32(P.bits[i]);
+        if (i == 0 || i + 1 == nwords) {
+          if (v) atomicOr(&ow[i], v);
+        } else {
+          ow[i] = v;
+        }
+      }
+      pos += stepbits;
+      __syncthreads();
     }
-    w.flush();
   }
 }
 
