@@ -71,19 +71,36 @@ __device__ __forceinline__ uint32_t cyc_pos(uint32_t v, uint32_t d, uint32_t len
   return q;
 }
 
-// Big-endian 4 bytes at p (any alignment; every text buffer has >= 16 bytes of padding).
-__device__ __forceinline__ uint32_t ld_be4(const uint8_t* p) {
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-  return __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u)));
+// 4 bytes at p, any alignment (one unaligned global_load_dword; every text buffer has >= 16
+// bytes of padding).
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
+  uint32_t x;
+  __builtin_memcpy(&x, p, 4);
+  return x;
+}
+__device__ __forceinline__ uint32_t ld_be4(const uint8_t* p) { return __builtin_bswap32(ld_u32(p)); }
+
+// The 4 characters of t[0..len) starting at q (< len) when they wrap past the unit end.
+__device__ __forceinline__ uint32_t text_key4_wrap(const uint8_t* t, uint32_t len, uint32_t q) {
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < 4; i++) k = (k << 8) | t[(q + i) % len];
+  return k;
+}
+// Same for len >= 4 (S1 units are longer than kBig): one subtraction per character.
+__device__ __forceinline__ uint32_t text_key4_wrap_long(const uint8_t* t, uint32_t len, uint32_t q) {
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++) {
+    const uint32_t p = q + i;
+    k = (k << 8) | t[p >= len ? p - len : p];
+  }
+  return k;
 }
 
 // The 4 characters of the cyclic unit text t[0..len) starting at q (< len).
 __device__ __forceinline__ uint32_t text_key4(const uint8_t* t, uint32_t len, uint32_t q) {
   if (q + 4 <= len) return ld_be4(t + q);
-  uint32_t k = 0;
-  for (uint32_t i = 0; i < 4; i++) k = (k << 8) | t[(q + i) % len];
-  return k;
+  return text_key4_wrap(t, len, q);
 }
 
 // The 16 characters starting at q, as four big-endian words.
@@ -138,22 +155,64 @@ __global__ void k_group_tiles(const Grp* __restrict__ L, uint32_t n, uint32_t* _
 }
 
 // ---------------------------------------------------------------- S1 byte passes
-// Every workgroup takes kDTile rotations of one group; loads are issued kPerT at a time.
+// Every member of a group carries a key cache (sk / sk2 beside sa / sa2): the next characters
+// of its rotation, most significant first, of which grp_cache(g) bytes are valid.  A pass
+// consumes the top byte; a group whose cache is empty gathers 4 characters from the text
+// (identity groups read them coalesced), so the text is read once per 4 passes.
+//   counting kernels (k_s1_hist, k_s1s_count) leave, for an empty cache, the gathered key in
+//   the source slot's cache (each member is owned by one workgroup), so that
+//   scatter kernels (k_s1_scatter, k_s1s_scatter) find a full cache in every non-identity slot.
+// Loads are issued through a selected address (cache slot or text) before any value is used,
+// so a wave keeps all kPerT gathers in flight; keys that wrap past the unit end are patched
+// afterwards (rare).
+
+// Loads members [lo, hi) of group gr: rotations vv and keys kk (top byte = this pass's
+// character).  Lanes past hi get a copy of member hi - 1.  kCounting: empty caches are
+// refilled from the text and stored back.
+template <bool kCounting>
 __device__ __forceinline__ void s1_load(const SortBufs& B, const Grp& gr, const Unit& U, uint32_t lo, uint32_t hi,
-                                        uint32_t (&vv)[kPerT], uint32_t (&dd)[kPerT]) {
-  const uint32_t* src = (gr.flags & kGrpAlt) ? B.sa2 : B.sa;
+                                        uint32_t (&vv)[kPerT], uint32_t (&kk)[kPerT]) {
+  const bool alt = gr.flags & kGrpAlt;
+  const uint32_t* src = alt ? B.sa2 : B.sa;
+  uint32_t* srck = alt ? B.sk2 : B.sk;
   const bool ident = gr.flags & kGrpIdent;
   const uint32_t depth = grp_depth(gr);
+  const bool fresh = ident || (kCounting && grp_cache(gr) == 0);
+  const uint8_t* ut = B.text + U.toff;
+  // (whole-loop uniform branches keep vv / kk in registers)
+  if (ident) {
 #pragma unroll
-  for (int i = 0; i < (int)kPerT; i++) {
-    const uint32_t e = lo + i * kT + threadIdx.x;
-    vv[i] = e < hi ? (ident ? e : src[gr.start + e]) : 0u;
-  }
+    for (int i = 0; i < (int)kPerT; i++) vv[i] = min(lo + i * kT + threadIdx.x, hi - 1);
+  } else {
 #pragma unroll
-  for (int i = 0; i < (int)kPerT; i++) {
-    const uint32_t e = lo + i * kT + threadIdx.x;
-    dd[i] = e < hi ? (uint32_t)B.text[U.toff + cyc_pos(vv[i], depth, U.len)] : 0u;
+    for (int i = 0; i < (int)kPerT; i++) vv[i] = src[gr.start + min(lo + i * kT + threadIdx.x, hi - 1)];
   }
+  if (!fresh) {
+#pragma unroll
+    for (int i = 0; i < (int)kPerT; i++) kk[i] = srck[gr.start + min(lo + i * kT + threadIdx.x, hi - 1)];
+  }
+  if (fresh) {
+#pragma unroll
+    for (int i = 0; i < (int)kPerT; i++) kk[i] = ld_u32(ut + cyc_pos(vv[i], depth, U.len));
+#pragma unroll
+    for (int i = 0; i < (int)kPerT; i++) {
+      const uint32_t q = cyc_pos(vv[i], depth, U.len);
+      kk[i] = q + 4 <= U.len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(ut, U.len, q);
+    }
+    if (kCounting && !ident) {
+#pragma unroll
+      for (int i = 0; i < (int)kPerT; i++) {
+        const uint32_t e = lo + i * kT + threadIdx.x;
+        if (e < hi) srck[gr.start + e] = kk[i];
+      }
+    }
+  }
+}
+
+// cache bytes valid in the buckets of a group after this pass
+__device__ __forceinline__ uint32_t s1_next_cache(const Grp& gr) {
+  const uint32_t c = (gr.flags & kGrpIdent) ? 0u : grp_cache(gr);
+  return c ? c - 1 : 3u;
 }
 
 __global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
@@ -165,12 +224,12 @@ __global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, uint3
   const Unit U = B.units[gr.unit];
   const uint32_t lo = (t - TP[g]) * kDTile, hi = min(gr.size, lo + kDTile);
   h[threadIdx.x] = 0;
-  uint32_t vv[kPerT], dd[kPerT];
-  s1_load(B, gr, U, lo, hi, vv, dd);
+  uint32_t vv[kPerT], kk[kPerT];
+  s1_load<true>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[dd[i]], 1u);
+    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[kk[i] >> 24], 1u);
   __syncthreads();
   hist[(size_t)t * 256 + threadIdx.x] = h[threadIdx.x];
 }
@@ -214,22 +273,26 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
   }
   if (cl == kClsDeep) {  // rare: a bucket still larger than kBig after kDBig characters
     const uint32_t dst_alt = (gr.flags & kGrpIdent) ? 0u : ((gr.flags & kGrpAlt) ^ 1u);
-    deep[atomicAdd(n_deep, 1u)] = Grp{base, total, gr.unit, dst_alt | (depth << 2)};
+    deep[atomicAdd(n_deep, 1u)] = Grp{base, total, gr.unit, grp_flags(dst_alt, depth, s1_next_cache(gr))};
   }
   __syncthreads();
   if (d < (uint32_t)kNCls) ccnt[(size_t)d * nTot + g] = cc[d];
 }
 
 // Scatter of one tile into the bucket order; the first tile of a group also emits the
-// group's buckets into the class lists (cscan: exclusive scan of ccnt).
+// group's buckets into the class lists (cscan: exclusive scan of ccnt).  The tile is first
+// reordered by bucket in LDS, so the global stores run along each bucket's range.
 __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
                                                    SortBufs B, SortOut O, const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ tot, const uint32_t* __restrict__ cscan,
                                                    uint32_t nTot, ClsLists C) {
   __shared__ uint32_t cnt[256];
-  __shared__ uint32_t base[256];
+  __shared__ uint32_t base[256];   // global slot of the bucket's first element - its LDS start
   __shared__ uint32_t single[256];
   __shared__ uint32_t wc[kT / 64][kNCls + 1];
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t Lv[kDTile], Lk[kDTile];
+  static_assert(kDTile == kPerT * kT, "one element per thread and round");
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const uint32_t g = upper_idx(TP, nG, t);
   const Grp gr = G[g];
@@ -237,27 +300,54 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, ui
   const uint32_t lo = (t - TP[g]) * kDTile, hi = min(gr.size, lo + kDTile);
   const bool dst_alt = !(gr.flags & kGrpIdent) && !(gr.flags & kGrpAlt);
   uint32_t* dst = dst_alt ? B.sa2 : B.sa;
+  uint32_t* dstk = dst_alt ? B.sk2 : B.sk;
   const uint32_t d = threadIdx.x;
   const uint32_t total = tot[(size_t)g * 256 + d];
+  const uint32_t gbase = off[(size_t)t * 256 + d];
   cnt[d] = 0;
-  base[d] = off[(size_t)t * 256 + d];
   single[d] = total == 1;
-  uint32_t vv[kPerT], dd[kPerT];
-  s1_load(B, gr, U, lo, hi, vv, dd);
+  uint32_t vv[kPerT], kk[kPerT];
+  s1_load<false>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
-  uint32_t pos[kPerT];
+  uint32_t rk[kPerT];
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    pos[i] = (lo + i * kT + threadIdx.x < hi) ? base[dd[i]] + atomicAdd(&cnt[dd[i]], 1u) : 0u;
+    if (lo + i * kT + threadIdx.x < hi) rk[i] = atomicAdd(&cnt[kk[i] >> 24], 1u);
+  __syncthreads();
+  {
+    const uint32_t c = cnt[d];
+    const uint32_t lstart = block_incl_sum(c, sh, (uint32_t*)nullptr) - c;
+    cnt[d] = lstart;
+    base[d] = gbase - lstart;
+  }
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++) {
     if (lo + i * kT + threadIdx.x < hi) {
-      dst[pos[i]] = vv[i];
-      // a bucket of one: this rotation is ordered (its primary-SA copy is made by
-      // k_s1_single, since other workgroups may still read the primary SA in this pass)
-      if (single[dd[i]]) emit_final(B, O, U, gr.unit, pos[i], vv[i], !dst_alt);
+      const uint32_t lp = cnt[kk[i] >> 24] + rk[i];
+      Lv[lp] = vv[i];
+      Lk[lp] = kk[i];
     }
   }
+  __syncthreads();
+  const uint32_t m = hi - lo;
+  uint32_t pos[kPerT];
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++) {
+    const uint32_t x = i * kT + threadIdx.x;
+    if (x < m) {
+      vv[i] = Lv[x];
+      kk[i] = Lk[x];
+      pos[i] = base[kk[i] >> 24] + x;
+      dst[pos[i]] = vv[i];
+      dstk[pos[i]] = kk[i] << 8;
+    }
+  }
+  // a bucket of one: this rotation is ordered (its primary-SA copy is made by k_s1_single,
+  // since other workgroups may still read the primary SA in this pass)
+#pragma unroll
+  for (int i = 0; i < (int)kPerT; i++)
+    if (i * kT + threadIdx.x < m && single[kk[i] >> 24]) emit_final(B, O, U, gr.unit, pos[i], vv[i], !dst_alt);
   if (t != TP[g]) return;
   // ---- bucket emission (digit order within the group)
   const uint32_t depth = grp_depth(gr) + 1;
@@ -274,7 +364,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, ui
   if (cl < (uint32_t)kNCls) {
     for (uint32_t x = 0; x < w; x++) rank += wc[x][cl];
     const uint32_t p = C.base[cl] + cscan[(size_t)cl * nTot + g] - cscan[(size_t)cl * nTot] + rank;
-    C.l[cl][p] = Grp{base[d], total, gr.unit, (dst_alt ? kGrpAlt : 0u) | (depth << 2)};
+    C.l[cl][p] = Grp{gbase, total, gr.unit, grp_flags(dst_alt ? kGrpAlt : 0u, depth, s1_next_cache(gr))};
   }
 }
 
@@ -293,8 +383,8 @@ __global__ void __launch_bounds__(kT) k_s1_single(const Grp* __restrict__ G, Sor
 // groups whose element prefix falls in a kSG window; <= kSGrp groups, < 2 kSG rotations).
 // A group lies in one tile, so its counts, bases and scatter stay in LDS, and singletons can
 // write the primary SA directly.  Two kernels per pass: counts of buckets per size class
-// (for the class-major scan), then the scatter and bucket emission; the second reads the
-// digits the first stored (dig, indexed by slot).
+// (for the class-major scan), then the scatter and bucket emission; both take the pass's
+// character from the key caches (the first refills empty caches of non-identity groups).
 constexpr uint32_t kSGrp = kSG / (kBig + 1) + 2;
 
 // tile index of item i = P[i] / kSG; mark the first item of each tile and one past its last.
@@ -312,11 +402,13 @@ __global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, uint32_t* _
   if (g < n) sizes[g] = L[g].size;
 }
 
+// packed kernels: 512 threads x 8 elements (a tile holds < 2 kSG rotations)
+constexpr uint32_t kTS = 512, kPerTS = 2 * kSG / kTS;
 struct S1sLds {
   uint32_t cnt[kSGrp * 256];   // bucket counts
   uint32_t cur[kSGrp * 256];   // bucket cursors (tile-relative)
   uint32_t gstart[kSGrp], goff[kSGrp + 1], gfl[kSGrp], gunit[kSGrp], gtoff[kSGrp], glen[kSGrp];
-  uint32_t sh[kT / 64];
+  uint32_t sh[kTS / 64];
   uint32_t cc[kNCls + 1];
 };
 
@@ -336,7 +428,7 @@ __device__ __forceinline__ uint32_t s1s_setup(S1sLds& S, const Grp* __restrict__
     S.gtoff[threadIdx.x] = U.toff;
     S.glen[threadIdx.x] = U.len;
   }
-  for (uint32_t i = threadIdx.x; i < ni * 256; i += kT) S.cnt[i] = 0;
+  for (uint32_t i = threadIdx.x; i < ni * 256; i += kTS) S.cnt[i] = 0;
   if (threadIdx.x <= (uint32_t)kNCls) S.cc[threadIdx.x] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -347,15 +439,66 @@ __device__ __forceinline__ uint32_t s1s_setup(S1sLds& S, const Grp* __restrict__
   return ni;
 }
 
-__device__ __forceinline__ uint32_t s1s_owner(const S1sLds& S, uint32_t ni, uint32_t e) {
-  uint32_t j = 0;
+// Group boundaries of the tile in registers (goff[q], or ~0 past the last group): the owner
+// of a tile element is then a few compares.
+struct S1sOwner {
+  uint32_t go[kSGrp - 1];
+  __device__ __forceinline__ S1sOwner(const S1sLds& S, uint32_t ni) {
 #pragma unroll
-  for (uint32_t q = 1; q < kSGrp; q++) j += (q < ni && e >= S.goff[q]);
-  return j;
+    for (uint32_t q = 1; q < kSGrp; q++) go[q - 1] = __builtin_amdgcn_readfirstlane(q < ni ? S.goff[q] : 0xffffffffu);
+  }
+  __device__ __forceinline__ uint32_t operator()(uint32_t e) const {
+    uint32_t j = 0;
+#pragma unroll
+    for (uint32_t q = 0; q + 1 < kSGrp; q++) j += e >= go[q];
+    return j;
+  }
+};
+
+// Packed path: rotations vv, keys kk and groups jj of the tile's elements (lanes past n get
+// element n - 1's).  kCounting: empty caches are refilled from the text and stored back.
+template <bool kCounting>
+__device__ __forceinline__ void s1s_load(const S1sLds& S, const SortBufs& B, uint32_t ni, uint32_t n,
+                                         uint32_t (&vv)[kPerTS], uint32_t (&kk)[kPerTS], uint32_t (&jj)[kPerTS]) {
+  const S1sOwner own(S, ni);
+  uint32_t sl[kPerTS];  // slot
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    const uint32_t e = min(i * kTS + threadIdx.x, n - 1);
+    const uint32_t j = own(e), o = e - S.goff[j], fl = S.gfl[j];
+    jj[i] = j;
+    sl[i] = S.gstart[j] + o;
+    vv[i] = (fl & kGrpIdent) ? o : ((fl & kGrpAlt) ? B.sa2 : B.sa)[sl[i]];
+  }
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    const uint32_t j = jj[i], fl = S.gfl[j];
+    const bool fresh = (fl & kGrpIdent) || (kCounting && grp_cache(Grp{0, 0, 0, fl}) == 0);
+    const uint8_t* p = fresh ? B.text + S.gtoff[j] + cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j])
+                             : reinterpret_cast<const uint8_t*>(((fl & kGrpAlt) ? B.sk2 : B.sk) + sl[i]);
+    kk[i] = ld_u32(p);
+  }
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    const uint32_t j = jj[i], fl = S.gfl[j];
+    const bool fresh = (fl & kGrpIdent) || (kCounting && grp_cache(Grp{0, 0, 0, fl}) == 0);
+    if (fresh) {
+      const uint32_t q = cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j]);
+      kk[i] = q + 4 <= S.glen[j] ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.gtoff[j], S.glen[j], q);
+    }
+  }
+  if (kCounting) {
+#pragma unroll
+    for (int i = 0; i < (int)kPerTS; i++) {
+      const uint32_t fl = S.gfl[jj[i]];
+      if (i * kTS + threadIdx.x < n && !(fl & kGrpIdent) && grp_cache(Grp{0, 0, 0, fl}) == 0)
+        ((fl & kGrpAlt) ? B.sk2 : B.sk)[sl[i]] = kk[i];
+    }
+  }
 }
 
-__global__ void __launch_bounds__(kT) k_s1s_count(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
-                                                  const uint32_t* __restrict__ last, SortBufs B, uint8_t* __restrict__ dig,
+__global__ void __launch_bounds__(kTS) k_s1s_count(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+                                                  const uint32_t* __restrict__ last, SortBufs B,
                                                   uint32_t* __restrict__ ccnt, uint32_t nTot, uint32_t ibase) {
   __shared__ S1sLds S;
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
@@ -365,29 +508,13 @@ __global__ void __launch_bounds__(kT) k_s1s_count(const Grp* __restrict__ SG, co
     return;
   }
   const uint32_t n = S.goff[ni];
-  uint32_t vv[kPerT], jj[kPerT];
+  uint32_t vv[kPerTS], jj[kPerTS], kk[kPerTS];
+  s1s_load<true>(S, B, ni, n, vv, kk, jj);
 #pragma unroll
-  for (int i = 0; i < (int)kPerT; i++) {
-    const uint32_t e = i * kT + threadIdx.x;
-    jj[i] = s1s_owner(S, ni, e);
-    vv[i] = 0;
-    if (e < n) {
-      const uint32_t j = jj[i], o = e - S.goff[j], fl = S.gfl[j];
-      vv[i] = (fl & kGrpIdent) ? o : ((fl & kGrpAlt) ? B.sa2 : B.sa)[S.gstart[j] + o];
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < (int)kPerT; i++) {
-    const uint32_t e = i * kT + threadIdx.x;
-    if (e < n) {
-      const uint32_t j = jj[i];
-      const uint32_t d = B.text[S.gtoff[j] + cyc_pos(vv[i], grp_depth(Grp{0, 0, 0, S.gfl[j]}), S.glen[j])];
-      dig[S.gstart[j] + e - S.goff[j]] = (uint8_t)d;
-      atomicAdd(&S.cnt[j * 256 + d], 1u);
-    }
-  }
+  for (int i = 0; i < (int)kPerTS; i++)
+    if (i * kTS + threadIdx.x < n) atomicAdd(&S.cnt[jj[i] * 256 + (kk[i] >> 24)], 1u);
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < ni * 256; b += kT) {
+  for (uint32_t b = threadIdx.x; b < ni * 256; b += kTS) {
     const uint32_t j = b >> 8;
     const uint32_t cl = bucket_cls(S.cnt[b], grp_depth(Grp{0, 0, 0, S.gfl[j]}) + 1);
     if (cl < (uint32_t)kNCls) atomicAdd(&S.cc[cl], 1u);
@@ -396,35 +523,25 @@ __global__ void __launch_bounds__(kT) k_s1s_count(const Grp* __restrict__ SG, co
   if (threadIdx.x < (uint32_t)kNCls) ccnt[(size_t)threadIdx.x * nTot + ibase + t] = S.cc[threadIdx.x];
 }
 
-__global__ void __launch_bounds__(kT) k_s1s_scatter(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+__global__ void __launch_bounds__(kTS) k_s1s_scatter(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
                                                     const uint32_t* __restrict__ last, SortBufs B, SortOut O,
-                                                    const uint8_t* __restrict__ dig, const uint32_t* __restrict__ cscan,
+                                                    const uint32_t* __restrict__ cscan,
                                                     uint32_t nTot, uint32_t ibase, ClsLists C) {
   __shared__ S1sLds S;
+  __shared__ uint32_t Lv[2 * kSG], Lk[2 * kSG];  // the tile in bucket order
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const uint32_t ni = s1s_setup(S, SG, first, last, t, B);
   if (ni == 0) return;
   const uint32_t n = S.goff[ni];
-  uint32_t vv[kPerT], pk[kPerT];  // pk: group | digit << 8
+  uint32_t vv[kPerTS], kk[kPerTS], jj[kPerTS];
+  s1s_load<false>(S, B, ni, n, vv, kk, jj);
 #pragma unroll
-  for (int i = 0; i < (int)kPerT; i++) {
-    const uint32_t e = i * kT + threadIdx.x;
-    const uint32_t j = s1s_owner(S, ni, e);
-    vv[i] = 0;
-    pk[i] = j;
-    if (e < n) {
-      const uint32_t o = e - S.goff[j], fl = S.gfl[j];
-      vv[i] = (fl & kGrpIdent) ? o : ((fl & kGrpAlt) ? B.sa2 : B.sa)[S.gstart[j] + o];
-      pk[i] |= (uint32_t)dig[S.gstart[j] + o] << 8;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < (int)kPerT; i++)
-    if (i * kT + threadIdx.x < n) atomicAdd(&S.cnt[(pk[i] & 255u) * 256 + (pk[i] >> 8)], 1u);
+  for (int i = 0; i < (int)kPerTS; i++)
+    if (i * kTS + threadIdx.x < n) jj[i] = atomicAdd(&S.cnt[jj[i] * 256 + (kk[i] >> 24)], 1u) | (jj[i] << 16);
   __syncthreads();
   // tile-relative bucket bases: exclusive scan over the (group, digit) bins
   {
-    constexpr uint32_t kB = kSGrp * 256 / kT;
+    constexpr uint32_t kB = (kSGrp * 256 + kTS - 1) / kTS;
     uint32_t c[kB], sum = 0;
 #pragma unroll
     for (int q = 0; q < (int)kB; q++) {
@@ -442,14 +559,15 @@ __global__ void __launch_bounds__(kT) k_s1s_scatter(const Grp* __restrict__ SG, 
   }
   __syncthreads();
   // bucket emission (before the cursors move)
-  for (uint32_t b = threadIdx.x; b < ni * 256; b += kT) {
+  for (uint32_t b = threadIdx.x; b < ni * 256; b += kTS) {
     const uint32_t j = b >> 8, total = S.cnt[b];
     const uint32_t fl = S.gfl[j];
     const uint32_t depth = grp_depth(Grp{0, 0, 0, fl}) + 1;
     const uint32_t cl = bucket_cls(total, depth);
     if (cl == 0xffu) continue;
     const uint32_t dst_alt = (fl & kGrpIdent) ? 0u : ((fl & kGrpAlt) ^ 1u);
-    const Grp nb{S.gstart[j] + S.cur[b] - S.goff[j], total, S.gunit[j], dst_alt | (depth << 2)};
+    const Grp gf{0, 0, 0, fl};
+    const Grp nb{S.gstart[j] + S.cur[b] - S.goff[j], total, S.gunit[j], grp_flags(dst_alt, depth, s1_next_cache(gf))};
     if (cl == kClsDeep) {
       O.deep[atomicAdd(O.n_deep, 1u)] = nb;
     } else {
@@ -457,19 +575,38 @@ __global__ void __launch_bounds__(kT) k_s1s_scatter(const Grp* __restrict__ SG, 
       C.l[cl][C.base[cl] + cscan[(size_t)cl * nTot + ibase + t] - cscan[(size_t)cl * nTot] + r] = nb;
     }
   }
-  __syncthreads();
+  // reorder the tile by bucket in LDS (jj = rank in bin | group << 16), then store along
+  // each group's slots
 #pragma unroll
-  for (int i = 0; i < (int)kPerT; i++) {
-    if (i * kT + threadIdx.x < n) {
-      const uint32_t j = pk[i] & 255u, d = pk[i] >> 8;
-      const uint32_t fl = S.gfl[j];
-      const uint32_t slot = S.gstart[j] + atomicAdd(&S.cur[j * 256 + d], 1u) - S.goff[j];
+  for (int i = 0; i < (int)kPerTS; i++) {
+    if (i * kTS + threadIdx.x < n) {
+      const uint32_t lp = S.cur[(jj[i] >> 16) * 256 + (kk[i] >> 24)] + (jj[i] & 0xffffu);
+      Lv[lp] = vv[i];
+      Lk[lp] = kk[i];
+    }
+  }
+  __syncthreads();
+  const S1sOwner own(S, ni);
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    const uint32_t x = i * kTS + threadIdx.x;
+    if (x < n) {
+      const uint32_t j = own(x), fl = S.gfl[j];
+      vv[i] = Lv[x];
+      kk[i] = Lk[x];
+      jj[i] = S.gstart[j] + x - S.goff[j];  // slot
       const bool dst_alt = !(fl & kGrpIdent) && !(fl & kGrpAlt);
-      (dst_alt ? B.sa2 : B.sa)[slot] = vv[i];
-      if (S.cnt[j * 256 + d] == 1) {
-        // a bucket of one: ordered (the group lies in this tile, so the primary SA is free)
-        emit_final(B, O, B.units[S.gunit[j]], S.gunit[j], slot, vv[i], true);
-      }
+      (dst_alt ? B.sa2 : B.sa)[jj[i]] = vv[i];
+      (dst_alt ? B.sk2 : B.sk)[jj[i]] = kk[i] << 8;
+    }
+  }
+  // a bucket of one: ordered (the group lies in this tile, so the primary SA is free)
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    const uint32_t x = i * kTS + threadIdx.x;
+    if (x < n) {
+      const uint32_t j = own(x);
+      if (S.cnt[j * 256 + (kk[i] >> 24)] == 1) emit_final(B, O, B.units[S.gunit[j]], S.gunit[j], jj[i], vv[i], true);
     }
   }
 }
@@ -540,7 +677,7 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
         const uint64_t mates = match_byte(cls, live);
         const uint32_t r = (uint32_t)__popcll(mates & lanemask_lt());
         B.sa[s0 + pos + r] = v;
-        if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, (uint32_t)__popcll(mates), unit, d << 2};
+        if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, (uint32_t)__popcll(mates), unit, d << kGrpDepthShift};
       }
       break;
     }
@@ -723,7 +860,7 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
               rank += q < p;
             }
           B.sa[g.start + pos[r] + rank] = v[r];
-          if (rank == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + pos[r], cnt, g.unit, depth << 2};
+          if (rank == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + pos[r], cnt, g.unit, depth << kGrpDepthShift};
         }
       break;
     }
@@ -975,6 +1112,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   SortBufs B{};
   B.sa = ws.u32("sort_sa", S + 16);
   B.sa2 = ws.u32("sort_sa2", S + 16);
+  B.sk = ws.u32("sort_sk", S + 16);
+  B.sk2 = ws.u32("sort_sk2", S + 16);
   B.text = r.blk;
   B.units = units;
   // class lists: a class-c bucket holds more than kClsMax[c-1] rotations
@@ -1005,7 +1144,6 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* P = ws.u32("sort_P", ccap[6] + 16);
   uint32_t* first = ws.u32("sort_first", max_ptiles);
   uint32_t* last = ws.u32("sort_last", max_ptiles);
-  uint8_t* dig = ws.u8("sort_dig", S + 16);
   uint32_t* scratch =
       ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[6])) + 64);
   uint32_t hc[24];
@@ -1053,7 +1191,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipMemsetAsync(first, 0xff, (size_t)nT * 4, st));
       k_tile_first<<<grid(n6), kT, 0, st>>>(P, n6, first, last);
       HIP_OK(hipGetLastError());
-      k_s1s_count<<<nT, kT, 0, st>>>(cur6, first, last, B, dig, ccnt, nTot, n7);
+      k_s1s_count<<<nT, kTS, 0, st>>>(cur6, first, last, B, ccnt, nTot, n7);
       HIP_OK(hipGetLastError());
     }
     if (n7) {
@@ -1077,7 +1215,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     if (nT) {
-      k_s1s_scatter<<<nT, kT, 0, st>>>(cur6, first, last, B, O, dig, ccnt, nTot, n7, Cp);
+      k_s1s_scatter<<<nT, kTS, 0, st>>>(cur6, first, last, B, O, ccnt, nTot, n7, Cp);
       HIP_OK(hipGetLastError());
     }
     read_counters();

@@ -12,16 +12,23 @@ struct Unit {
 };
 
 // A group of slots whose rotations are known equal to some depth.
-// flags: bit0 = data lives in the alternate buffer (sa2), bit1 = identity (slot e holds
-// rotation e; nothing stored yet), bits 2.. = depth (characters known equal).
+// flags: bit0 = data lives in the alternate buffers (sa2/sk2), bit1 = identity (slot e holds
+// rotation e; nothing stored yet), bits 2-4 = valid bytes of the members' key caches (S1),
+// bits 5.. = depth (characters known equal).
 struct Grp {
   uint32_t start, size, unit, flags;
 };
 constexpr uint32_t kGrpAlt = 1u, kGrpIdent = 2u;
-__host__ __device__ inline uint32_t grp_depth(const Grp& g) { return g.flags >> 2; }
+constexpr uint32_t kGrpDepthShift = 5;
+__host__ __device__ inline uint32_t grp_depth(const Grp& g) { return g.flags >> kGrpDepthShift; }
+__host__ __device__ inline uint32_t grp_cache(const Grp& g) { return (g.flags >> 2) & 7u; }
+__host__ __device__ inline uint32_t grp_flags(uint32_t alt, uint32_t depth, uint32_t cache) {
+  return alt | (cache << 2) | (depth << kGrpDepthShift);
+}
 
 struct SortBufs {
   uint32_t *sa, *isa, *key, *sa2, *key2;
+  uint32_t *sk, *sk2;  // S1 key caches beside sa / sa2: the next characters, most significant first
   const uint8_t* text;
   const Unit* units;
 };
