@@ -19,7 +19,8 @@ except Exception:  # pragma: no cover - torch is optional for the C ABI
     _torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbz2_amd.so")
+# BZ2_AMD_LIB: an alternative in-tree build of the same library (development A/B runs)
+LIB_PATH = os.environ.get("BZ2_AMD_LIB") or os.path.join(HERE, "libbz2_amd.so")
 
 # bzlib.h return codes (reference bzlib.h:33-46)
 BZ_RUN, BZ_FLUSH, BZ_FINISH = 0, 1, 2

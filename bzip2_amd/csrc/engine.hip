@@ -355,7 +355,7 @@ int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, u
     const uint32_t total = offsets[nb];
     Rle1Result r;
     r.nblocks = nb;
-    r.blk = e.ws.u8("blk", total + 16);
+    r.blk = e.ws.u8("blk", total + 64);
     r.boff = e.ws.u32("boff", nb + 2);
     HIP_OK(hipMemcpy(r.blk, blocks, total, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice));
@@ -389,7 +389,7 @@ int bzg_stage_mtf(const uint8_t* bwt_in, const uint32_t* offsets, uint32_t nb, u
     const uint32_t total = offsets[nb];
     Rle1Result r;
     r.nblocks = nb;
-    r.blk = e.ws.u8("blk", total + 16);
+    r.blk = e.ws.u8("blk", total + 64);
     r.boff = e.ws.u32("boff", nb + 2);
     HIP_OK(hipMemcpy(r.blk, bwt_in, total, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice));

@@ -719,29 +719,32 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
 // ---- buckets of 9..256 rotations: one segment of kSeg lanes x kPer registers per bucket
 // (64 / kSeg buckets per wave).  Element (lane, r) sits at position p = (lane % kSeg) * kPer
 // + r of its segment.  Sort key: (run start, 8 characters, element index); pads sort last.
-// Round 1 sorts by the first 8 characters after the bucket's depth; every later round
-// re-keys only the runs still tied, 8 characters deeper, and re-sorts (positions of unique
+// Round 1 sorts by the first 7 characters after the bucket's depth; every later round
+// re-keys only the runs still tied, 6 characters deeper, and re-sorts (positions of unique
 // elements never move since their run start is their own position).
-// The 96-bit key (run start:16, hi:32, lo:32, element index:16) in three words, so that
-// the order is the lexicographic order of (d0:d1 as 64 bits, d2).  Pads: run start 0xffff.
-struct BsortKey {
-  uint32_t d0, d1, d2;
-};
+// One 64-bit key, so a compare-exchange is one compare and two selects:
+//   round 1:  7 characters : 56 | element index : 8
+//   later:    run start : 8 | 6 characters : 48 | element index : 8
+// Pads are all ones.  No valid key is: the RLE1 output never holds 8 (cyclically) consecutive
+// 0xff bytes, so 7 characters of 0xff carry an index below 0xff in a segment with pads (a
+// padded segment has fewer than 256 elements); later rounds give valid run starts < 0xff
+// there as well, and a run start 0xff would be a singleton, whose key is (position, 0).
+using BsortKey = uint64_t;
+constexpr BsortKey kPadKey = ~0ull;
 
-__device__ __forceinline__ BsortKey make_key(uint32_t rs, uint32_t hi, uint32_t lo, uint32_t idx) {
-  return BsortKey{(rs << 16) | (hi >> 16), (hi << 16) | (lo >> 16), (lo << 16) | idx};
+__device__ __forceinline__ BsortKey make_key1(uint32_t hi, uint32_t lo, uint32_t idx) {
+  return ((((uint64_t)hi << 32) | lo) & ~0xffull) | idx;
 }
-__device__ __forceinline__ uint32_t key_rs(const BsortKey& k) { return k.d0 >> 16; }
-__device__ __forceinline__ uint32_t key_idx(const BsortKey& k) { return k.d2 & 0xffffu; }
+__device__ __forceinline__ BsortKey make_key2(uint32_t rs, uint32_t hi, uint32_t lo, uint32_t idx) {
+  return ((uint64_t)rs << 56) | (((((uint64_t)hi << 32) | lo) >> 16) << 8) | idx;
+}
+__device__ __forceinline__ bool key_valid(BsortKey k) { return k != kPadKey; }
+__device__ __forceinline__ uint32_t key_idx(BsortKey k) { return (uint32_t)k & 0xffu; }
 // same run start and characters (index ignored)
-__device__ __forceinline__ bool key_tied(const BsortKey& a, const BsortKey& b) {
-  return a.d0 == b.d0 && a.d1 == b.d1 && (a.d2 >> 16) == (b.d2 >> 16);
-}
+__device__ __forceinline__ bool key_tied(BsortKey a, BsortKey b) { return (a >> 8) == (b >> 8); }
+__device__ __forceinline__ bool key_less(BsortKey a, BsortKey b) { return a < b; }
 
-__device__ __forceinline__ bool key_less(const BsortKey& a, const BsortKey& b) {
-  const uint64_t a1 = ((uint64_t)a.d0 << 32) | a.d1, b1 = ((uint64_t)b.d0 << 32) | b.d1;
-  return (a1 < b1) | ((a1 == b1) & (a.d2 < b.d2));
-}
+
 
 // x from lane ^ J (J < 64): DPP within quads, ds_swizzle within 32 lanes, bpermute across.
 template <int J>
@@ -757,11 +760,8 @@ __device__ __forceinline__ void bitonic_xlane(BsortKey (&K)[kPer], int k, uint32
   constexpr int jl = J / kPer;
   BsortKey o[kPer];
 #pragma unroll
-  for (int r = 0; r < kPer; r++) {
-    o[r].d0 = xor_lane<jl>(K[r].d0);
-    o[r].d1 = xor_lane<jl>(K[r].d1);
-    o[r].d2 = xor_lane<jl>(K[r].d2);
-  }
+  for (int r = 0; r < kPer; r++)
+    o[r] = ((uint64_t)xor_lane<jl>((uint32_t)(K[r] >> 32)) << 32) | xor_lane<jl>((uint32_t)K[r]);
 #pragma unroll
   for (int r = 0; r < kPer; r++) {
     const uint32_t p = sl * kPer + r;
@@ -803,6 +803,7 @@ __device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
   for (int k = 2; k <= kN; k <<= 1) bitonic_j<kSeg, kPer, kN / 2>(K, k, sl);
 }
 
+
 // Runs still tied after kBsRounds bitonic rounds (few rotations, often long repeats) are
 // finished in place: every tied rotation ranks itself among the members of its run that are
 // still tied with it (same class, named by the lowest position of the class) on the next 16
@@ -820,7 +821,7 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
   uint32_t v[kPer], pos[kPer], cls[kPer], rlen[kPer];
 #pragma unroll
   for (int r = 0; r < kPer; r++) {
-    live[r] = !done[r] && key_rs(K[r]) != 0xffffu;
+    live[r] = !done[r] && key_valid(K[r]);
     v[r] = live[r] ? Lv[key_idx(K[r])] : 0u;
     pos[r] = rsn[r];
     cls[r] = rsn[r];
@@ -896,6 +897,7 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
   }
 }
 
+
 template <int kSeg, int kPer>
 __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_t nL, SortBufs B, SortOut O) {
   constexpr int kBPW = 64 / kSeg;
@@ -937,7 +939,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     }
     Lv[w][idx] = vq[r];
     Lc[w][idx] = c;
-    K[r] = make_key(valid ? 0u : 0xffffu, hi, lo, idx);
+    K[r] = valid ? make_key1(hi, lo, idx) : kPadKey;
   }
   bool done[kPer];
 #pragma unroll
@@ -953,12 +955,11 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
       if (r > 0) {
         q = K[r - 1];
       } else {
-        q.d0 = (uint32_t)__shfl_up((int)K[kPer - 1].d0, 1, 64);
-        q.d1 = (uint32_t)__shfl_up((int)K[kPer - 1].d1, 1, 64);
-        q.d2 = (uint32_t)__shfl_up((int)K[kPer - 1].d2, 1, 64);
-        if (sl == 0) q.d0 = 0xfffe0000u;  // no previous element
+        q = ((uint64_t)(uint32_t)__shfl_up((int)(K[kPer - 1] >> 32), 1, 64) << 32) |
+            (uint32_t)__shfl_up((int)(uint32_t)K[kPer - 1], 1, 64);
+        if (sl == 0) q = ~K[r];  // no previous element
       }
-      tp[r] = key_rs(K[r]) != 0xffffu && key_tied(q, K[r]);
+      tp[r] = key_valid(K[r]) && key_tied(q, K[r]);
     }
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
@@ -992,7 +993,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     for (int r = 0; r < kPer; r++) {
       rsn[r] = max(rsn[r], pre);
       const uint32_t idx = key_idx(K[r]);
-      const bool valid = key_rs(K[r]) != 0xffffu;
+      const bool valid = key_valid(K[r]);
       const bool tied = valid && (tp[r] || tn[r]);
       const uint32_t p = sl * kPer + r;
       if (valid && !tied && !done[r]) {
@@ -1008,7 +1009,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
       any_tied |= tied;
     }
     if (__ballot(any_tied) == 0) break;
-    depth += 8;  // tied runs are equal to this depth
+    depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
     if (++round >= kBsRounds || depth >= kDWave) {
       bsort_tail<kSeg, kPer>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       break;
@@ -1017,15 +1018,14 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
       const uint32_t idx = key_idx(K[r]);
-      const bool valid = key_rs(K[r]) != 0xffffu;
-      if (!valid) continue;
+      if (!key_valid(K[r])) continue;
       const uint32_t p = sl * kPer + r;
       if (done[r]) {
-        K[r] = make_key(p, 0, 0, idx);
+        K[r] = make_key2(p, 0, 0, idx);
       } else {
         uint32_t hi, lo;
         text_key8(t, U.len, cyc_pos(Lv[w][idx], depth, U.len), hi, lo);
-        K[r] = make_key(rsn[r], hi, lo, idx);
+        K[r] = make_key2(rsn[r], hi, lo, idx);
       }
     }
   }

@@ -11,6 +11,6 @@ for r in csv.DictReader(open(sys.argv[1])):
     if "bsort" in n:
         n = f"{n}<{r['Grid_Size_X']}>"
     agg[n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 / steps
-for k, v in sorted(agg.items(), key=lambda x: -x[1])[:18]:
+for k, v in sorted(agg.items(), key=lambda x: -x[1])[:int(sys.argv[3]) if len(sys.argv) > 3 else 18]:
     print(f"{k:40s} {v:8.2f}")
 print("total", round(sum(agg.values()), 2))

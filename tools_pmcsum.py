@@ -14,7 +14,10 @@ def short(name):
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        agg[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        k = short(r["Kernel_Name"])
+        if k == "k_bsort":
+            k += "<%s>" % r["Grid_Size"]
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
 names = sorted({c for k in agg.values() for c in k})
 print(f'{"kernel":22s} ' + " ".join(f"{n[3:17]:>14s}" for n in names))
 for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1].values()))[:24]:
