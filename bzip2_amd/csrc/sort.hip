@@ -103,6 +103,32 @@ __device__ __forceinline__ uint32_t text_key4(const uint8_t* t, uint32_t len, ui
   return text_key4_wrap(t, len, q);
 }
 
+// Characters q .. q + 4N - 1 of the cyclic unit text as big-endian words, one at a time
+// (the wrap-around path; rare).
+template <int N>
+__device__ __forceinline__ void text_words_wrap(const uint8_t* t, uint32_t len, uint32_t q, uint32_t (&k)[N]) {
+  for (int w = 0; w < N; w++) {
+    uint32_t x = 0;
+    for (uint32_t i = 0; i < 4; i++) x = (x << 8) | t[(q + 4 * w + i) % len];
+    k[w] = x;
+  }
+}
+// The N + 1 aligned words covering characters p .. p + 4N - 1 (loads only; text_words_of
+// turns them into big-endian words).  Split so that a caller issues the loads of all its
+// elements before it uses any.
+template <int N>
+__device__ __forceinline__ void text_raw(const uint8_t* p, uint32_t (&x)[N + 1]) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+#pragma unroll
+  for (int i = 0; i <= N; i++) x[i] = w[i];
+}
+template <int N>
+__device__ __forceinline__ void text_words_of(const uint8_t* p, const uint32_t (&x)[N + 1], uint32_t (&k)[N]) {
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+#pragma unroll
+  for (int i = 0; i < N; i++) k[i] = __builtin_bswap32(__builtin_amdgcn_alignbyte(x[i + 1], x[i], sh));
+}
+
 // The 16 characters starting at q, as four big-endian words.
 __device__ __forceinline__ void text_key16(const uint8_t* t, uint32_t len, uint32_t q, uint32_t (&k)[4]) {
   if (q + 16 <= len) {
@@ -804,13 +830,13 @@ __device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
 }
 
 
-// Runs still tied after kBsRounds bitonic rounds (few rotations, often long repeats) are
+// Runs still tied after kRounds bitonic rounds (few rotations, often long repeats) are
 // finished in place: every tied rotation ranks itself among the members of its run that are
 // still tied with it (same class, named by the lowest position of the class) on the next 16
 // characters per step; positions do not move any more, the final slot is run start + rank.
-constexpr int kBsRounds = 2;
 
-template <int kSeg, int kPer>
+
+template <int kSeg, int kPer, bool kBatch>
 __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, const Unit& U, uint32_t depth,
                            const BsortKey (&K)[kPer], const bool (&done)[kPer], const uint32_t (&rsn)[kPer],
                            const uint32_t* Lv, uint32_t* Lk, uint4* TK, uint32_t* TC) {
@@ -840,13 +866,31 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
     for (int r = 0; r < kPer; r++) any |= live[r];
     if (__ballot(any) == 0) break;
     const bool deep = depth >= kDWave;
+    if constexpr (kBatch) {
+      uint32_t raw[kPer][5], qq[kPer];
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
-      const uint32_t wp = sb + sl * kPer + r;
-      uint32_t k[4] = {0u, 0u, 0u, 0u};
-      if (live[r] && !deep) text_key16(t, U.len, cyc_pos(v[r], depth, U.len), k);
-      TK[wp] = make_uint4(k[0], k[1], k[2], k[3]);
-      TC[wp] = live[r] ? cls[r] : 0xffffffffu;
+      for (int r = 0; r < kPer; r++) {
+        qq[r] = live[r] ? cyc_pos(v[r], depth, U.len) : 0u;
+        text_raw<4>(t + qq[r], raw[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < kPer; r++) {
+        const uint32_t wp = sb + sl * kPer + r;
+        uint32_t k[4];
+        text_words_of<4>(t + qq[r], raw[r], k);
+        if (live[r] && qq[r] + 16 > U.len) text_words_wrap<4>(t, U.len, qq[r], k);
+        TK[wp] = make_uint4(k[0], k[1], k[2], k[3]);
+        TC[wp] = live[r] ? cls[r] : 0xffffffffu;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kPer; r++) {
+        const uint32_t wp = sb + sl * kPer + r;
+        uint32_t k[4] = {0u, 0u, 0u, 0u};
+        if (live[r] && !deep) text_key16(t, U.len, cyc_pos(v[r], depth, U.len), k);
+        TK[wp] = make_uint4(k[0], k[1], k[2], k[3]);
+        TC[wp] = live[r] ? cls[r] : 0xffffffffu;
+      }
     }
     wave_sync();
     if (deep) {  // still tied after kDWave characters: leave to the doubling fallback
@@ -898,7 +942,7 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
 }
 
 
-template <int kSeg, int kPer>
+template <int kSeg, int kPer, int kRounds, bool kBatch>
 __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_t nL, SortBufs B, SortOut O) {
   constexpr int kBPW = 64 / kSeg;
   constexpr int kE = 64 * kPer;  // elements per wave
@@ -927,19 +971,43 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     const uint32_t p = sl * kPer + r;
     vq[r] = p < m ? ((g.flags & kGrpIdent) ? p : src[g.start + p]) : 0u;
   }
+  if constexpr (kBatch) {
+    // all loads issued before any is used (3 aligned words and the BWT byte per rotation);
+    // keys that wrap past the unit end are rebuilt afterwards
+    uint32_t raw[kPer][3], cq[kPer];
 #pragma unroll
-  for (int r = 0; r < kPer; r++) {
-    const uint32_t p = sl * kPer + r, idx = lane * kPer + r;
-    const bool valid = p < m;
-    uint32_t hi = 0xffffffffu, lo = 0xffffffffu;
-    uint8_t c = 0;
-    if (valid) {
-      text_key8(t, U.len, cyc_pos(vq[r], depth, U.len), hi, lo);
-      c = t[vq[r] == 0 ? U.len - 1 : vq[r] - 1];
+    for (int r = 0; r < kPer; r++) {
+      cq[r] = cyc_pos(vq[r], depth, U.len);
+      text_raw<2>(t + cq[r], raw[r]);
+      cq[r] |= (uint32_t)t[vq[r] == 0 ? U.len - 1 : vq[r] - 1] << 24;
     }
-    Lv[w][idx] = vq[r];
-    Lc[w][idx] = c;
-    K[r] = valid ? make_key1(hi, lo, idx) : kPadKey;
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const uint32_t p = sl * kPer + r, idx = lane * kPer + r;
+      const bool valid = p < m;
+      const uint32_t q = cq[r] & 0xffffffu;
+      uint32_t k2[2];
+      text_words_of<2>(t + q, raw[r], k2);
+      if (valid && q + 8 > U.len) text_words_wrap<2>(t, U.len, q, k2);
+      Lv[w][idx] = vq[r];
+      Lc[w][idx] = (uint8_t)(cq[r] >> 24);
+      K[r] = valid ? make_key1(k2[0], k2[1], idx) : kPadKey;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const uint32_t p = sl * kPer + r, idx = lane * kPer + r;
+      const bool valid = p < m;
+      uint32_t hi = 0xffffffffu, lo = 0xffffffffu;
+      uint8_t c = 0;
+      if (valid) {
+        text_key8(t, U.len, cyc_pos(vq[r], depth, U.len), hi, lo);
+        c = t[vq[r] == 0 ? U.len - 1 : vq[r] - 1];
+      }
+      Lv[w][idx] = vq[r];
+      Lc[w][idx] = c;
+      K[r] = valid ? make_key1(hi, lo, idx) : kPadKey;
+    }
   }
   bool done[kPer];
 #pragma unroll
@@ -1010,8 +1078,8 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     }
     if (__ballot(any_tied) == 0) break;
     depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
-    if (++round >= kBsRounds || depth >= kDWave) {
-      bsort_tail<kSeg, kPer>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
+    if (++round >= kRounds || depth >= kDWave) {
+      bsort_tail<kSeg, kPer, kBatch>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       break;
     }
     // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
@@ -1230,11 +1298,25 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     fprintf(stderr, "[bzg sort S2] buckets by class: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", ncls[0],
             ncls[1], ncls[2], ncls[3], ncls[4], ncls[5]);
   if (ncls[0]) k_tiny<<<ceil_div(ncls[0], 8 * (kT / 64)), kT, 0, st>>>(C.l[0], ncls[0], B, O);
-  if (ncls[1]) k_bsort<16, 1><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
-  if (ncls[2]) k_bsort<32, 1><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O);
-  if (ncls[3]) k_bsort<64, 1><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O);
-  if (ncls[4]) k_bsort<64, 2><<<ceil_div(ncls[4], kT / 64), kT, 0, st>>>(C.l[4], ncls[4], B, O);
-  if (ncls[5]) k_bsort<64, 4><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O);
+  // bitonic rounds before the rank-counting tail, and batched gathers, per class (measured:
+  // rounds are cheaper than the tail for the large classes)
+#ifndef BZG_R5
+#define BZG_R5 16
+#endif
+#ifndef BZG_R4
+#define BZG_R4 8
+#endif
+#ifndef BZG_BL4
+#define BZG_BL4 1
+#endif
+#ifndef BZG_BL5
+#define BZG_BL5 0
+#endif
+  if (ncls[1]) k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
+  if (ncls[2]) k_bsort<32, 1, 2, false><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O);
+  if (ncls[3]) k_bsort<64, 1, 2, false><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O);
+  if (ncls[4]) k_bsort<64, 2, BZG_R4, (bool)BZG_BL4><<<ceil_div(ncls[4], kT / 64), kT, 0, st>>>(C.l[4], ncls[4], B, O);
+  if (ncls[5]) k_bsort<64, 4, BZG_R5, (bool)BZG_BL5><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O);
   HIP_OK(hipGetLastError());
   read_counters();
   const uint32_t n_deep = hc[19];
