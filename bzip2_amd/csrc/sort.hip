@@ -185,9 +185,10 @@ __global__ void k_group_tiles(const Grp* __restrict__ L, uint32_t n, uint32_t* _
 // of its rotation, most significant first, of which grp_cache(g) bytes are valid.  A pass
 // consumes the top byte; a group whose cache is empty gathers 4 characters from the text
 // (identity groups read them coalesced), so the text is read once per 4 passes.
-//   counting kernels (k_s1_hist, k_s1s_count) leave, for an empty cache, the gathered key in
+//   k_s1_hist leaves, for an empty cache, the gathered key in
 //   the source slot's cache (each member is owned by one workgroup), so that
-//   scatter kernels (k_s1_scatter, k_s1s_scatter) find a full cache in every non-identity slot.
+//   k_s1_scatter finds a full cache in every non-identity slot (k_s1s_pass, which counts and
+//   scatters in one kernel, refills in registers).
 // Loads are issued through a selected address (cache slot or text) before any value is used,
 // so a wave keeps all kPerT gathers in flight; keys that wrap past the unit end are patched
 // afterwards (rare).
@@ -482,8 +483,9 @@ struct S1sOwner {
 };
 
 // Packed path: rotations vv, keys kk and groups jj of the tile's elements (lanes past n get
-// element n - 1's).  kCounting: empty caches are refilled from the text and stored back.
-template <bool kCounting>
+// element n - 1's).  kCounting: empty caches are refilled from the text (kWriteBack: and
+// stored back to the source slots).
+template <bool kCounting, bool kWriteBack = kCounting>
 __device__ __forceinline__ void s1s_load(const S1sLds& S, const SortBufs& B, uint32_t ni, uint32_t n,
                                          uint32_t (&vv)[kPerTS], uint32_t (&kk)[kPerTS], uint32_t (&jj)[kPerTS]) {
   const S1sOwner own(S, ni);
@@ -513,7 +515,7 @@ __device__ __forceinline__ void s1s_load(const S1sLds& S, const SortBufs& B, uin
       kk[i] = q + 4 <= S.glen[j] ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.gtoff[j], S.glen[j], q);
     }
   }
-  if (kCounting) {
+  if (kWriteBack) {
 #pragma unroll
     for (int i = 0; i < (int)kPerTS; i++) {
       const uint32_t fl = S.gfl[jj[i]];
@@ -523,44 +525,34 @@ __device__ __forceinline__ void s1s_load(const S1sLds& S, const SortBufs& B, uin
   }
 }
 
-__global__ void __launch_bounds__(kTS) k_s1s_count(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
-                                                  const uint32_t* __restrict__ last, SortBufs B,
-                                                  uint32_t* __restrict__ ccnt, uint32_t nTot, uint32_t ibase) {
+// One packed pass in one kernel: counts, LDS reorder, stores of the slots and caches, and
+// the tile's buckets of two or more rotations as records (group:4 | start:14 | size:14,
+// tile-relative) in the tile's own part of `rec` (it starts at half the tile's first element
+// offset: a tile of n rotations has at most n / 2 such buckets), with the per-class counts for
+// the class-major scan.  k_s1s_emit turns the records into class-list entries.
+__device__ __forceinline__ uint32_t rec_pack(uint32_t j, uint32_t start, uint32_t size) {
+  return (j << 28) | (start << 14) | size;
+}
+
+__global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+                                                 const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
+                                                 SortBufs B, SortOut O, uint32_t* __restrict__ rec,
+                                                 uint32_t* __restrict__ nrec, uint32_t* __restrict__ ccnt, uint32_t nTot,
+                                                 uint32_t ibase) {
   __shared__ S1sLds S;
+  __shared__ uint32_t Lv[2 * kSG], Lk[2 * kSG];  // the tile in bucket order
+  __shared__ uint32_t nr;
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const uint32_t ni = s1s_setup(S, SG, first, last, t, B);
   if (ni == 0) {
     if (threadIdx.x < (uint32_t)kNCls) ccnt[(size_t)threadIdx.x * nTot + ibase + t] = 0;
+    if (threadIdx.x == 0) nrec[t] = 0;
     return;
   }
-  const uint32_t n = S.goff[ni];
-  uint32_t vv[kPerTS], jj[kPerTS], kk[kPerTS];
-  s1s_load<true>(S, B, ni, n, vv, kk, jj);
-#pragma unroll
-  for (int i = 0; i < (int)kPerTS; i++)
-    if (i * kTS + threadIdx.x < n) atomicAdd(&S.cnt[jj[i] * 256 + (kk[i] >> 24)], 1u);
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < ni * 256; b += kTS) {
-    const uint32_t j = b >> 8;
-    const uint32_t cl = bucket_cls(S.cnt[b], grp_depth(Grp{0, 0, 0, S.gfl[j]}) + 1);
-    if (cl < (uint32_t)kNCls) atomicAdd(&S.cc[cl], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x < (uint32_t)kNCls) ccnt[(size_t)threadIdx.x * nTot + ibase + t] = S.cc[threadIdx.x];
-}
-
-__global__ void __launch_bounds__(kTS) k_s1s_scatter(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
-                                                    const uint32_t* __restrict__ last, SortBufs B, SortOut O,
-                                                    const uint32_t* __restrict__ cscan,
-                                                    uint32_t nTot, uint32_t ibase, ClsLists C) {
-  __shared__ S1sLds S;
-  __shared__ uint32_t Lv[2 * kSG], Lk[2 * kSG];  // the tile in bucket order
-  const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t ni = s1s_setup(S, SG, first, last, t, B);
-  if (ni == 0) return;
+  if (threadIdx.x == 0) nr = 0;
   const uint32_t n = S.goff[ni];
   uint32_t vv[kPerTS], kk[kPerTS], jj[kPerTS];
-  s1s_load<false>(S, B, ni, n, vv, kk, jj);
+  s1s_load<true, false>(S, B, ni, n, vv, kk, jj);
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++)
     if (i * kTS + threadIdx.x < n) jj[i] = atomicAdd(&S.cnt[jj[i] * 256 + (kk[i] >> 24)], 1u) | (jj[i] << 16);
@@ -584,25 +576,16 @@ __global__ void __launch_bounds__(kTS) k_s1s_scatter(const Grp* __restrict__ SG,
     }
   }
   __syncthreads();
-  // bucket emission (before the cursors move)
+  // bucket records and class counts
+  uint32_t* trec = rec + P[first[t]] / 2;
   for (uint32_t b = threadIdx.x; b < ni * 256; b += kTS) {
     const uint32_t j = b >> 8, total = S.cnt[b];
-    const uint32_t fl = S.gfl[j];
-    const uint32_t depth = grp_depth(Grp{0, 0, 0, fl}) + 1;
-    const uint32_t cl = bucket_cls(total, depth);
+    const uint32_t cl = bucket_cls(total, grp_depth(Grp{0, 0, 0, S.gfl[j]}) + 1);
     if (cl == 0xffu) continue;
-    const uint32_t dst_alt = (fl & kGrpIdent) ? 0u : ((fl & kGrpAlt) ^ 1u);
-    const Grp gf{0, 0, 0, fl};
-    const Grp nb{S.gstart[j] + S.cur[b] - S.goff[j], total, S.gunit[j], grp_flags(dst_alt, depth, s1_next_cache(gf))};
-    if (cl == kClsDeep) {
-      O.deep[atomicAdd(O.n_deep, 1u)] = nb;
-    } else {
-      const uint32_t r = atomicAdd(&S.cc[cl], 1u);
-      C.l[cl][C.base[cl] + cscan[(size_t)cl * nTot + ibase + t] - cscan[(size_t)cl * nTot] + r] = nb;
-    }
+    if (cl < (uint32_t)kNCls) atomicAdd(&S.cc[cl], 1u);
+    trec[atomicAdd(&nr, 1u)] = rec_pack(j, S.cur[b], total);
   }
-  // reorder the tile by bucket in LDS (jj = rank in bin | group << 16), then store along
-  // each group's slots
+  // reorder the tile by bucket in LDS (jj = rank in bin | group << 16)
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {
     if (i * kTS + threadIdx.x < n) {
@@ -612,6 +595,8 @@ __global__ void __launch_bounds__(kTS) k_s1s_scatter(const Grp* __restrict__ SG,
     }
   }
   __syncthreads();
+  if (threadIdx.x < (uint32_t)kNCls) ccnt[(size_t)threadIdx.x * nTot + ibase + t] = S.cc[threadIdx.x];
+  if (threadIdx.x == 0) nrec[t] = nr;
   const S1sOwner own(S, ni);
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {
@@ -633,6 +618,47 @@ __global__ void __launch_bounds__(kTS) k_s1s_scatter(const Grp* __restrict__ SG,
     if (x < n) {
       const uint32_t j = own(x);
       if (S.cnt[j * 256 + (kk[i] >> 24)] == 1) emit_final(B, O, B.units[S.gunit[j]], S.gunit[j], jj[i], vv[i], true);
+    }
+  }
+}
+
+// The records of k_s1s_pass into the class lists (class-major offsets from cscan) or the
+// deep list.
+__global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+                                                const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
+                                                const SortBufs B, SortOut O, const uint32_t* __restrict__ rec,
+                                                const uint32_t* __restrict__ nrec, const uint32_t* __restrict__ cscan,
+                                                uint32_t nTot, uint32_t ibase, ClsLists C) {
+  __shared__ uint32_t gstart[kSGrp], goff[kSGrp], gfl[kSGrp], gunit[kSGrp];
+  __shared__ uint32_t cc[kNCls];
+  const uint32_t t = blockIdx.x;
+  const uint32_t i0 = first[t];
+  if (i0 == 0xffffffffu) return;
+  const uint32_t ni = min(last[t], i0 + kSGrp) - i0;
+  if (threadIdx.x < ni) {
+    const Grp g = SG[i0 + threadIdx.x];
+    gstart[threadIdx.x] = g.start;
+    goff[threadIdx.x] = P[i0 + threadIdx.x] - P[i0];
+    gfl[threadIdx.x] = g.flags;
+    gunit[threadIdx.x] = g.unit;
+  }
+  if (threadIdx.x < (uint32_t)kNCls) cc[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t* trec = rec + P[i0] / 2;
+  const uint32_t m = nrec[t];
+  for (uint32_t x = threadIdx.x; x < m; x += kT) {
+    const uint32_t r = trec[x];
+    const uint32_t j = r >> 28, start = (r >> 14) & 0x3fffu, total = r & 0x3fffu;
+    const uint32_t fl = gfl[j];
+    const uint32_t depth = grp_depth(Grp{0, 0, 0, fl}) + 1;
+    const uint32_t cl = bucket_cls(total, depth);
+    const uint32_t dst_alt = (fl & kGrpIdent) ? 0u : ((fl & kGrpAlt) ^ 1u);
+    const Grp nb{gstart[j] + start - goff[j], total, gunit[j], grp_flags(dst_alt, depth, s1_next_cache(Grp{0, 0, 0, fl}))};
+    if (cl == kClsDeep) {
+      O.deep[atomicAdd(O.n_deep, 1u)] = nb;
+    } else {
+      const uint32_t q = atomicAdd(&cc[cl], 1u);
+      C.l[cl][C.base[cl] + cscan[(size_t)cl * nTot + ibase + t] - cscan[(size_t)cl * nTot] + q] = nb;
     }
   }
 }
@@ -1212,6 +1238,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* P = ws.u32("sort_P", ccap[6] + 16);
   uint32_t* first = ws.u32("sort_first", max_ptiles);
   uint32_t* last = ws.u32("sort_last", max_ptiles);
+  uint32_t* nrec = ws.u32("sort_nrec", max_ptiles);
+  uint32_t* srec = ws.u32("sort_rec", S / 2 + 64);  // packed-pass bucket records
   uint32_t* scratch =
       ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[6])) + 64);
   uint32_t hc[24];
@@ -1259,7 +1287,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipMemsetAsync(first, 0xff, (size_t)nT * 4, st));
       k_tile_first<<<grid(n6), kT, 0, st>>>(P, n6, first, last);
       HIP_OK(hipGetLastError());
-      k_s1s_count<<<nT, kTS, 0, st>>>(cur6, first, last, B, ccnt, nTot, n7);
+      k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
       HIP_OK(hipGetLastError());
     }
     if (n7) {
@@ -1283,7 +1311,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     if (nT) {
-      k_s1s_scatter<<<nT, kTS, 0, st>>>(cur6, first, last, B, O, ccnt, nTot, n7, Cp);
+      k_s1s_emit<<<nT, kT, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7, Cp);
       HIP_OK(hipGetLastError());
     }
     read_counters();
