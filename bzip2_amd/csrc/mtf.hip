@@ -150,7 +150,10 @@ __global__ void __launch_bounds__(64) k_compose(const uint32_t* __restrict__ bof
 // search and shift, no memory access); positions 32..255 live in LDS as 56 words laid out
 // [word][thread].  Ranks >= 32 are rare (< 0.1% on text), so the LDS part is touched by few
 // steps of a wave.
-constexpr int kRegW = 8;
+#ifndef BZG_MTF_REGW
+#define BZG_MTF_REGW 8
+#endif
+constexpr int kRegW = BZG_MTF_REGW;  // list words (4 positions each) held in registers
 __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                                 const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
                                                 uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
@@ -182,17 +185,28 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
     uint32_t pos;
     if (fw < (uint32_t)kRegW) {
       pos = fw * 4 + ((uint32_t)__builtin_ctz(fz) >> 3);
-    } else {  // beyond position 31: LDS words (every block byte is in the list)
+    } else {  // beyond the register words: LDS words, 4 loads in flight per step (every
+              // block byte is in the list)
       uint32_t w = kRegW, x = 0;
-      for (; w < 64; w++) {
-        x = lst[w - kRegW][t] ^ pat;
-        const uint32_t zz = (x - 0x01010101u) & ~x & 0x80808080u;
-        if (zz) {
-          x = zz;
+      for (; w < 64; w += 4) {
+        uint32_t y[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) y[k] = lst[w + k - kRegW][t] ^ pat;
+        uint32_t hit = 4;
+#pragma unroll
+        for (int k = 3; k >= 0; k--) {
+          const uint32_t zz = (y[k] - 0x01010101u) & ~y[k] & 0x80808080u;
+          if (zz) {
+            hit = (uint32_t)k;
+            x = zz;
+          }
+        }
+        if (hit < 4) {
+          w += hit;
           break;
         }
       }
-      if (w == 64) {  // only a corrupt input; keeps the loop finite
+      if (w >= 64) {  // only a corrupt input; keeps the loop finite
         w = 63;
         x = 0x80000000u;
       }
@@ -235,7 +249,18 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
       }
     }
     if (tw >= (uint32_t)kRegW) {
-      for (uint32_t w = kRegW; w < tw; w++) {
+      uint32_t w = kRegW;
+      for (; w + 4 <= tw; w += 4) {  // 4 loads in flight per step
+        uint32_t y[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) y[k] = lst[w + k - kRegW][t];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          lst[w + k - kRegW][t] = (y[k] << 8) | carry;
+          carry = y[k] >> 24;
+        }
+      }
+      for (; w < tw; w++) {
         const uint32_t v = lst[w - kRegW][t];
         lst[w - kRegW][t] = (v << 8) | carry;
         carry = v >> 24;

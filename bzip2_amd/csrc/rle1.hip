@@ -87,7 +87,7 @@ __device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_
   for (int k = 0; k < kPer; k++) {
     uint64_t i = base + k;
     uint32_t rs = st[k] > before ? st[k] : before;
-    uint32_t r = (uint32_t)((i - rs) % 255u);
+    uint32_t r = (uint32_t)(i - rs) % 255u;  // run offsets fit 32 bits (n < 2^32)
     uint8_t nx = (k + 1 < kPer) ? v[k + 1] : next_after;
     bool last = (i + 1 >= n) || (nx != v[k]) || (r == 254);
     uint8_t e = r <= 2 ? 1 : (r == 3 ? (uint8_t)(1 + (last ? 1 : 0)) : (uint8_t)(last ? 1 : 0));
@@ -123,6 +123,10 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
                                              uint32_t* __restrict__ last_len1) {
   __shared__ uint32_t sh[kT / 64];
   __shared__ uint32_t thr[kT];
+  // the tile's output (<= 5/4 of its input) staged so that LDS word k is output word
+  // (tile start & ~3) / 4 + k; written back with whole-word stores
+  __shared__ uint32_t ow[kTile * 5 / 16 + 4];
+  uint8_t* ob = reinterpret_cast<uint8_t*>(ow);
   const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
   uint8_t v[kPer];
   load16(x, n, base, v);
@@ -131,8 +135,11 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
   uint32_t s = 0;
 #pragma unroll
   for (int k = 0; k < kPer; k++) s += bi[k].e;
-  uint32_t incl = block_incl_sum(s, sh, (uint32_t*)nullptr);
-  uint32_t pos = out_base[blockIdx.x] + incl - s;
+  uint32_t tot;
+  uint32_t incl = block_incl_sum(s, sh, &tot);
+  const uint32_t t0 = out_base[blockIdx.x];
+  const uint32_t lofs = t0 & 3u;  // LDS byte of output byte p: p - t0 + lofs
+  uint32_t pos = t0 + incl - s;
   // chunk-start bits of this thread's outputs span <= 2 words (<= 32 output bytes)
   const uint32_t w0 = pos >> 5;
   uint32_t bits0 = 0, bits1 = 0;
@@ -147,16 +154,30 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
       if (w == w0) bits0 |= 1u << (pos & 31);
       else bits1 |= 1u << (pos & 31);
     }
+    const uint32_t lp = pos - t0 + lofs;
     if (b.r <= 3) {
-      out[pos] = v[k];
-      if (b.r == 3 && b.last) out[pos + 1] = 0;
+      ob[lp] = v[k];
+      if (b.r == 3 && b.last) ob[lp + 1] = 0;
     } else if (b.last) {
-      out[pos] = (uint8_t)(b.r - 3);
+      ob[lp] = (uint8_t)(b.r - 3);
     }
     pos += b.e;
   }
   if (bits0) atomicOr(&cbits[w0], bits0);
   if (bits1) atomicOr(&cbits[w0 + 1], bits1);
+  __syncthreads();
+  // output words [t0 / 4, (t0 + tot + 3) / 4): interior ones whole, the two edge words
+  // byte by byte (they are shared with the neighbouring tiles)
+  const uint32_t nw = (lofs + tot + 3) >> 2;
+  uint32_t* outw = reinterpret_cast<uint32_t*>(out) + (t0 >> 2);
+  for (uint32_t q = threadIdx.x; q < nw; q += kT) {
+    const uint32_t b0 = q * 4, b1 = b0 + 4;
+    if (b0 >= lofs && b1 <= lofs + tot) {
+      outw[q] = ow[q];
+    } else {
+      for (uint32_t c = max(b0, lofs); c < min(b1, lofs + tot); c++) out[(t0 & ~3u) + c] = ob[c];
+    }
+  }
 }
 
 // Input offset of the chunk whose first output byte is p (p a chunk start), by re-deriving
@@ -278,88 +299,139 @@ __device__ __forceinline__ uint32_t xpow8(const uint32_t* __restrict__ xp2, uint
   return r;
 }
 
-// Block CRC over input [binst[b], binst[b+1]): each thread takes a contiguous slice, slices
-// are folded in order with multiplications by x^(8*len).
+// Block CRC over input [binst[b], binst[b+1]).  The CRC without init / final xor is linear:
+// crc(A || B) = crc(A) * x^(8|B|) + crc(B) over GF(2).  kCrcSplit workgroups per block take
+// equal sub-ranges; in a sub-range, round r gives thread t the 16 bytes at 4096 r + 16 t
+// (coalesced loads), whose CRC (slicing by 16, LDS tables) is folded into the thread's
+// accumulator as acc = acc * x^(8*4096) + crc(piece) (the multiplication by a constant is a
+// linear map: 4 LDS table lookups).  The accumulators are then shifted to their end
+// positions and xor-ed; k_crc_combine folds the sub-ranges and the init/final xor.
+constexpr uint32_t kCrcSplit = 8;
+constexpr uint32_t kCrcRound = kT * 16;
+
+__device__ __forceinline__ uint32_t crc_pow_mul(uint32_t a, const uint32_t* __restrict__ xp2, uint64_t len) {
+  return len ? gf_mul(a, xpow8(xp2, len)) : a;
+}
+
 __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x, const uint32_t* __restrict__ binst,
                                                   const uint32_t* __restrict__ crc_table_g,
-                                                  const uint32_t* __restrict__ xp2_g,
-                                                  uint32_t* __restrict__ bcrc) {
-  // slicing-by-8 tables for the MSB-first CRC: tab[k][b] = tab[0][b] advanced by k zero bytes
-  __shared__ uint32_t tab[8][256];
+                                                  const uint32_t* __restrict__ xp2_g, uint32_t* __restrict__ part) {
+  __shared__ uint32_t tab[16][256];  // tab[k][b] = crc of byte b followed by k zero bytes
+  __shared__ uint32_t mul[4][256];   // byte k of a (from the top) times x^(8*4096)
   __shared__ uint32_t xp2[48];
-  __shared__ uint32_t part[kT];
-  __shared__ uint64_t plen[kT];
-  const int b = blockIdx.x;
+  __shared__ uint32_t red[kT / 64];
+  const uint32_t b = blockIdx.y, w = blockIdx.x;
+  if (threadIdx.x < 48) xp2[threadIdx.x] = xp2_g[threadIdx.x];
   {
     uint32_t v = crc_table_g[threadIdx.x];
     tab[0][threadIdx.x] = v;
     __syncthreads();
 #pragma unroll
-    for (int k = 1; k < 8; k++) {
+    for (int k = 1; k < 16; k++) {
       v = (v << 8) ^ tab[0][v >> 24];
       tab[k][threadIdx.x] = v;
     }
   }
-  if (threadIdx.x < 48) xp2[threadIdx.x] = xp2_g[threadIdx.x];
   __syncthreads();
-  const uint64_t lo = binst[b], hi = binst[b + 1], len = hi - lo;
-  const uint64_t per = (len + kT - 1) / kT;
-  uint64_t s = lo + per * threadIdx.x, e = s + per;
-  if (s > hi) s = hi;
-  if (e > hi) e = hi;
-  uint32_t c = 0;
-  uint64_t i = s;
-  for (; i < e && (i & 7); i++) c = (c << 8) ^ tab[0][(c >> 24) ^ x[i]];
-  for (; i + 8 <= e; i += 8) {
-    const uint2 w = *reinterpret_cast<const uint2*>(x + i);
-    const uint32_t a = c ^ bswap32(w.x), d = bswap32(w.y);
-    c = tab[7][a >> 24] ^ tab[6][(a >> 16) & 255u] ^ tab[5][(a >> 8) & 255u] ^ tab[4][a & 255u] ^
-        tab[3][d >> 24] ^ tab[2][(d >> 16) & 255u] ^ tab[1][(d >> 8) & 255u] ^ tab[0][d & 255u];
+  {
+    const uint32_t xr = xpow8(xp2, kCrcRound);
+#pragma unroll
+    for (int k = 0; k < 4; k++) mul[k][threadIdx.x] = gf_mul(threadIdx.x << (8 * (3 - k)), xr);
   }
-  for (; i < e; i++) c = (c << 8) ^ tab[0][(c >> 24) ^ x[i]];
-  part[threadIdx.x] = c;
-  plen[threadIdx.x] = e - s;
+  const uint32_t lo = binst[b], hi = binst[b + 1];
+  const uint32_t per = ceil_div(hi - lo, kCrcSplit);
+  const uint32_t s0 = min(hi, lo + w * per), s1 = min(hi, s0 + per);
+  const uint32_t len = s1 - s0, R = len / kCrcRound, T = len - R * kCrcRound;
   __syncthreads();
-  // tree fold: combine(a, b) = a * x^(8 len_b) ^ b
-  for (int stride = 1; stride < kT; stride <<= 1) {
-    int i = threadIdx.x;
-    if ((i % (2 * stride)) == 0 && i + stride < kT) {
-      uint64_t lb = plen[i + stride];
-      uint32_t a = part[i];
-      part[i] = (lb ? gf_mul(a, xpow8(xp2, lb)) : a) ^ part[i + stride];
-      plen[i] += lb;
+  auto crc16 = [&](const uint8_t* p) {
+    uint4 q;
+    __builtin_memcpy(&q, p, 16);
+    const uint32_t a = bswap32(q.x), d1 = bswap32(q.y), d2 = bswap32(q.z), d3 = bswap32(q.w);
+    return tab[15][a >> 24] ^ tab[14][(a >> 16) & 255u] ^ tab[13][(a >> 8) & 255u] ^ tab[12][a & 255u] ^
+           tab[11][d1 >> 24] ^ tab[10][(d1 >> 16) & 255u] ^ tab[9][(d1 >> 8) & 255u] ^ tab[8][d1 & 255u] ^
+           tab[7][d2 >> 24] ^ tab[6][(d2 >> 16) & 255u] ^ tab[5][(d2 >> 8) & 255u] ^ tab[4][d2 & 255u] ^
+           tab[3][d3 >> 24] ^ tab[2][(d3 >> 16) & 255u] ^ tab[1][(d3 >> 8) & 255u] ^ tab[0][d3 & 255u];
+  };
+  uint32_t acc = 0;
+  const uint8_t* px = x + s0 + 16 * threadIdx.x;
+  for (uint32_t r = 0; r < R; r++) {
+    const uint32_t c = crc16(px + (size_t)r * kCrcRound);
+    acc = mul[0][acc >> 24] ^ mul[1][(acc >> 16) & 255u] ^ mul[2][(acc >> 8) & 255u] ^ mul[3][acc & 255u] ^ c;
+  }
+  uint32_t res = R ? crc_pow_mul(acc, xp2, kCrcRound - 16 * (threadIdx.x + 1) + T) : 0u;
+  // the tail: thread t takes bytes [16 t, 16 t + 16) of it
+  const uint32_t tb = 16 * threadIdx.x;
+  if (tb < T) {
+    const uint32_t m = min(16u, T - tb);
+    const uint8_t* pt = x + s0 + R * kCrcRound + tb;
+    uint32_t c = 0;
+    if (m == 16) {
+      c = crc16(pt);
+    } else {
+      for (uint32_t i = 0; i < m; i++) c = (c << 8) ^ tab[0][(c >> 24) ^ pt[i]];
     }
-    __syncthreads();
+    res ^= crc_pow_mul(c, xp2, T - tb - m);
   }
-  if (threadIdx.x == 0) {
-    uint32_t init = len ? gf_mul(0xffffffffu, xpow8(xp2, len)) : 0xffffffffu;
-    bcrc[b] = ~(init ^ part[0]);
+  // xor over the workgroup
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) res ^= (uint32_t)__shfl_xor((int)res, o, 64);
+  if (__lane_id() == 0) red[threadIdx.x >> 6] = res;
+  __syncthreads();
+  if (threadIdx.x == 0) part[b * kCrcSplit + w] = red[0] ^ red[1] ^ red[2] ^ red[3];
+}
+
+__global__ void k_crc_combine(const uint32_t* __restrict__ binst, const uint32_t* __restrict__ part,
+                              const uint32_t* __restrict__ xp2, uint32_t nb, uint32_t* __restrict__ bcrc) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint32_t lo = binst[b], hi = binst[b + 1];
+  const uint32_t per = ceil_div(hi - lo, kCrcSplit);
+  uint32_t c = crc_pow_mul(0xffffffffu, xp2, hi - lo);  // the initial register, shifted through
+  for (uint32_t w = 0; w < kCrcSplit; w++) {
+    const uint32_t e = min(hi, min(hi, lo + w * per) + per);
+    c ^= crc_pow_mul(part[b * kCrcSplit + w], xp2, hi - e);
+  }
+  bcrc[b] = ~c;
+}
+
+// In-use bitmap (8 words) per block; blocks are boff[b]..boff[b+1] of blk.  kInUseSplit
+// workgroups per block mark seen bytes in LDS flags from 16-byte loads and OR their bitmap
+// into the (zeroed) global one; k_ninuse counts.
+constexpr uint32_t kInUseSplit = 16;
+__global__ void __launch_bounds__(kT) k_in_use(const uint8_t* __restrict__ blk, const uint32_t* __restrict__ boff,
+                                               uint32_t* __restrict__ inuse) {
+  __shared__ uint8_t seen[256];
+  const uint32_t b = blockIdx.y;
+  seen[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lo = boff[b], hi = boff[b + 1];
+  const uint32_t per = (ceil_div(hi - lo, kInUseSplit) + 15) & ~15u;
+  const uint32_t s0 = lo + blockIdx.x * per, s1 = min(hi, s0 + per);
+  // head bytes up to 16-byte alignment, aligned 16-byte words, tail bytes
+  const uint32_t a0 = min(s1, (s0 + 15) & ~15u), a1 = max(a0, s1 & ~15u);
+  for (uint32_t i = s0 + threadIdx.x; i < a0; i += kT) seen[blk[i]] = 1;
+  for (uint32_t i = a1 + threadIdx.x; i < s1; i += kT) seen[blk[i]] = 1;
+  for (uint32_t i = a0 + threadIdx.x * 16; i < a1; i += kT * 16) {
+    const uint4 q = *reinterpret_cast<const uint4*>(blk + i);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 16; k++) seen[(w[k >> 2] >> (8 * (k & 3))) & 0xffu] = 1;
+  }
+  __syncthreads();
+  const uint64_t m = __ballot(seen[threadIdx.x] != 0);
+  if (__lane_id() < 2) {
+    const uint32_t word = (uint32_t)(m >> (32 * __lane_id()));
+    if (word) atomicOr(&inuse[b * 8 + (threadIdx.x >> 6) * 2 + __lane_id()], word);
   }
 }
 
-// In-use bitmap (8 words) and nInUse per block; blocks are boff[b]..boff[b+1] of blk.
-__global__ void __launch_bounds__(kT) k_in_use(const uint8_t* __restrict__ blk, const uint32_t* __restrict__ boff,
-                                               uint32_t* __restrict__ inuse, uint32_t* __restrict__ ninuse) {
-  __shared__ uint32_t f[8];
-  const int b = blockIdx.x;
-  if (threadIdx.x < 8) f[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t lo = boff[b], hi = boff[b + 1];
-  uint32_t local[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) {
-    uint8_t c = blk[i];
-    local[c >> 5] |= 1u << (c & 31);
-  }
+__global__ void k_ninuse(const uint32_t* __restrict__ inuse, uint32_t nb, uint32_t* __restrict__ ninuse) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  uint32_t c = 0;
 #pragma unroll
-  for (int k = 0; k < 8; k++)
-    if (local[k]) atomicOr(&f[k], local[k]);
-  __syncthreads();
-  if (threadIdx.x < 8) inuse[b * 8 + threadIdx.x] = f[threadIdx.x];
-  if (threadIdx.x == 0) {
-    uint32_t c = 0;
-    for (int k = 0; k < 8; k++) c += __builtin_popcount(f[k]);
-    ninuse[b] = c;
-  }
+  for (int k = 0; k < 8; k++) c += __builtin_popcount(inuse[b * 8 + k]);
+  ninuse[b] = c;
 }
 
 // Primitive period of each block: smallest divisor p of n with blk[i] == blk[i+p] for
@@ -482,7 +554,10 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
 
   const int B = (int)res.nblocks;
   uint32_t* bcrc = ws.u32("bcrc", max_blocks + 2);
-  k_block_crc<<<B, kT, 0, st>>>(d_in, binst, ws.crc_table(), ws.xpow2_table(), bcrc);
+  uint32_t* cpart = ws.u32("crc_part", (size_t)(max_blocks + 2) * kCrcSplit);
+  k_block_crc<<<dim3(kCrcSplit, B), kT, 0, st>>>(d_in, binst, ws.crc_table(), ws.xpow2_table(), cpart);
+  HIP_OK(hipGetLastError());
+  k_crc_combine<<<ceil_div(B, 64), 64, 0, st>>>(binst, cpart, ws.xpow2_table(), B, bcrc);
   HIP_OK(hipGetLastError());
   res.bcrc = bcrc;
   res.blk = blk;
@@ -497,7 +572,10 @@ void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st) {
   res.inuse = ws.u32("inuse", (size_t)(B + 2) * 8);
   res.ninuse = ws.u32("ninuse", B + 2);
   res.period = ws.u32("period", B + 2);
-  k_in_use<<<B, kT, 0, st>>>(res.blk, res.boff, res.inuse, res.ninuse);
+  HIP_OK(hipMemsetAsync(res.inuse, 0, (size_t)B * 8 * 4, st));
+  k_in_use<<<dim3(kInUseSplit, B), kT, 0, st>>>(res.blk, res.boff, res.inuse);
+  HIP_OK(hipGetLastError());
+  k_ninuse<<<ceil_div(B, kT), kT, 0, st>>>(res.inuse, B, res.ninuse);
   HIP_OK(hipGetLastError());
   k_period<<<B, kT, 0, st>>>(res.blk, res.boff, res.period);
   HIP_OK(hipGetLastError());
