@@ -180,6 +180,9 @@ __global__ void k_group_tiles(const Grp* __restrict__ L, uint32_t n, uint32_t* _
   if (g < n) cnt[g] = ceil_div(L[g].size, kDTile);
 }
 
+// LDS exchange among the lanes of one wave (LDS operations of a wave complete in order)
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
 // ---------------------------------------------------------------- S1 byte passes
 // Every member of a group carries a key cache (sk / sk2 beside sa / sa2): the next characters
 // of its rotation, most significant first, of which grp_cache(g) bytes are valid.  A pass
@@ -623,30 +626,37 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
 }
 
 // The records of k_s1s_pass into the class lists (class-major offsets from cscan) or the
-// deep list.
+// deep list; one wave per tile.
 __global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
                                                 const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
-                                                const SortBufs B, SortOut O, const uint32_t* __restrict__ rec,
+                                                uint32_t nT, SortOut O, const uint32_t* __restrict__ rec,
                                                 const uint32_t* __restrict__ nrec, const uint32_t* __restrict__ cscan,
                                                 uint32_t nTot, uint32_t ibase, ClsLists C) {
-  __shared__ uint32_t gstart[kSGrp], goff[kSGrp], gfl[kSGrp], gunit[kSGrp];
-  __shared__ uint32_t cc[kNCls];
-  const uint32_t t = blockIdx.x;
+  __shared__ uint32_t Wg[kT / 64][4][kSGrp];
+  __shared__ uint32_t Wcc[kT / 64][kNCls];
+  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
+  uint32_t* gstart = Wg[wv][0];
+  uint32_t* goff = Wg[wv][1];
+  uint32_t* gfl = Wg[wv][2];
+  uint32_t* gunit = Wg[wv][3];
+  uint32_t* cc = Wcc[wv];
+  const uint32_t t = blockIdx.x * (kT / 64) + wv;
+  if (t >= nT) return;
   const uint32_t i0 = first[t];
   if (i0 == 0xffffffffu) return;
   const uint32_t ni = min(last[t], i0 + kSGrp) - i0;
-  if (threadIdx.x < ni) {
-    const Grp g = SG[i0 + threadIdx.x];
-    gstart[threadIdx.x] = g.start;
-    goff[threadIdx.x] = P[i0 + threadIdx.x] - P[i0];
-    gfl[threadIdx.x] = g.flags;
-    gunit[threadIdx.x] = g.unit;
+  if (lane < ni) {
+    const Grp g = SG[i0 + lane];
+    gstart[lane] = g.start;
+    goff[lane] = P[i0 + lane] - P[i0];
+    gfl[lane] = g.flags;
+    gunit[lane] = g.unit;
   }
-  if (threadIdx.x < (uint32_t)kNCls) cc[threadIdx.x] = 0;
-  __syncthreads();
+  if (lane < (uint32_t)kNCls) cc[lane] = 0;
+  wave_sync();
   const uint32_t* trec = rec + P[i0] / 2;
   const uint32_t m = nrec[t];
-  for (uint32_t x = threadIdx.x; x < m; x += kT) {
+  for (uint32_t x = lane; x < m; x += 64) {
     const uint32_t r = trec[x];
     const uint32_t j = r >> 28, start = (r >> 14) & 0x3fffu, total = r & 0x3fffu;
     const uint32_t fl = gfl[j];
@@ -672,7 +682,6 @@ __global__ void k_cls_bounds(const uint32_t* __restrict__ cscan, uint32_t nTot, 
 }
 
 // ---------------------------------------------------------------- S2
-__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
 // The 8 characters starting at q (< len) as two big-endian words.
 __device__ __forceinline__ void text_key8(const uint8_t* t, uint32_t len, uint32_t q, uint32_t& hi, uint32_t& lo) {
@@ -1311,7 +1320,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     if (nT) {
-      k_s1s_emit<<<nT, kT, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7, Cp);
+      k_s1s_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(cur6, first, last, P, nT, O, srec, nrec, ccnt, nTot, n7, Cp);
       HIP_OK(hipGetLastError());
     }
     read_counters();
