@@ -42,7 +42,7 @@ EXPORTS = [
 ]
 ENGINE_EXPORTS = [
     "bzg_stream_init", "bzg_compress_device", "bzg_compress_host", "bzg_compress_host_stream",
-    "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_last_stats",
+    "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_stage_code_lengths", "bzg_last_stats",
     "bzg_release", "bzg_device_ok", "bzg_periodic_origptr",
 ]
 
@@ -113,6 +113,7 @@ def lib() -> ctypes.CDLL:
         L.bzg_stage_rle1.argtypes = [vp, u64, ci, ci, vp, u64, vp, vp, ctypes.POINTER(u32), u32]
         L.bzg_stage_bwt.argtypes = [vp, vp, u32, vp, vp]
         L.bzg_stage_mtf.argtypes = [vp, vp, u32, vp, vp, vp, vp]
+        L.bzg_stage_code_lengths.argtypes = [vp, vp, u32, ci, vp]
         L.bzg_last_stats.argtypes = [ctypes.POINTER(bzg_stats)]
         L.bzg_periodic_origptr.argtypes = [vp, ctypes.c_int32]
         L.bzg_periodic_origptr.restype = ctypes.c_int32
@@ -216,6 +217,23 @@ def compress_device(d_in_ptr: int, n: int, level: int, d_out_ptr: int, out_cap: 
     if rc != BZ_OK:
         raise BzError(rc, "bzg_compress_device")
     return ob.value, cons.value, st
+
+
+def code_lengths(tables, max_len: int = 17):
+    """BZ2_hbMakeCodeLengths (reference huffman.c:63-148) on the GPU for a list of frequency
+    tables (2..258 counts each); returns the code lengths per table."""
+    n = len(tables)
+    freq = (ctypes.c_uint32 * (max(n, 1) * 258))()
+    alpha = (ctypes.c_int32 * max(n, 1))()
+    for t, f in enumerate(tables):
+        alpha[t] = len(f)
+        for i, v in enumerate(f):
+            freq[t * 258 + i] = v
+    lens = (ctypes.c_uint8 * (max(n, 1) * 258))()
+    rc = lib().bzg_stage_code_lengths(freq, alpha, n, max_len, lens)
+    if rc != BZ_OK:
+        raise BzError(rc, "bzg_stage_code_lengths")
+    return [[lens[t * 258 + i] for i in range(len(f))] for t, f in enumerate(tables)]
 
 
 def periodic_origptr(block: bytes) -> int:

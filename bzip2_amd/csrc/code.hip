@@ -18,59 +18,74 @@ namespace bzg {
 namespace {
 constexpr int kT = 256;
 
-// BZ2_hbMakeCodeLengths (huffman.c:63-148) on one lane: leaf weight = max(freq,1) << 8 | 0,
-// merge = sum of weights | (1 + max depth); heap moves use strict '<'; rescale with
-// w = 1 + w/2 while any length exceeds max_len.
-__device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, int max_len, int32_t* heap,
+// BZ2_hbMakeCodeLengths (huffman.c:63-148), called by all 64 lanes of a wave.  Leaf weight =
+// max(freq,1) << 8 | 0, merge = sum of weights | (1 + max depth); heap moves use strict '<' on
+// weights only; rescale with w = 1 + w/2 while any length exceeds max_len.
+// The heap itself is sequential and runs on lane 0.  Heap entries carry their weight
+// (weight << 32 | node), so a sift step is one LDS round trip; both children are loaded
+// together.  Lengths (parent-chain walks) and the rescale run on all lanes.
+__device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, int max_len, uint64_t* heap,
                                 int32_t* weight, int32_t* parent) {
-  for (int i = 0; i < alpha; i++) weight[i + 1] = (int32_t)((freq[i] == 0 ? 1u : freq[i]) << 8);
+  const int lane = (int)__lane_id();
+  for (int i = lane; i < alpha; i += 64) weight[i + 1] = (int32_t)((freq[i] == 0 ? 1u : freq[i]) << 8);
+  auto wt = [](uint64_t e) { return (int32_t)(e >> 32); };
   for (int round = 0; round < 64; round++) {  // converges in a few rounds for valid tables
-    int nodes = alpha, nheap = 0;
-    heap[0] = 0;
-    weight[0] = 0;
-    parent[0] = -2;
-    for (int i = 1; i <= alpha; i++) {
-      parent[i] = -1;
-      heap[++nheap] = i;
-      int z = nheap, item = heap[z];
-      while (weight[item] < weight[heap[z >> 1]]) {
-        heap[z] = heap[z >> 1];
-        z >>= 1;
-      }
-      heap[z] = item;
-    }
-    while (nheap > 1) {
-      int pick[2];
-      for (int k = 0; k < 2; k++) {
-        pick[k] = heap[1];
-        heap[1] = heap[nheap--];
-        int z = 1, item = heap[1];
+    for (int i = lane; i < 2 * alpha; i += 64) parent[i] = -1;
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      int nodes = alpha, nheap = 0;
+      heap[0] = 0;  // weight 0 sentinel above the root
+      for (int i = 1; i <= alpha; i++) {
+        const uint64_t item = ((uint64_t)(uint32_t)weight[i] << 32) | (uint32_t)i;
+        int z = ++nheap;
         for (;;) {
-          int y = z << 1;
-          if (y > nheap) break;
-          if (y < nheap && weight[heap[y + 1]] < weight[heap[y]]) y++;
-          if (weight[item] < weight[heap[y]]) break;
-          heap[z] = heap[y];
-          z = y;
+          const uint64_t up = heap[z >> 1];
+          if (!(wt(item) < wt(up))) break;
+          heap[z] = up;
+          z >>= 1;
         }
         heap[z] = item;
       }
-      nodes++;
-      parent[pick[0]] = parent[pick[1]] = nodes;
-      const int32_t w0 = weight[pick[0]], w1 = weight[pick[1]];
-      const int32_t d0 = w0 & 0xff, d1 = w1 & 0xff;
-      weight[nodes] = (int32_t)(((uint32_t)w0 & 0xffffff00u) + ((uint32_t)w1 & 0xffffff00u)) | (1 + (d0 > d1 ? d0 : d1));
-      parent[nodes] = -1;
-      heap[++nheap] = nodes;
-      int z = nheap, item = heap[z];
-      while (weight[item] < weight[heap[z >> 1]]) {
-        heap[z] = heap[z >> 1];
-        z >>= 1;
+      while (nheap > 1) {
+        uint64_t pick[2];
+        for (int k = 0; k < 2; k++) {
+          pick[k] = heap[1];
+          const uint64_t item = heap[nheap--];
+          int z = 1;
+          for (;;) {
+            int y = z << 1;
+            if (y > nheap) break;
+            uint64_t c = heap[y];
+            const uint64_t c2 = heap[y + 1];  // in bounds: the array has kMaxAlpha + 4 entries
+            if (y < nheap && wt(c2) < wt(c)) {
+              c = c2;
+              y++;
+            }
+            if (wt(item) < wt(c)) break;
+            heap[z] = c;
+            z = y;
+          }
+          heap[z] = item;
+        }
+        nodes++;
+        parent[(uint32_t)pick[0]] = parent[(uint32_t)pick[1]] = nodes;
+        const int32_t w0 = wt(pick[0]), w1 = wt(pick[1]);
+        const int32_t d0 = w0 & 0xff, d1 = w1 & 0xff;
+        const int32_t wn = (int32_t)(((uint32_t)w0 & 0xffffff00u) + ((uint32_t)w1 & 0xffffff00u)) | (1 + (d0 > d1 ? d0 : d1));
+        const uint64_t item = ((uint64_t)(uint32_t)wn << 32) | (uint32_t)nodes;
+        int z = ++nheap;
+        for (;;) {
+          const uint64_t up = heap[z >> 1];
+          if (!(wt(item) < wt(up))) break;
+          heap[z] = up;
+          z >>= 1;
+        }
+        heap[z] = item;
       }
-      heap[z] = item;
     }
+    __builtin_amdgcn_wave_barrier();
     bool too_long = false;
-    for (int i = 1; i <= alpha; i++) {
+    for (int i = lane + 1; i <= alpha; i += 64) {
       int d = 0, k = i;
       while (parent[k] >= 0) {
         k = parent[k];
@@ -79,8 +94,8 @@ __device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, i
       len[i - 1] = (uint8_t)d;
       if (d > max_len) too_long = true;
     }
-    if (!too_long) return;
-    for (int i = 1; i <= alpha; i++) weight[i] = (1 + ((weight[i] >> 8) / 2)) << 8;
+    if (__ballot(too_long) == 0) return;
+    for (int i = lane + 1; i <= alpha; i += 64) weight[i] = (1 + ((weight[i] >> 8) / 2)) << 8;
   }
 }
 
@@ -213,8 +228,8 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
 // BZ2_hbMakeCodeLengths for table t of block b (one wave; the heap work is sequential).
 __global__ void __launch_bounds__(64) k_huff(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
                                              uint32_t* __restrict__ rf_g, uint8_t* __restrict__ lens_g) {
-  __shared__ int32_t heap[kMaxAlpha + 4];
-  __shared__ int32_t weight[kMaxAlpha * 2];
+  __shared__ uint64_t heap[kMaxAlpha + 4];
+  __shared__ int32_t weight[kMaxAlpha + 2];
   __shared__ int32_t parent[kMaxAlpha * 2];
   __shared__ uint32_t fq[kMaxAlpha];
   __shared__ uint8_t len[kMaxAlpha + 2];
@@ -228,10 +243,29 @@ __global__ void __launch_bounds__(64) k_huff(const uint32_t* __restrict__ nmtf_g
     rf[v] = 0;  // ready for the next iteration
   }
   __syncthreads();
-  if (threadIdx.x == 0) hb_code_lengths(len, fq, alpha, kMaxCodeLen, heap, weight, parent);
+  hb_code_lengths(len, fq, alpha, kMaxCodeLen, heap, weight, parent);
   __syncthreads();
   uint8_t* L = lens_g + ((size_t)b * kNGroups + t) * kMaxAlpha;
   for (int v = threadIdx.x; v < alpha; v += 64) L[v] = len[v];
+}
+
+// Test hook: code lengths of n tables (freq[t * kMaxAlpha ..], alpha[t], max_len) with the
+// same device routine as k_huff.
+__global__ void __launch_bounds__(64) k_code_lengths_test(const uint32_t* __restrict__ freq_g,
+                                                          const int32_t* __restrict__ alpha_g, int max_len,
+                                                          uint8_t* __restrict__ lens_g) {
+  __shared__ uint64_t heap[kMaxAlpha + 4];
+  __shared__ int32_t weight[kMaxAlpha + 2];
+  __shared__ int32_t parent[kMaxAlpha * 2];
+  __shared__ uint32_t fq[kMaxAlpha];
+  __shared__ uint8_t len[kMaxAlpha + 2];
+  const uint32_t t = blockIdx.x;
+  const int alpha = alpha_g[t];
+  for (int v = threadIdx.x; v < alpha; v += 64) fq[v] = freq_g[(size_t)t * kMaxAlpha + v];
+  __syncthreads();
+  hb_code_lengths(len, fq, alpha, max_len, heap, weight, parent);
+  __syncthreads();
+  for (int v = threadIdx.x; v < alpha; v += 64) lens_g[(size_t)t * kMaxAlpha + v] = len[v];
 }
 
 // Canonical codes (huffman.c:152-166), selector MTF (compress.c:573-631), table bits
@@ -636,6 +670,13 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
     carry.carry_byte = 0;
   }
   return full;
+}
+
+void code_lengths_test(const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len, uint8_t* d_lens,
+                       hipStream_t st) {
+  if (n == 0) return;
+  k_code_lengths_test<<<n, 64, 0, st>>>(d_freq, d_alpha, max_len, d_lens);
+  HIP_OK(hipGetLastError());
 }
 
 }  // namespace bzg

@@ -407,4 +407,29 @@ int bzg_stage_mtf(const uint8_t* bwt_in, const uint32_t* offsets, uint32_t nb, u
   }
 }
 
+int bzg_stage_code_lengths(const uint32_t* freq, const int32_t* alpha, uint32_t ntables, int max_len,
+                           uint8_t* lens) {
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  if (ntables == 0) return BZ_OK;
+  for (uint32_t t = 0; t < ntables; t++)
+    if (alpha[t] < 2 || alpha[t] > kMaxAlpha) return BZ_PARAM_ERROR;
+  if (max_len < 1 || max_len > 32) return BZ_PARAM_ERROR;
+  try {
+    const size_t nf = (size_t)ntables * kMaxAlpha;
+    uint32_t* d_freq = e.ws.u32("test_freq", nf);
+    int32_t* d_alpha = reinterpret_cast<int32_t*>(e.ws.u32("test_alpha", ntables));
+    uint8_t* d_lens = e.ws.u8("test_lens", nf);
+    HIP_OK(hipMemcpy(d_freq, freq, 4 * nf, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_alpha, alpha, 4 * (size_t)ntables, hipMemcpyHostToDevice));
+    code_lengths_test(d_freq, d_alpha, ntables, max_len, d_lens, e.stream);
+    HIP_OK(hipStreamSynchronize(e.stream));
+    HIP_OK(hipMemcpy(lens, d_lens, nf, hipMemcpyDeviceToHost));
+    return BZ_OK;
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+}
+
 }  // extern "C"

@@ -93,6 +93,9 @@ struct StreamCarry {
 };
 // Encodes all blocks into `out` (device), starting with the carried partial byte; when
 // `final_batch` appends the stream trailer.  Returns bytes fully written; updates carry.
+// Test hook: BZ2_hbMakeCodeLengths on n tables (kMaxAlpha frequencies each) on the GPU.
+void code_lengths_test(const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len, uint8_t* d_lens,
+                       hipStream_t st);
 uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, const uint32_t* origptr,
                     uint32_t nblocks, int level, bool final_batch, StreamCarry& carry, uint8_t* out,
                     uint64_t out_cap, hipStream_t st);

@@ -66,6 +66,9 @@ int bzg_stage_rle1(const void *src, uint64_t n, int level, int tail_merge, uint8
 int bzg_stage_bwt(const uint8_t *blocks, const uint32_t *offsets, uint32_t nblocks, uint8_t *bwt, int32_t *origptr);
 int bzg_stage_mtf(const uint8_t *bwt, const uint32_t *offsets, uint32_t nblocks, uint16_t *mtfv,
                   uint32_t *mtf_offsets, uint32_t *nmtf, uint32_t *freq);
+/* BZ2_hbMakeCodeLengths (reference huffman.c:63-148) on the GPU for ntables tables: freq holds
+ * kMaxAlpha (258) counts per table, alpha[t] in 2..258 of them used; lens the same layout. */
+int bzg_stage_code_lengths(const uint32_t *freq, const int32_t *alpha, uint32_t ntables, int max_len, uint8_t *lens);
 
 /* origPtr the reference assigns to one exactly periodic block w^k (SURVEY.md 8a row A5;
  * host-side replay of the reference's divsufsort tie order, bzip2_amd/csrc/resolver.cpp).

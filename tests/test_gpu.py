@@ -69,6 +69,37 @@ def gpu_mtf(bwt: bytes, offs):
     return [arr[moff[b]: moff[b] + nmtf[b]].copy() for b in range(nb)], fr
 
 
+def _huffman_tables(seed, n):
+    rng = random.Random(seed)
+    out = [[10] * 6, [int(2 ** (i // 2)) if i < 40 else 1 for i in range(258)]]
+    fib = [1, 1]
+    while len(fib) < 60:
+        fib.append(fib[-1] + fib[-2])
+    out.append(fib[:28])  # depth 27 > 17: rescale rounds (sum 832,039 <= nMTF max, weights fit int32)
+    while len(out) < n:
+        alpha = rng.randint(3, 258)
+        mode = rng.random()
+        if mode < 0.3:
+            f = [rng.randint(0, 5) for _ in range(alpha)]
+        elif mode < 0.6:
+            f = [int(rng.paretovariate(1.1) * 10) for _ in range(alpha)]
+        else:
+            f = [rng.randint(0, 900_000 // alpha) for _ in range(alpha)]
+        out.append(f)
+    return out
+
+
+def test_code_lengths_vs_reference():
+    """A8 (huffman.c:63-148) on the GPU: tie order, rescale rounds, random tables."""
+    tables = _huffman_tables(11, 400)
+    got = B.code_lengths(tables)
+    for f, g in zip(tables, got):
+        want = O.ref_code_lengths(f) if O.has_ref() else O.orc_code_lengths(f)
+        assert g == want, (len(f), f[:8])
+    assert got[0] == [3, 3, 2, 3, 2, 3]
+    assert max(got[1]) == 17 and max(got[2]) <= 17  # table 2 needed rescale rounds (depth 27 unscaled)
+
+
 RLE_CASES = {
     "text": lambda: datagen.text(2_500_000, 21),
     "random": lambda: datagen.random_bytes(700_000, 22),
