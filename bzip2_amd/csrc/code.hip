@@ -186,6 +186,7 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
       const uint16_t* c = S.chunk + threadIdx.x * kGroupSize;
       const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
       uint32_t a = 0, bsum = 0;
+#pragma unroll 10
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t v = c[i];
         a += S.lenp[0][v];
@@ -207,7 +208,22 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
             bt = t;
           }
         selo[g] = (uint8_t)bt;
-        for (uint32_t i = 0; i < n; i++) atomicAdd(&S.rfreq[bt][c[i]], 1u);
+        // symbols 0..3 (RUNA, RUNB and the nearest ranks: most of the group on text) are
+        // counted in registers first, so few lanes of a wave hit the same LDS counter
+        uint32_t f0 = 0, f1 = 0, f2 = 0, f3 = 0;
+#pragma unroll 10
+        for (uint32_t i = 0; i < n; i++) {
+          const uint32_t v = c[i];
+          f0 += v == 0;
+          f1 += v == 1;
+          f2 += v == 2;
+          f3 += v == 3;
+          if (v > 3) atomicAdd(&S.rfreq[bt][v], 1u);
+        }
+        if (f0) atomicAdd(&S.rfreq[bt][0], f0);
+        if (f1) atomicAdd(&S.rfreq[bt][1], f1);
+        if (f2) atomicAdd(&S.rfreq[bt][2], f2);
+        if (f3) atomicAdd(&S.rfreq[bt][3], f3);
       }
     }
   }
