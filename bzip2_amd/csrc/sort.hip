@@ -977,8 +977,20 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
 }
 
 
-template <int kSeg, int kPer, int kRounds, bool kBatch>
-__global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_t nL, SortBufs B, SortOut O) {
+// S2 run emission (classes with one group per wave): after kRounds rounds the runs still tied
+// are left as new groups.  Their rotations are stored at their slots (primary SA) and each run
+// becomes a record (depth:15 | run start:8 | size:9) in the group's own part of `rec` (from
+// half its first slot; a group of m has at most m / 2 runs), with per-class counts
+// ccnt[c * total + gbase + list index] for the class-major scan.  k_s2_emit builds the lists.
+struct S2Emit {
+  uint32_t* rec;
+  uint32_t* ccnt;
+  uint32_t total, gbase;
+};
+
+template <int kSeg, int kPer, int kRounds, bool kBatch, bool kEmit = false>
+__global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_t nL, SortBufs B, SortOut O,
+                                              S2Emit E = S2Emit{}) {
   constexpr int kBPW = 64 / kSeg;
   constexpr int kE = 64 * kPer;  // elements per wave
   __shared__ uint32_t Lv[kT / 64][kE];
@@ -1114,6 +1126,28 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     if (__ballot(any_tied) == 0) break;
     depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
     if (++round >= kRounds || depth >= kDWave) {
+      if constexpr (kEmit) {
+        static_assert(kSeg == 64, "one group per wave");
+        if (depth < kDWave) {
+          uint32_t* cc = Lk[w];  // per-class counters, then the record cursor
+          if (lane < 8) cc[lane] = 0;
+          wave_sync();
+#pragma unroll
+          for (int r = 0; r < kPer; r++) {
+            if (!key_valid(K[r]) || done[r]) continue;
+            const uint32_t p = sl * kPer + r;
+            B.sa[g.start + p] = Lv[w][key_idx(K[r])];
+            if (!tn[r]) {  // last member of its run
+              const uint32_t size = p - rsn[r] + 1;
+              atomicAdd(&cc[size_cls(size)], 1u);
+              E.rec[g.start / 2 + atomicAdd(&cc[7], 1u)] = (depth << 17) | (rsn[r] << 9) | size;
+            }
+          }
+          wave_sync();
+          if (lane < 6) E.ccnt[(size_t)lane * E.total + E.gbase + bi] = cc[lane];
+          break;
+        }
+      }
       bsort_tail<kSeg, kPer, kBatch>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       break;
     }
@@ -1132,6 +1166,45 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
       }
     }
   }
+}
+
+// The records of the emitting k_bsort launches into the next class lists.  One thread per
+// group g of the concatenated classes 3..5 (gb[c]: index of class c's first group, c = 3..6).
+struct S2Lists {
+  const Grp* cur[3];
+  uint32_t gb[4];
+};
+__global__ void k_s2_emit(S2Lists Ls, const uint32_t* __restrict__ rec, const uint32_t* __restrict__ cscan,
+                          uint32_t total, ClsLists N) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  uint32_t n = 0, pos[6];
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    const uint32_t a = cscan[(size_t)c * total + g], e = cscan[(size_t)c * total + g + 1];
+    pos[c] = a - cscan[(size_t)c * total];
+    n += e - a;
+  }
+  if (n == 0) return;
+  const int k = g >= Ls.gb[2] ? 2 : g >= Ls.gb[1] ? 1 : 0;
+  const Grp gr = Ls.cur[k][g - Ls.gb[k]];
+  const uint32_t* gr_rec = rec + gr.start / 2;
+  for (uint32_t x = 0; x < n; x++) {
+    const uint32_t r = gr_rec[x];
+    const uint32_t size = r & 511u, rs = (r >> 9) & 255u, depth = r >> 17;
+    const uint32_t c = size_cls(size);
+    uint32_t p = 0;
+#pragma unroll
+    for (int q = 0; q < 6; q++)
+      if ((uint32_t)q == c) p = pos[q]++;
+    N.l[c][p] = Grp{gr.start + rs, size, gr.unit, grp_flags(0u, depth, 0u)};
+  }
+}
+
+// out[c] = size of class c in a class-major scan of 6 classes (c < 6).
+__global__ void k_s2_bounds(const uint32_t* __restrict__ cscan, uint32_t total, uint32_t* __restrict__ out) {
+  const uint32_t c = threadIdx.x;
+  if (c < 6) out[c] = cscan[(size_t)(c + 1) * total] - cscan[(size_t)c * total];
 }
 
 // ---------------------------------------------------------------- fallback glue
@@ -1235,7 +1308,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   O.deep = ws.typed<Grp>("sort_deep", S / 2 + nb + 16);
   // counters: 0..7 class counts (init), 8..16 class bounds + total, 17 tiles, 18 packed total,
   // 19 n_deep, 20 min depth
-  uint32_t* cnt = ws.u32("sort_cnt", 64);
+  uint32_t* cnt = ws.u32("sort_cnt", 64);  // counters: see below; 24..29 S2 class sizes
   O.n_deep = cnt + 19;
   const size_t max_tiles = S / kDTile + ccap[7] + 16;
   const size_t max_ptiles = S / kSG + 64;
@@ -1251,7 +1324,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* srec = ws.u32("sort_rec", S / 2 + 64);  // packed-pass bucket records
   uint32_t* scratch =
       ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[6])) + 64);
-  uint32_t hc[24];
+  uint32_t hc[32];
   auto read_counters = [&]() {
     HIP_OK(hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -1334,26 +1407,57 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   if (debug)
     fprintf(stderr, "[bzg sort S2] buckets by class: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", ncls[0],
             ncls[1], ncls[2], ncls[3], ncls[4], ncls[5]);
-  if (ncls[0]) k_tiny<<<ceil_div(ncls[0], 8 * (kT / 64)), kT, 0, st>>>(C.l[0], ncls[0], B, O);
-  // bitonic rounds before the rank-counting tail, and batched gathers, per class (measured:
-  // rounds are cheaper than the tail for the large classes)
+  // bitonic rounds before the rank-counting tail (classes 1, 2) or before the still-tied runs
+  // are emitted as new groups (classes 3..5, one group per wave; the S2 loop repeats until
+  // every list is empty)
 #ifndef BZG_R5
-#define BZG_R5 16
+#define BZG_R5 2
 #endif
 #ifndef BZG_R4
-#define BZG_R4 8
+#define BZG_R4 2
 #endif
-#ifndef BZG_BL4
-#define BZG_BL4 1
+#ifndef BZG_R3
+#define BZG_R3 8
 #endif
-#ifndef BZG_BL5
-#define BZG_BL5 0
-#endif
-  if (ncls[1]) k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
-  if (ncls[2]) k_bsort<32, 1, 2, false><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O);
-  if (ncls[3]) k_bsort<64, 1, 2, false><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O);
-  if (ncls[4]) k_bsort<64, 2, BZG_R4, (bool)BZG_BL4><<<ceil_div(ncls[4], kT / 64), kT, 0, st>>>(C.l[4], ncls[4], B, O);
-  if (ncls[5]) k_bsort<64, 4, BZG_R5, (bool)BZG_BL5><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O);
+  {
+    ClsLists N{};
+    for (int c = 0; c < 6; c++) N.l[c] = ws.typed<Grp>("sort_s2n" + std::to_string(c), ccap[c]);
+    const size_t max_s2 = ccap[3] + ccap[4] + ccap[5];
+    uint32_t* ccnt2 = ws.u32("sort_s2cnt", 6 * max_s2 + 16);
+    uint32_t* scratch2 = ws.u32("sort_s2scan", scan_scratch_words(6 * max_s2 + 16) + 64);
+    int s2_iters = 0;
+    for (;;) {
+      ++s2_iters;
+      if (debug)
+        fprintf(stderr, "[bzg sort S2] iter %d: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", s2_iters,
+                ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5]);
+      if (ncls[0]) k_tiny<<<ceil_div(ncls[0], 8 * (kT / 64)), kT, 0, st>>>(C.l[0], ncls[0], B, O);
+      if (ncls[1]) k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
+      if (ncls[2]) k_bsort<32, 1, 2, false><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O);
+      HIP_OK(hipGetLastError());
+      const uint32_t total = ncls[3] + ncls[4] + ncls[5];
+      if (total == 0) break;
+      HIP_OK(hipMemsetAsync(ccnt2, 0, (6 * (size_t)total + 1) * 4, st));
+      S2Emit E{srec, ccnt2, total, 0};
+      if (ncls[3]) k_bsort<64, 1, BZG_R3, false, true><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O, E);
+      E.gbase += ncls[3];
+      if (ncls[4]) k_bsort<64, 2, BZG_R4, true, true><<<ceil_div(ncls[4], kT / 64), kT, 0, st>>>(C.l[4], ncls[4], B, O, E);
+      E.gbase += ncls[4];
+      if (ncls[5]) k_bsort<64, 4, BZG_R5, false, true><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O, E);
+      HIP_OK(hipGetLastError());
+      scan_u32(ScanOp::Sum, true, ccnt2, ccnt2, 6 * (size_t)total + 1, nullptr, scratch2, st);
+      S2Lists Ls{{C.l[3], C.l[4], C.l[5]}, {0, ncls[3], ncls[3] + ncls[4], total}};
+      k_s2_emit<<<grid(total), kT, 0, st>>>(Ls, srec, ccnt2, total, N);
+      k_s2_bounds<<<1, 64, 0, st>>>(ccnt2, total, cnt + 24);
+      HIP_OK(hipGetLastError());
+      read_counters();
+      for (int c = 0; c < 6; c++) {
+        ncls[c] = hc[24 + c];
+        std::swap(C.l[c], N.l[c]);
+      }
+    }
+    if (stats) stats->s2_iters = s2_iters;
+  }
   HIP_OK(hipGetLastError());
   read_counters();
   const uint32_t n_deep = hc[19];

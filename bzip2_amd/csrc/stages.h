@@ -69,6 +69,7 @@ void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st);
 struct SortStats {
   int iterations = 0;
   uint64_t unsorted_elems = 0;  // sum over iterations of elements in unsorted groups
+  int s2_iters = 0;             // S2 rounds of run emission
 };
 void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& h_boff,
                const std::vector<uint32_t>& h_period, uint8_t* bwt, uint32_t* rank0,
