@@ -213,7 +213,7 @@ __device__ __forceinline__ void s1_load(const SortBufs& B, const Grp& gr, const 
   if (ident) {
 #pragma unroll
     for (int i = 0; i < (int)kPerT; i++) vv[i] = min(lo + i * kT + threadIdx.x, hi - 1);
-  } else {
+  } else if (!kCounting || fresh) {  // the histogram of a full cache needs no rotations
 #pragma unroll
     for (int i = 0; i < (int)kPerT; i++) vv[i] = src[gr.start + min(lo + i * kT + threadIdx.x, hi - 1)];
   }
