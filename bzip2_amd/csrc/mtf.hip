@@ -275,35 +275,62 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
   inner[r.gidx] = cnt;
 }
 
-// 4b. per block: carried zero runs, chunk output offsets, nMTF
-__global__ void k_rle2_plan(const uint32_t* __restrict__ boff, const uint32_t* __restrict__ cbase, uint32_t nb,
-                            const uint32_t* __restrict__ ninuse, const uint32_t* __restrict__ lead,
-                            const uint32_t* __restrict__ trail, const uint32_t* __restrict__ inner,
-                            uint32_t* __restrict__ zin, uint32_t* __restrict__ coff, uint32_t* __restrict__ finalrun,
-                            uint32_t* __restrict__ nmtf) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nb) return;
+// 4b. per block (one wave): carried zero runs, chunk output offsets, nMTF.  The zero run
+// entering chunk c is a reset-and-add scan over the chunks (a chunk with a nonzero rank
+// resets it to its trailing zeros, an all-zero chunk adds its length); a chunk's output is
+// nsym(run + its leading zeros) + its inner symbols, and the offsets are their prefix sum.
+// 64 chunks per step, carries between steps.
+__global__ void __launch_bounds__(64) k_rle2_plan(const uint32_t* __restrict__ boff, const uint32_t* __restrict__ cbase,
+                                                  const uint32_t* __restrict__ lead, const uint32_t* __restrict__ trail,
+                                                  const uint32_t* __restrict__ inner, uint32_t* __restrict__ zin,
+                                                  uint32_t* __restrict__ coff, uint32_t* __restrict__ finalrun,
+                                                  uint32_t* __restrict__ nmtf) {
+  const uint32_t b = blockIdx.x, lane = __lane_id();
   const uint32_t n = boff[b + 1] - boff[b];
   const uint32_t nch = ceil_div(n, kChunk);
-  uint32_t zp = 0, off = 0;
-  for (uint32_t c = 0; c < nch; c++) {
+  uint32_t zc = 0, oc = 0;  // carried zero run and output offset
+  for (uint32_t c0 = 0; c0 < nch; c0 += 64) {
+    const uint32_t c = c0 + lane;
+    const bool in = c < nch;
     const uint32_t g = cbase[b] + c;
-    coff[g] = off;
-    const uint32_t ld = lead[g];
-    if (ld == 0xffffffffu) {
-      zp += (c + 1 < nch ? kChunk : n - c * kChunk);
-      zin[g] = 0;
-      continue;
+    const uint32_t ld = in ? lead[g] : 0xffffffffu;
+    const bool allz = ld == 0xffffffffu;
+    // (reset, value): all-zero chunk adds its length, others reset to their trailing zeros
+    uint32_t rs = (in && !allz) ? 1u : 0u;
+    uint32_t v = !in ? 0u : allz ? (c + 1 < nch ? kChunk : n - c * kChunk) : trail[g];
+    const uint32_t inr = (in && !allz) ? inner[g] : 0u;
+    // inclusive scan of the transforms: f2 after f1 = r2 ? (1, v2) : (r1, v1 + v2)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t pr = (uint32_t)__shfl_up((int)rs, o, 64), pv = (uint32_t)__shfl_up((int)v, o, 64);
+      if (lane >= (uint32_t)o && !rs) {
+        rs = pr;
+        v += pv;
+      }
     }
-    const uint32_t z = zp + ld;
-    zin[g] = z;
-    off += nsym(z) + inner[g];
-    zp = trail[g];
+    // run after this chunk = rs ? v : zc + v; the run entering it is the previous lane's
+    const uint32_t after = rs ? v : zc + v;
+    uint32_t before = (uint32_t)__shfl_up((int)after, 1, 64);
+    if (lane == 0) before = zc;
+    const uint32_t z = before + (allz ? 0u : ld);
+    const uint32_t out = (in && !allz) ? nsym(z) + inr : 0u;
+    uint32_t incl = out;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = (uint32_t)__shfl_up((int)incl, o, 64);
+      if (lane >= (uint32_t)o) incl += x;
+    }
+    if (in) {
+      coff[g] = oc + incl - out;
+      zin[g] = allz ? 0u : z;
+    }
+    zc = (uint32_t)__shfl((int)after, 63, 64);
+    oc += (uint32_t)__shfl((int)incl, 63, 64);
   }
-  finalrun[b] = zp;
-  off += nsym(zp) + 1;  // final run + EOB, emitted by the last chunk
-  nmtf[b] = off;
-  (void)ninuse;
+  if (lane == 0) {
+    finalrun[b] = zc;
+    nmtf[b] = oc + nsym(zc) + 1;  // final run + EOB, emitted by the last chunk
+  }
 }
 
 // 4c. emission + symbol frequencies: one wave per chunk, lane l owns ranks [16l, 16l+16).
@@ -470,7 +497,7 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
   HIP_OK(hipGetLastError());
   k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, init, ranks, lead, trail, inner);
   HIP_OK(hipGetLastError());
-  k_rle2_plan<<<ceil_div(nb, 64), 64, 0, st>>>(r.boff, cbase, nb, r.ninuse, lead, trail, inner, zin, coff, finalrun,
+  k_rle2_plan<<<nb, 64, 0, st>>>(r.boff, cbase, lead, trail, inner, zin, coff, finalrun,
                                                 res.nmtf);
   HIP_OK(hipGetLastError());
   k_rle2_emit<<<dim3(ceil_div(maxch, kEW), nb), 64 * kEW, 0, st>>>(ranks, r.boff, cbase, r.ninuse, zin, coff, finalrun,
