@@ -236,16 +236,20 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
     cnt++;
     // move c to the front: positions [0, pos) shift up by one byte
     const uint32_t tw = pos >> 2, tb = pos & 3;
-    uint32_t carry = c;
+    // word w takes its bytes 0..min(pos - 4w, 3) from the list shifted up by one byte
+    // (alignbyte of it and the word below), the rest unchanged (bfi with a byte mask)
+    uint32_t carry = W[kRegW - 1] >> 24;  // the byte pushed into the LDS part (pos >= 4 kRegW)
+    {
+      uint32_t prev = c << 24;
+      const int nbits = 8 * (int)(pos + 1);
 #pragma unroll
-    for (int w = 0; w < kRegW; w++) {
-      const uint32_t v = W[w];
-      if ((uint32_t)w < tw) {
-        W[w] = (v << 8) | carry;
-        carry = v >> 24;
-      } else if ((uint32_t)w == tw) {
-        const uint32_t lowmask = (tb == 3) ? 0xffffffffu : ((1u << (8 * (tb + 1))) - 1u);  // bytes 0..tb
-        W[w] = (v & ~lowmask) | (((v << 8) | carry) & lowmask);
+      for (int w = 0; w < kRegW; w++) {
+        const uint32_t v = W[w];
+        const uint32_t shifted = __builtin_amdgcn_alignbyte(v, prev, 3);
+        const uint32_t sb = (uint32_t)min(max(nbits - 32 * w, 0), 32);
+        const uint32_t m = (uint32_t)((0xffffffffull << sb) >> 32);
+        W[w] = (shifted & m) | (v & ~m);
+        prev = v;
       }
     }
     if (tw >= (uint32_t)kRegW) {
