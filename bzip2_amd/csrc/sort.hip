@@ -33,7 +33,10 @@ namespace {
 
 constexpr int kT = 256;
 constexpr uint32_t kBig = 256;        // buckets larger than this are split by S1 byte passes
-constexpr uint32_t kDTile = 4096;     // rotations per workgroup in an S1 pass
+#ifndef BZG_DTILE
+#define BZG_DTILE 4096
+#endif
+constexpr uint32_t kDTile = BZG_DTILE;  // rotations per workgroup in an S1 pass
 constexpr uint32_t kPerT = kDTile / kT;
 constexpr uint32_t kDBig = 16;        // S1 byte passes stop at this depth (then doubling)
 constexpr uint32_t kDWave = 1024;     // S2 rounds stop at this depth (then doubling)
