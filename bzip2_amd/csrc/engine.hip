@@ -4,7 +4,9 @@
 // guarded by a mutex: bzlib streams from several host threads are serialised on it.
 #include <algorithm>
 #include <cstring>
+#include <exception>
 #include <mutex>
+#include <thread>
 
 #include "../../include/bzg.h"
 #include "resolver.h"
@@ -87,8 +89,11 @@ struct Engine {
   bool init = false;
   bool ok = false;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // the second half of a batch's block sort
   Workspace ws;
+  Workspace ws2;
   hipEvent_t ev[6];
+  hipEvent_t ev2;
   bzg_stats last{};
 
   bool ensure() {
@@ -97,9 +102,58 @@ struct Engine {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ok = false;
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return ok = false;
+    if (hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking) != hipSuccess) return ok = false;
     for (auto& e : ev)
       if (hipEventCreate(&e) != hipSuccess) return ok = false;
+    if (hipEventCreateWithFlags(&ev2, hipEventDisableTiming) != hipSuccess) return ok = false;
     return ok = true;
+  }
+
+  // The block sort of a batch.  Large batches are sorted as two halves of their blocks on two
+  // streams, each driven by its own host thread and workspace: the sorter's host
+  // synchronisations (list sizes between passes) and its narrow late passes then overlap
+  // with the other half's kernels.
+  void sort_blocks(const Rle1Result& r, const std::vector<uint32_t>& hboff, const std::vector<uint32_t>& hper,
+                   uint8_t* bwt, uint32_t* rank0, SortStats* ss, hipStream_t s) {
+    const uint32_t nb = r.nblocks;
+    if (nb < 64) {
+      bwt_stage(ws, r, hboff, hper, bwt, rank0, ss, s);
+      return;
+    }
+    const uint32_t mid = nb / 2;
+    Rle1Result ra = r, rb = r;
+    ra.nblocks = mid;
+    rb.nblocks = nb - mid;
+    rb.blk = r.blk + hboff[mid];
+    std::vector<uint32_t> ha(hboff.begin(), hboff.begin() + mid + 1), pa(hper.begin(), hper.begin() + mid);
+    std::vector<uint32_t> hb(hboff.begin() + mid, hboff.end()), pb(hper.begin() + mid, hper.end());
+    for (auto& x : hb) x -= hboff[mid];
+    HIP_OK(hipEventRecord(ev2, s));  // the second stream starts after this batch's RLE1
+    HIP_OK(hipStreamWaitEvent(stream2, ev2, 0));
+    SortStats sb;
+    std::exception_ptr err;
+    std::thread th([&] {
+      try {
+        bwt_stage(ws2, rb, hb, pb, bwt + hboff[mid], rank0 + mid, &sb, stream2);
+      } catch (...) {
+        err = std::current_exception();
+      }
+    });
+    try {
+      bwt_stage(ws, ra, ha, pa, bwt, rank0, ss, s);
+    } catch (...) {
+      th.join();
+      throw;
+    }
+    th.join();
+    if (err) std::rethrow_exception(err);
+    HIP_OK(hipEventRecord(ev2, stream2));
+    HIP_OK(hipStreamWaitEvent(s, ev2, 0));
+    if (ss) {
+      ss->iterations = std::max(ss->iterations, sb.iterations);
+      ss->unsorted_elems += sb.unsorted_elems;
+      ss->s2_iters = std::max(ss->s2_iters, sb.s2_iters);
+    }
   }
 
   // Compress one batch.  Throws HipFailure on device errors.
@@ -124,7 +178,7 @@ struct Engine {
       HIP_OK(hipStreamSynchronize(s));
       uint8_t* bwt = ws.u8("bwt", hboff[nb] + 16);
       uint32_t* rank0 = ws.u32("rank0", nb + 2);
-      bwt_stage(ws, r, hboff, hper, bwt, rank0, &ss, s);
+      sort_blocks(r, hboff, hper, bwt, rank0, &ss, s);
       std::vector<uint32_t> hr(nb);
       HIP_OK(hipMemcpyAsync(hr.data(), rank0, 4 * nb, hipMemcpyDeviceToHost, s));
       HIP_OK(hipStreamSynchronize(s));
@@ -306,6 +360,7 @@ void bzg_release(void) {
   if (e.init && e.ok) {
     (void)hipDeviceSynchronize();
     e.ws.release_all();
+    e.ws2.release_all();
   }
 }
 
