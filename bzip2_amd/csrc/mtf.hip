@@ -352,9 +352,13 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
                                                         const uint32_t* __restrict__ mtf_off,
                                                         uint16_t* __restrict__ mtfv, uint32_t* __restrict__ freq) {
   __shared__ uint32_t hist[kMaxAlpha];
+  // the chunk's symbols (<= kChunk ranks + carried-in and final runs + EOB), written out
+  // coalesced once the wave has placed them
+  __shared__ uint16_t stage[kEW][kChunk + 96];
   for (int i = threadIdx.x; i < kMaxAlpha; i += 64 * kEW) hist[i] = 0;
   __syncthreads();
   const uint32_t b = blockIdx.y, lane = __lane_id();
+  uint16_t* st = stage[threadIdx.x >> 6];
   const uint32_t c = blockIdx.x * kEW + (threadIdx.x >> 6);
   const uint32_t n = boff[b + 1] - boff[b];
   if (c * kChunk < n) {
@@ -414,15 +418,17 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
     const uint32_t fr = finalrun[b];
     const uint32_t tail = (lastchunk && lane == 63) ? nsym(fr) + 1 : 0u;  // final run + EOB
     const uint32_t tot = ecount + tail;
-    const uint32_t excl = wave_incl_sum(tot) - tot;
-    uint16_t* out = mtfv + mtf_off[b] + coff[g] + excl;
-    uint32_t o = 0;
+    const uint32_t incl = wave_incl_sum(tot), excl = incl - tot;
+    const uint32_t wtot = (uint32_t)__shfl((int)incl, 63, 64);
+    uint16_t* out = st + excl;
+    uint32_t o = 0, runa = 0, runb = 0;  // RUNA / RUNB counted in registers
     auto put_run = [&](uint32_t zz) {
       while (zz > 0) {
         zz--;
         const uint32_t d = zz & 1u;
         out[o++] = (uint16_t)d;
-        atomicAdd(&hist[d], 1u);
+        runa += d ^ 1u;
+        runb += d;
         zz >>= 1;
       }
     };
@@ -450,6 +456,11 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
       out[o++] = (uint16_t)eob;
       atomicAdd(&hist[eob], 1u);
     }
+    if (runa) atomicAdd(&hist[0], runa);
+    if (runb) atomicAdd(&hist[1], runb);
+    __builtin_amdgcn_wave_barrier();
+    uint16_t* gout = mtfv + mtf_off[b] + coff[g];
+    for (uint32_t i = lane; i < wtot; i += 64) gout[i] = st[i];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kMaxAlpha; i += 64 * kEW)
