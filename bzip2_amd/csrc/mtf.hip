@@ -70,18 +70,20 @@ __device__ __forceinline__ ChunkRef chunk_ref(const uint32_t* __restrict__ boff,
 __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                             const uint32_t* __restrict__ cbase, uint8_t* __restrict__ sig,
                                             uint32_t* __restrict__ siglen) {
-  __shared__ uint32_t seen[8][kT];
   const ChunkRef r = chunk_ref(boff, cbase);
-#pragma unroll
-  for (int k = 0; k < 8; k++) seen[k][threadIdx.x] = 0;
   if (!r.valid) return;
   uint8_t* out = sig + (size_t)r.gidx * 256;
   uint32_t cnt = 0;
+  uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // seen bytes, in registers
   for_bytes<false>(L, r.lo, r.hi, [&](uint32_t, uint32_t c) {
-    const uint32_t bit = 1u << (c & 31);
-    const uint32_t w = seen[c >> 5][threadIdx.x];
+    const uint64_t bit = 1ull << (c & 63);
+    const uint32_t q = c >> 6;
+    const uint64_t w = q == 0 ? s0 : q == 1 ? s1 : q == 2 ? s2 : s3;
     if (!(w & bit)) {
-      seen[c >> 5][threadIdx.x] = w | bit;
+      s0 |= q == 0 ? bit : 0ull;
+      s1 |= q == 1 ? bit : 0ull;
+      s2 |= q == 2 ? bit : 0ull;
+      s3 |= q == 3 ? bit : 0ull;
       out[cnt++] = (uint8_t)c;
     }
   });
@@ -113,18 +115,27 @@ __global__ void __launch_bounds__(64) k_compose(const uint32_t* __restrict__ bof
     nu = __shfl(incl, 63, 64);
   }
   __syncthreads();
+  // the next chunk's signature is loaded one step ahead (lane l: bytes 4l..4l+3)
+  uint32_t sl_n = nch ? siglen[cbase[b]] : 0u;
+  uint32_t sw_n = nch ? reinterpret_cast<const uint32_t*>(sig + (size_t)cbase[b] * 256)[lane] : 0u;
   for (uint32_t c = 0; c < nch; c++) {
     const uint32_t g = cbase[b] + c;
+    const uint32_t sl = sl_n, sw = sw_n;
+    if (c + 1 < nch) {
+      sl_n = siglen[g + 1];
+      sw_n = reinterpret_cast<const uint32_t*>(sig + (size_t)(g + 1) * 256)[lane];
+    }
     // publish the initial list of chunk c
     reinterpret_cast<uint32_t*>(init + (size_t)g * 64)[lane] = reinterpret_cast<const uint32_t*>(list)[lane];
-    const uint32_t sl = siglen[g];
     if (lane < 8) mem[lane] = 0;
     __syncthreads();
-    const uint8_t* sg = sig + (size_t)g * 256;
-    for (uint32_t k = lane; k < sl; k += 64) {
-      const uint8_t s = sg[k];
-      atomicOr(&mem[s >> 5], 1u << (s & 31));
-      nlist[k] = s;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      if (lane * 4 + k < sl) {
+        const uint32_t s = (sw >> (8 * k)) & 0xffu;
+        atomicOr(&mem[s >> 5], 1u << (s & 31));
+        nlist[lane * 4 + k] = (uint8_t)s;
+      }
     }
     __syncthreads();
     uint32_t keep = 0;
