@@ -116,7 +116,8 @@ struct Engine {
   void sort_blocks(const Rle1Result& r, const std::vector<uint32_t>& hboff, const std::vector<uint32_t>& hper,
                    uint8_t* bwt, uint32_t* rank0, SortStats* ss, hipStream_t s) {
     const uint32_t nb = r.nblocks;
-    if (nb < 64) {
+    static const bool one_stream = getenv("BZG_ONE_STREAM") != nullptr;  // per-kernel profiling
+    if (nb < 64 || one_stream) {
       bwt_stage(ws, r, hboff, hper, bwt, rank0, ss, s);
       return;
     }
