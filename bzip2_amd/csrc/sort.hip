@@ -1063,7 +1063,6 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
 #pragma unroll
   for (int r = 0; r < kPer; r++) done[r] = false;
   int round = 0;
-  bool emitted = false;  // kEmit: this group's class counts are written
   for (;;) {
     bitonic<kSeg, kPer>(K);
     // ties with the previous / next position of the segment (same run start and key)
@@ -1149,7 +1148,6 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
           }
           wave_sync();
           if (lane < 6) E.ccnt[(size_t)lane * E.total + E.gbase + bi] = cc[lane];
-          emitted = true;
           break;
         }
       }
@@ -1170,9 +1168,6 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
         K[r] = make_key2(rsn[r], hi, lo, idx);
       }
     }
-  }
-  if constexpr (kEmit) {  // no runs left: zero counts (the list is not cleared beforehand)
-    if (!emitted && lane < 6) E.ccnt[(size_t)lane * E.total + E.gbase + bi] = 0;
   }
 }
 
@@ -1445,7 +1440,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
       const uint32_t total = ncls[3] + ncls[4] + ncls[5];
       if (total == 0) break;
-      HIP_OK(hipMemsetAsync(ccnt2 + 6 * (size_t)total, 0, 4, st));  // the scan's closing entry
+      HIP_OK(hipMemsetAsync(ccnt2, 0, (6 * (size_t)total + 1) * 4, st));
       S2Emit E{srec, ccnt2, total, 0};
       if (ncls[3]) k_bsort<64, 1, BZG_R3, false, true><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O, E);
       E.gbase += ncls[3];
