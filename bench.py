@@ -43,6 +43,23 @@ def parse():
     return p.parse_args()
 
 
+def max_over_ranks(x: float, device) -> float:
+    """The job's time: the maximum of the ranks' timed regions (all_reduce MAX)."""
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_mbps(bytes_per_rank: int, world: int, steps: int, elapsed: float) -> float:
+    """Whole-job input-side MB/s: every rank's bytes over the slowest rank's time."""
+    return bytes_per_rank * world * steps / elapsed / 1e6
+
+
+def rank_seed(rank: int) -> int:
+    """Each rank compresses its own synthetic object (weak scaling, no shared input)."""
+    return 0x5EED0001 + rank
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -54,7 +71,7 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     t0 = time.time()
-    data = datagen.text(a.bytes, 0x5EED0001 + rank)
+    data = datagen.text(a.bytes, rank_seed(rank))
     gen_s = time.time() - t0
     d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
     cap = B.bound(len(data))
@@ -84,13 +101,10 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t_start
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, "cuda")
     stats = B.last_stats()
     ms_per_step = elapsed * 1000.0 / a.steps
-    total_bytes = a.bytes * world * a.steps
-    value = total_bytes / elapsed / 1e6  # MB/s, whole job
+    value = job_mbps(a.bytes, world, a.steps, elapsed)  # MB/s, whole job
 
     if rank == 0:
         ratio = out_bytes / a.bytes

@@ -133,8 +133,11 @@ struct Engine {
     HIP_OK(hipStreamWaitEvent(stream2, ev2, 0));
     SortStats sb;
     std::exception_ptr err;
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
     std::thread th([&] {
       try {
+        HIP_OK(hipSetDevice(dev));  // the current device is per host thread
         bwt_stage(ws2, rb, hb, pb, bwt + hboff[mid], rank0 + mid, &sb, stream2);
       } catch (...) {
         err = std::current_exception();

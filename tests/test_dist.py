@@ -1,0 +1,50 @@
+"""Multi-rank logic of bench.py on CPU (gloo, world size 2): every rank reports the slowest
+rank's time, the job value counts every rank's bytes, and ranks compress distinct objects
+(independent streams shard with no data-path collective)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+from tests import datagen
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        elapsed = 1.0 + rank  # rank 1 is the slow one
+        t = bench.max_over_ranks(elapsed, "cpu")
+        v = bench.job_mbps(1000, world, 3, t)
+        out[rank] = (t, v)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_max_time_and_job_value():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        t, v = out[r]
+        assert t == 2.0
+        assert v == pytest.approx(1000 * world * 3 / 2.0 / 1e6)
+
+
+def test_ranks_get_distinct_objects():
+    a = datagen.text(100_000, bench.rank_seed(0))
+    b = datagen.text(100_000, bench.rank_seed(1))
+    assert len(a) == len(b) == 100_000 and a != b
