@@ -183,13 +183,19 @@ struct Engine {
       uint8_t* bwt = ws.u8("bwt", hboff[nb] + 16);
       uint32_t* rank0 = ws.u32("rank0", nb + 2);
       sort_blocks(r, hboff, hper, bwt, rank0, &ss, s);
-      std::vector<uint32_t> hr(nb);
-      HIP_OK(hipMemcpyAsync(hr.data(), rank0, 4 * nb, hipMemcpyDeviceToHost, s));
-      HIP_OK(hipStreamSynchronize(s));
-      resolve_origptrs(r.blk, hboff, hper, hr);  // periodic roots: reference tie rank (A5)
-      HIP_OK(hipMemcpyAsync(origptr, hr.data(), 4 * nb, hipMemcpyHostToDevice, s));
+      bool periodic = false;
+      for (uint32_t b = 0; b < nb; b++) periodic |= hper[b] != hboff[b + 1] - hboff[b];
+      if (periodic) {
+        std::vector<uint32_t> hr(nb);
+        HIP_OK(hipMemcpyAsync(hr.data(), rank0, 4 * nb, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+        resolve_origptrs(r.blk, hboff, hper, hr);  // periodic roots: reference tie rank (A5)
+        HIP_OK(hipMemcpyAsync(origptr, hr.data(), 4 * nb, hipMemcpyHostToDevice, s));
+      } else {  // every origPtr is the sorted rank of rotation 0
+        HIP_OK(hipMemcpyAsync(origptr, rank0, 4 * nb, hipMemcpyDeviceToDevice, s));
+      }
       HIP_OK(hipEventRecord(ev[2], s));
-      mtf_stage(ws, r, bwt, nb, hboff[nb], m, s);
+      mtf_stage(ws, r, bwt, nb, hboff[nb], m, s, &hboff);
       HIP_OK(hipEventRecord(ev[3], s));
     } else {
       HIP_OK(hipEventRecord(ev[2], s));

@@ -481,12 +481,17 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
 }  // namespace
 
 void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t nb, uint32_t total_bytes,
-               MtfResult& res, hipStream_t st) {
+               MtfResult& res, hipStream_t st, const std::vector<uint32_t>* host_boff) {
   (void)total_bytes;
   if (nb == 0) return;
-  std::vector<uint32_t> hboff(nb + 1);
-  HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  std::vector<uint32_t> hboff;
+  if (host_boff) {
+    hboff = *host_boff;
+  } else {
+    hboff.resize(nb + 1);
+    HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
   std::vector<uint32_t> hcb(nb + 1), hmo(nb + 1);
   uint32_t maxch = 0;
   for (uint32_t b = 0; b < nb; b++) {

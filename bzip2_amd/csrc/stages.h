@@ -83,7 +83,7 @@ struct MtfResult {
   uint32_t* freq = nullptr;   // 258 per block
 };
 void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t nblocks,
-               uint32_t total_bytes, MtfResult& res, hipStream_t st);
+               uint32_t total_bytes, MtfResult& res, hipStream_t st, const std::vector<uint32_t>* host_boff = nullptr);
 
 // ---- stage A7/A8/A3 --------------------------------------------------------------------
 struct StreamCarry {
