@@ -40,7 +40,10 @@ constexpr uint32_t kDTile = BZG_DTILE;  // rotations per workgroup in an S1 pass
 constexpr uint32_t kPerT = kDTile / kT;
 constexpr uint32_t kDBig = 16;        // S1 byte passes stop at this depth (then doubling)
 constexpr uint32_t kDWave = 1024;     // S2 rounds stop at this depth (then doubling)
-constexpr uint32_t kSG = 2048;        // S1 groups up to this size are packed into shared tiles
+#ifndef BZG_SG
+#define BZG_SG 2048
+#endif
+constexpr uint32_t kSG = BZG_SG;      // S1 groups up to this size are packed into shared tiles
 // size classes: 0..5 go to S2 (2-8 .. 129-256), 6 / 7 to the next S1 pass (packed / tiled),
 // 8 (still big after kDBig characters) to the doubling fallback
 constexpr int kNCls = 8;
