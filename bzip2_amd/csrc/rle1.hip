@@ -126,7 +126,9 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
   // the tile's output (<= 5/4 of its input) staged so that LDS word k is output word
   // (tile start & ~3) / 4 + k; written back with whole-word stores
   __shared__ uint32_t ow[kTile * 5 / 16 + 4];
+  __shared__ uint32_t cb[kTile * 5 / 128 + 4];  // chunk-start bits, word k = global word (t0 >> 5) + k
   uint8_t* ob = reinterpret_cast<uint8_t*>(ow);
+  for (uint32_t i = threadIdx.x; i < kTile * 5 / 128 + 4; i += kT) cb[i] = 0;
   const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
   uint8_t v[kPer];
   load16(x, n, base, v);
@@ -163,9 +165,20 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
     }
     pos += b.e;
   }
-  if (bits0) atomicOr(&cbits[w0], bits0);
-  if (bits1) atomicOr(&cbits[w0 + 1], bits1);
+  if (bits0) atomicOr(&cb[w0 - (t0 >> 5)], bits0);
+  if (bits1) atomicOr(&cb[w0 + 1 - (t0 >> 5)], bits1);
   __syncthreads();
+  {  // chunk-start words: the two edge words are shared with the neighbouring tiles
+    const uint32_t c0 = t0 >> 5, c1 = tot ? (t0 + tot - 1) >> 5 : c0;
+    for (uint32_t q = threadIdx.x; q <= c1 - c0; q += kT) {
+      const uint32_t v = cb[q];
+      if (q == 0 || q == c1 - c0) {
+        if (v) atomicOr(&cbits[c0 + q], v);
+      } else {
+        cbits[c0 + q] = v;
+      }
+    }
+  }
   // output words [t0 / 4, (t0 + tot + 3) / 4): interior ones whole, the two edge words
   // byte by byte (they are shared with the neighbouring tiles)
   const uint32_t nw = (lofs + tot + 3) >> 2;
