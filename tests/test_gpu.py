@@ -291,6 +291,34 @@ def test_round_trip_large_properties():
     assert B.buff_to_buff_compress(sl, 9) == expected(sl, 9)
 
 
+def _chunks(buf, size):
+    mv = memoryview(buf)
+    return (mv[i:i + size] for i in range(0, len(buf), size))
+
+
+def test_full_size_single_byte_4gib():
+    """BASELINE config 4 at full size: 4 GiB of one byte through chunked BZ2_bzCompress (u32
+    limits, long-run RLE1, periodic blocks); the system decoder returns the input exactly."""
+    n = 1 << 32
+    data = b"a" * n
+    comp = B.stream_compress(_chunks(data, 1 << 28), 9, out_chunk=1 << 24)
+    out = bz2.decompress(comp)
+    assert len(out) == n and out == data
+
+
+def test_full_size_random_4gib_properties():
+    """BASELINE config 5 at full size: 4 GiB of PRNG bytes.  Properties (the whole-stream
+    reference run takes too long here): output size of an incompressible stream
+    (about 1.0044 x input), and the first 256 MiB decode exactly."""
+    n = 1 << 32
+    data = np.random.default_rng(0x5EED0005).integers(0, 256, size=n, dtype=np.uint8).tobytes()
+    comp = B.stream_compress(_chunks(data, 1 << 28), 9, out_chunk=1 << 24)
+    assert 1.003 < len(comp) / n < 1.006
+    d = bz2.BZ2Decompressor()
+    head = d.decompress(comp, max_length=1 << 28)
+    assert head == data[: 1 << 28]
+
+
 def test_device_api_with_torch_buffers():
     torch = pytest.importorskip("torch")
     data = datagen.text(3_000_000, 81)
