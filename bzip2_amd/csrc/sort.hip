@@ -341,7 +341,10 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, ui
   const uint32_t total = tot[(size_t)g * 256 + d];
   const uint32_t gbase = off[(size_t)t * 256 + d];
   cnt[d] = 0;
-  single[d] = total == 1;
+  {  // bit 0: a bucket of one; bit 1: the bucket stays in S1 (needs its key caches)
+    const uint32_t cl = bucket_cls(total, grp_depth(gr) + 1);
+    single[d] = (total == 1 ? 1u : 0u) | (cl == 6 || cl == 7 ? 2u : 0u);
+  }
   uint32_t vv[kPerT], kk[kPerT];
   s1_load<false>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
@@ -376,14 +379,14 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, ui
       kk[i] = Lk[x];
       pos[i] = base[kk[i] >> 24] + x;
       dst[pos[i]] = vv[i];
-      dstk[pos[i]] = kk[i] << 8;
+      if (single[kk[i] >> 24] & 2u) dstk[pos[i]] = kk[i] << 8;
     }
   }
   // a bucket of one: this rotation is ordered (its primary-SA copy is made by k_s1_single,
   // since other workgroups may still read the primary SA in this pass)
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    if (i * kT + threadIdx.x < m && single[kk[i] >> 24]) emit_final(B, O, U, gr.unit, pos[i], vv[i], !dst_alt);
+    if (i * kT + threadIdx.x < m && (single[kk[i] >> 24] & 1u)) emit_final(B, O, U, gr.unit, pos[i], vv[i], !dst_alt);
   if (t != TP[g]) return;
   // ---- bucket emission (digit order within the group)
   const uint32_t depth = grp_depth(gr) + 1;
@@ -617,7 +620,9 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
       jj[i] = S.gstart[j] + x - S.goff[j];  // slot
       const bool dst_alt = !(fl & kGrpIdent) && !(fl & kGrpAlt);
       (dst_alt ? B.sa2 : B.sa)[jj[i]] = vv[i];
-      (dst_alt ? B.sk2 : B.sk)[jj[i]] = kk[i] << 8;
+      // key caches only for buckets that stay in S1 (S2 and S3 read the text)
+      if (bucket_cls(S.cnt[j * 256 + (kk[i] >> 24)], grp_depth(Grp{0, 0, 0, fl}) + 1) == 6u)
+        (dst_alt ? B.sk2 : B.sk)[jj[i]] = kk[i] << 8;
     }
   }
   // a bucket of one: ordered (the group lies in this tile, so the primary SA is free)
