@@ -141,6 +141,27 @@ def main():
             "sort_iterations": stats["sort_iterations"],
             "gen_s": round(gen_s, 1),
         }
+        # SURVEY.md 8(d) second timed region: host buffers in and out (H2D + kernels + D2H),
+        # through BZ2_bzBuffToBuffCompress; never `value`
+        import numpy as np
+        src = np.frombuffer(data, dtype=np.uint8)
+        dst = np.empty(cap, dtype=np.uint8)
+        dl = ctypes.c_uint(cap)
+        L = B.lib()
+
+        def h2h_call():
+            dl.value = cap
+            rc = L.BZ2_bzBuffToBuffCompress(dst.ctypes.data, ctypes.byref(dl), src.ctypes.data, len(data),
+                                            a.level, 0, 30)
+            assert rc == B.BZ_OK, rc
+
+        h2h_call()  # warm-up (host staging buffers)
+        t1 = time.perf_counter()
+        h2h_call()
+        h2h = time.perf_counter() - t1
+        result["host_to_host"] = {"value": round(a.bytes / h2h / 1e6, 2), "unit": "MB/s", "ms": round(h2h * 1e3, 3),
+                                  "out_bytes": int(dl.value),
+                                  "api": "BZ2_bzBuffToBuffCompress, pageable host buffers (H2D + kernels + D2H)"}
         if not a.no_cpu:
             result.update(cpu_and_parity(data, a, d_in))
         print(json.dumps(result), flush=True)
