@@ -38,8 +38,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--bytes", type=int, default=1_000_000_000, help="input bytes per GPU")
     p.add_argument("--level", type=int, default=9)
-    p.add_argument("--cpu-sample", type=int, default=200_000_000, help="bytes for the CPU reference timing")
+    p.add_argument("--cpu-sample", type=int, default=300_000_000, help="bytes for the CPU reference timing")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-h2h", action="store_true", help="skip the host-to-host region (profiling runs)")
     return p.parse_args()
 
 
@@ -131,6 +132,7 @@ def main():
                        "parallelism": f"{world} independent streams"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "traffic_note": "no PMC profile for this workload under profiles/",
                          "model": "SURVEY.md 8(d) B_alg = 1 + 25*rho + 3*c bytes per input byte, whole pipeline",
                          "b_alg_per_byte": round(b_alg, 3),
                          "dominant_stage": {"name": "bwt", "ms": round(stage_ms["bwt"], 3),
@@ -141,33 +143,67 @@ def main():
             "sort_iterations": stats["sort_iterations"],
             "gen_s": round(gen_s, 1),
         }
-        # SURVEY.md 8(d) second timed region: host buffers in and out (H2D + kernels + D2H),
-        # through BZ2_bzBuffToBuffCompress; never `value`
-        import numpy as np
-        src = np.frombuffer(data, dtype=np.uint8)
-        dst = np.empty(cap, dtype=np.uint8)
-        dl = ctypes.c_uint(cap)
-        L = B.lib()
-
-        def h2h_call():
-            dl.value = cap
-            rc = L.BZ2_bzBuffToBuffCompress(dst.ctypes.data, ctypes.byref(dl), src.ctypes.data, len(data),
-                                            a.level, 0, 30)
-            assert rc == B.BZ_OK, rc
-
-        h2h_call()  # warm-up (host staging buffers)
-        t1 = time.perf_counter()
-        h2h_call()
-        h2h = time.perf_counter() - t1
-        result["host_to_host"] = {"value": round(a.bytes / h2h / 1e6, 2), "unit": "MB/s", "ms": round(h2h * 1e3, 3),
-                                  "out_bytes": int(dl.value),
-                                  "api": "BZ2_bzBuffToBuffCompress, pageable host buffers (H2D + kernels + D2H)"}
+        pmc = pmc_traffic(a)
+        if pmc is not None:
+            rl = result["roofline"]
+            rl["traffic"] = round(pmc["traffic_B_per_step"] / (ms_per_step / 1e3) / 1e9, 2)
+            rl["traffic_note"] = (f"GB/s: HBM bytes per step from rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this "
+                                  f"workload ({pmc['file']}, {pmc['correction']}; uncorrected "
+                                  f"{pmc['traffic_lower_B_per_step'] / 1e9:.1f} GB) over this run's step time")
+            rl["traffic_B_per_step"] = round(pmc["traffic_B_per_step"])
+        if not a.no_h2h:
+            result["host_to_host"] = host_to_host(data, a, cap)
         if not a.no_cpu:
             result.update(cpu_and_parity(data, a, d_in))
         print(json.dumps(result), flush=True)
     if dist:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+
+
+def pmc_traffic(a):
+    """HBM bytes per step of this workload, from the newest committed PMC summary
+    (profiles/*_hbm_traffic_v*.json, written by tools_traffic.py); None if there is none."""
+    import glob
+    import re
+
+    best = None
+    for f in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_hbm_traffic_v*.json")):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("bytes_per_step") != a.bytes or f"-{a.level}" not in d.get("workload", ""):
+            continue
+        v = int(re.search(r"_v(\d+)\.json$", f).group(1))
+        if best is None or v > best[0]:
+            d["file"] = "profiles/" + os.path.basename(f)
+            best = (v, d)
+    return best[1] if best else None
+
+
+def host_to_host(data, a, cap):
+    """SURVEY.md 8(d) second timed region: host buffers in and out (H2D + kernels + D2H),
+    through BZ2_bzBuffToBuffCompress; never `value`."""
+    import numpy as np
+    src = np.frombuffer(data, dtype=np.uint8)
+    dst = np.empty(cap, dtype=np.uint8)
+    dl = ctypes.c_uint(cap)
+    L = B.lib()
+
+    def h2h_call():
+        dl.value = cap
+        rc = L.BZ2_bzBuffToBuffCompress(dst.ctypes.data, ctypes.byref(dl), src.ctypes.data, len(data),
+                                        a.level, 0, 30)
+        assert rc == B.BZ_OK, rc
+
+    h2h_call()  # warm-up (host staging buffers)
+    t1 = time.perf_counter()
+    h2h_call()
+    h2h = time.perf_counter() - t1
+    return {"value": round(a.bytes / h2h / 1e6, 2), "unit": "MB/s", "ms": round(h2h * 1e3, 3),
+            "out_bytes": int(dl.value),
+            "api": "BZ2_bzBuffToBuffCompress, pageable host buffers (H2D + kernels + D2H)"}
 
 
 def cpu_and_parity(data, a, d_in):
