@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=300_000_000, help="bytes for the CPU reference timing")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-h2h", action="store_true", help="skip the host-to-host region (profiling runs)")
+    p.add_argument("--mode", choices=["stream", "independent"], default=None,
+                   help="stream: the ranks' inputs are consecutive shards of ONE .bz2 stream, gathered on "
+                        "rank 0 (bzip2_amd/shard.py; default for N > 1); independent: one stream per rank")
     return p.parse_args()
 
 
@@ -67,9 +70,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    if os.environ.get("BZG_DIST_BACKEND") == "gloo":  # rehearsal: every rank on the box's one GPU
+        local = 0
     torch.cuda.set_device(local)
+    mode = a.mode or ("stream" if world > 1 else "independent")
     if dist:
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BZG_DIST_BACKEND", "nccl")  # gloo: multi-rank rehearsal on one GPU
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
 
     t0 = time.time()
     data = datagen.text(a.bytes, rank_seed(rank))
@@ -81,6 +91,11 @@ def main():
     sp = stream.cuda_stream
 
     def step():
+        if mode == "stream":
+            from bzip2_amd import shard
+
+            res = shard.compress_sharded(d_in, rank * a.bytes, world * a.bytes, a.level)
+            return res.numel() / world if res is not None else 0  # per-rank share of the one stream
         nb, cons, _ = B.compress_device(d_in.data_ptr(), len(data), a.level, d_out.data_ptr(), cap, stream_ptr=sp)
         return nb
 
@@ -129,7 +144,9 @@ def main():
             "config": {"workload": f"enwik9-class synthetic text (tests/datagen.py), {a.bytes} B per GPU, -{a.level}",
                        "level": a.level, "bytes_per_gpu": a.bytes, "blocks": stats["nblocks"],
                        "bz2_ratio": round(ratio, 4), "rle1_rho": round(rho, 4),
-                       "parallelism": f"{world} independent streams"},
+                       "parallelism": (f"one stream of {world} x {a.bytes} B sharded over {world} ranks "
+                                       "(RCCL cut chain, P2P halo, bitstream gather to rank 0)")
+                       if mode == "stream" else f"{world} independent streams"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
                          "traffic_note": "no PMC profile for this workload under profiles/",

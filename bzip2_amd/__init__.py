@@ -43,7 +43,7 @@ EXPORTS = [
 ENGINE_EXPORTS = [
     "bzg_stream_init", "bzg_compress_device", "bzg_compress_host", "bzg_compress_host_stream",
     "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_stage_code_lengths", "bzg_last_stats",
-    "bzg_release", "bzg_device_ok", "bzg_periodic_origptr",
+    "bzg_release", "bzg_device_ok", "bzg_periodic_origptr", "bzg_seg_map", "bzg_seg_walk",
 ]
 
 
@@ -116,6 +116,8 @@ def lib() -> ctypes.CDLL:
         L.bzg_stage_code_lengths.argtypes = [vp, vp, u32, ci, vp]
         L.bzg_last_stats.argtypes = [ctypes.POINTER(bzg_stats)]
         L.bzg_periodic_origptr.argtypes = [vp, ctypes.c_int32]
+        L.bzg_seg_map.argtypes = [vp, u64, ci, vp]
+        L.bzg_seg_walk.argtypes = [u32, ci, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.bzg_periodic_origptr.restype = ctypes.c_int32
         _lib = L
     return _lib
@@ -217,6 +219,24 @@ def compress_device(d_in_ptr: int, n: int, level: int, d_out_ptr: int, out_cap: 
     if rc != BZ_OK:
         raise BzError(rc, "bzg_compress_device")
     return ob.value, cons.value, st
+
+
+def seg_map(d_ptr: int, n: int, level: int, stream_ptr: int = 0) -> None:
+    """bzg_seg_map: RLE1 chunk map of a device region that starts at a chunk start."""
+    rc = lib().bzg_seg_map(ctypes.c_void_p(d_ptr), n, level, ctypes.c_void_p(stream_ptr or None))
+    if rc != BZ_OK:
+        raise BzError(rc, "bzg_seg_map")
+
+
+def seg_walk(fill_in: int, final_region: bool, max_cuts: int):
+    """bzg_seg_walk over the last mapped region: (cuts, last_chunk, last_fill), region-relative."""
+    cuts = (ctypes.c_uint64 * max(1, max_cuts))()
+    nc, lc, lf = ctypes.c_uint32(0), ctypes.c_uint64(0), ctypes.c_uint32(0)
+    rc = lib().bzg_seg_walk(fill_in, 1 if final_region else 0, cuts, max_cuts, ctypes.byref(nc), ctypes.byref(lc),
+                            ctypes.byref(lf))
+    if rc != BZ_OK:
+        raise BzError(rc, "bzg_seg_walk")
+    return [int(cuts[i]) for i in range(nc.value)], lc.value, lf.value
 
 
 def code_lengths(tables, max_len: int = 17):

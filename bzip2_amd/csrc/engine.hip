@@ -92,6 +92,11 @@ struct Engine {
   hipStream_t stream2 = nullptr;  // the second half of a batch's block sort
   Workspace ws;
   Workspace ws2;
+  Workspace wseg;  // the mapped region of a sharded stream (bzg_seg_map / bzg_seg_walk)
+  const uint8_t* seg_in = nullptr;
+  uint64_t seg_n = 0;
+  int seg_level = 0;
+  hipStream_t seg_stream = nullptr;
   hipEvent_t ev[6];
   hipEvent_t ev2;
   bzg_stats last{};
@@ -286,6 +291,49 @@ int bzg_compress_device(const void* d_in, uint64_t n, unsigned flags, bzg_stream
     return f.err == hipErrorOutOfMemory ? BZ_OUTBUFF_FULL : BZ_CONFIG_ERROR;
   } catch (const ResolverFailure&) {
     return BZ_CONFIG_ERROR;
+  }
+}
+
+int bzg_seg_map(const void* d_in, uint64_t n, int level, void* stream) {
+  if (level < 1 || level > 9 || (n && !d_in) || n > kMaxBatch) return BZ_PARAM_ERROR;
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
+  try {
+    seg_map_stage(e.wseg, (const uint8_t*)d_in, n, s);
+    e.seg_in = (const uint8_t*)d_in;
+    e.seg_n = n;
+    e.seg_level = level;
+    e.seg_stream = s;
+    return BZ_OK;
+  } catch (const HipFailure& f) {
+    e.seg_in = nullptr;
+    return f.err == hipErrorOutOfMemory ? BZ_MEM_ERROR : BZ_CONFIG_ERROR;
+  }
+}
+
+int bzg_seg_walk(uint32_t fill_in, int final_region, uint64_t* cuts, uint32_t max_cuts, uint32_t* ncuts,
+                 uint64_t* last_chunk, uint32_t* last_fill) {
+  if (!ncuts || !last_chunk || !last_fill || (max_cuts && !cuts)) return BZ_PARAM_ERROR;
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  if (!e.seg_in && e.seg_n) return BZ_PARAM_ERROR;  // no successful bzg_seg_map
+  if (fill_in >= 100000u * (uint32_t)e.seg_level - 19u) return BZ_PARAM_ERROR;
+  try {
+    std::vector<uint64_t> c;
+    uint64_t lc = 0;
+    uint32_t lf = fill_in;
+    seg_walk_stage(e.wseg, e.seg_in, e.seg_n, e.seg_level, fill_in, final_region != 0, c, lc, lf, e.seg_stream);
+    if (c.size() > max_cuts) return BZ_OUTBUFF_FULL;
+    for (size_t i = 0; i < c.size(); i++) cuts[i] = c[i];
+    *ncuts = (uint32_t)c.size();
+    *last_chunk = lc;
+    *last_fill = lf;
+    return BZ_OK;
+  } catch (const HipFailure& f) {
+    return f.err == hipErrorOutOfMemory ? BZ_MEM_ERROR : BZ_CONFIG_ERROR;
   }
 }
 

@@ -291,6 +291,54 @@ __global__ void k_segment(const uint32_t* __restrict__ cbits,
   }
 }
 
+// Cut walk over one region of a sharded stream (one thread).  The region starts
+// at a chunk start of the stream with `fill_in` RLE1 bytes (< nblock_max) already in the open
+// block, so the first cut is the first chunk start at output position >= nblock_max - fill_in;
+// after that the rule is k_segment's.  qpos gets the cut positions followed by the region's last
+// chunk start; res = {ncuts, last chunk start, open-block fill at that chunk start}.
+__global__ void k_segment_fill(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ m_ptr,
+                               uint32_t nblock_max, uint32_t fill_in, int final_region,
+                               const uint32_t* __restrict__ last_len1_ptr, uint32_t* __restrict__ qpos,
+                               uint32_t* __restrict__ res, uint32_t max_cuts) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t m = *m_ptr;
+  if (m == 0) {
+    res[0] = res[1] = 0;
+    res[2] = fill_in;
+    qpos[0] = 0;
+    return;
+  }
+  uint32_t last_start = 0;
+  {
+    uint32_t w = (m - 1) >> 5;
+    for (;;) {
+      uint32_t bits = cbits[w] & (w == ((m - 1) >> 5) ? (0xffffffffu >> (31 - ((m - 1) & 31))) : ~0u);
+      if (bits) { last_start = (w << 5) + 31 - (uint32_t)__builtin_clz(bits); break; }
+      if (w == 0) break;
+      --w;
+    }
+  }
+  const uint32_t last_len1 = *last_len1_ptr;
+  int64_t s = -(int64_t)fill_in;  // output position of the open block's start
+  uint32_t b = 0;
+  for (;;) {
+    const int64_t t = s + (int64_t)nblock_max;
+    uint32_t p = (t <= 0) ? 0u : (t < (int64_t)m ? next_chunk_start(cbits, (uint32_t)t, m) : m);
+    if (p < m && final_region && p == last_start && last_len1) p = m;
+    if (p >= m) break;
+    if (b >= max_cuts) {  // cannot happen with the host's sizing; keep the walk finite
+      res[0] = 0xffffffffu;
+      return;
+    }
+    qpos[b++] = p;
+    s = p;
+  }
+  qpos[b] = last_start;
+  res[0] = b;
+  res[1] = last_start;
+  res[2] = (uint32_t)((int64_t)last_start - s);
+}
+
 // CRC helpers: MSB-first polynomial 0x04C11DB7.
 __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {  // a*b mod P
   uint32_t r = 0;
@@ -577,6 +625,67 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   res.boff = boff;
   res.binst = binst;
   block_info_stage(ws, res, st);
+}
+
+// ---- one region of a sharded stream ------------------------------------
+// seg_map_stage: RLE1 chunk map (chunk-start bitmap, output length) of d_in[0, n), a region
+// that starts at a chunk start.  seg_walk_stage: the cut walk for a given open-block fill,
+// returning region-relative input offsets.  The map is kept in `ws` between the two calls.
+void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t st) {
+  if (n == 0) return;
+  const uint64_t tiles = ceil_div64(n, kTile);
+  const uint64_t mcap = n + n / 4 + 64;
+  uint32_t* tmax = ws.u32("seg_tmax", tiles + 64);
+  uint32_t* tsum = ws.u32("seg_tsum", tiles + 64);
+  uint32_t* scratch = ws.u32("seg_scan", scan_scratch_words(tiles) + 64);
+  uint32_t* mtot = ws.u32("seg_m", 16);
+  uint8_t* blk = ws.u8("seg_blk", mcap + 64);
+  uint32_t* cbits = ws.u32("seg_cbits", mcap / 32 + 64);
+  k_run_starts<<<tiles, kT, 0, st>>>(d_in, n, tmax);
+  HIP_OK(hipGetLastError());
+  scan_u32(ScanOp::Max, true, tmax, tmax, tiles, nullptr, scratch, st);
+  k_emit_count<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum);
+  HIP_OK(hipGetLastError());
+  scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
+  HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
+  k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, blk, cbits, mtot + 8);
+  HIP_OK(hipGetLastError());
+}
+
+void seg_walk_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, uint32_t fill_in,
+                    bool final_region, std::vector<uint64_t>& cuts, uint64_t& last_chunk, uint32_t& last_fill,
+                    hipStream_t st) {
+  cuts.clear();
+  last_chunk = 0;
+  last_fill = fill_in;
+  if (n == 0) return;
+  const uint32_t nblock_max = 100000u * (uint32_t)level - 19u;
+  const uint64_t tiles = ceil_div64(n, kTile);
+  const uint64_t mcap = n + n / 4 + 64;
+  uint32_t* tmax = ws.u32("seg_tmax", tiles + 64);
+  uint32_t* tsum = ws.u32("seg_tsum", tiles + 64);
+  uint32_t* mtot = ws.u32("seg_m", 16);
+  uint32_t* cbits = ws.u32("seg_cbits", mcap / 32 + 64);
+  const uint32_t max_cuts = (uint32_t)(mcap / nblock_max + 8);
+  uint32_t* qpos = ws.u32("seg_qpos", max_cuts + 2);
+  uint32_t* inpos = ws.u32("seg_inpos", max_cuts + 2);
+  uint32_t* res = mtot + 12;
+  k_segment_fill<<<1, 64, 0, st>>>(cbits, mtot, nblock_max, fill_in, final_region ? 1 : 0, mtot + 8, qpos, res,
+                                   max_cuts);
+  HIP_OK(hipGetLastError());
+  uint32_t hres[3];
+  HIP_OK(hipMemcpyAsync(hres, res, 12, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (hres[0] == 0xffffffffu) throw HipFailure(hipErrorUnknown);
+  const uint32_t nq = hres[0] + 1;
+  k_chunk_inpos<<<nq, kT, 0, st>>>(d_in, n, tmax, tsum, (uint32_t)tiles, qpos, nq, inpos);
+  HIP_OK(hipGetLastError());
+  std::vector<uint32_t> h(nq);
+  HIP_OK(hipMemcpyAsync(h.data(), inpos, 4ull * nq, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  for (uint32_t i = 0; i + 1 < nq; i++) cuts.push_back(h[i]);
+  last_chunk = h[nq - 1];
+  last_fill = hres[2];
 }
 
 void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st) {

@@ -61,6 +61,12 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
                 bool tail_merge, Rle1Result& res, hipStream_t st);
 // in-use maps, nInUse and primitive periods of res.nblocks blocks given res.blk / res.boff
 void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st);
+// one region of a sharded stream: RLE1 chunk map, then block cuts for a given
+// open-block fill at the region start (input offsets relative to the region)
+void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t st);
+void seg_walk_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, uint32_t fill_in,
+                    bool final_region, std::vector<uint64_t>& cuts, uint64_t& last_chunk, uint32_t& last_fill,
+                    hipStream_t st);
 
 // ---- stage A4 ------------------------------------------------------------------------
 // Sorts the rotations of every block (of its primitive root when periodic) and writes the

@@ -84,6 +84,23 @@ typedef struct {
   uint64_t sort_unsorted;     /* elements revisited by doubling iterations */
   uint64_t mtf_symbols;       /* total nMTF */
 } bzg_stats;
+/* One region of a sharded stream (the ranks of a job each hold a contiguous
+ * shard of one input stream).  The global block cuts of bzlib.c:211-315 copy_input_until_stop
+ * (a block ends once it holds >= nblockMAX RLE1 bytes; the pending run starts the next one)
+ * depend on every byte before them, so ranks walk them in order; these two calls are the
+ * per-rank part of that chain.
+ *  bzg_seg_map:  RLE1 chunk map of d_in[0, n) (device memory, n <= 1.5e9), a region that starts
+ *                at a chunk start of the stream (a run start, or 255 bytes into a run).  Runs
+ *                on `stream` (0 = the library's own); kept until the next bzg_seg_map.
+ *  bzg_seg_walk: block cuts of the mapped region when the open block already holds fill_in
+ *                (< nblockMAX) RLE1 bytes at the region start: region-relative input offsets
+ *                of the blocks that start inside it (ascending), the offset of the region's
+ *                last chunk start and the open block's fill there.  final_region: the region
+ *                ends the stream (FINISH: the last input byte never starts a block by itself,
+ *                bzlib.c:276-308, 361-396).  BZ_OUTBUFF_FULL when more than max_cuts cuts exist. */
+int bzg_seg_map(const void *d_in, uint64_t n, int level, void *stream);
+int bzg_seg_walk(uint32_t fill_in, int final_region, uint64_t *cuts, uint32_t max_cuts, uint32_t *ncuts,
+                 uint64_t *last_chunk, uint32_t *last_fill);
 void bzg_last_stats(bzg_stats *out);
 
 /* Release the engine's device memory (it is re-acquired on the next call). */

@@ -351,3 +351,82 @@ def test_device_api_continuation_batches():
                                      flags=B.BZG_FLAG_END_SEGMENT | B.BZG_FLAG_TRAILER, state=st)
     out += d_out[:nb].cpu().numpy().tobytes()
     assert bytes(out) == O.orc_compress(data, 1, tail_merge=0)
+
+
+# ------------------------------------------------------------------ one stream sharded
+def _shard_inputs():
+    from tests.test_shard import _inputs
+
+    d = _inputs()
+    d["text_big"] = datagen.text(6_000_000, 93)
+    return d
+
+
+@pytest.mark.parametrize("level", [1, 9])
+def test_seg_walk_chain_matches_whole_stream_cuts(level):
+    """bzg_seg_map / bzg_seg_walk (device) through the rank chain of bzip2_amd.shard, run locally
+    shard after shard, against the whole-stream cut rule (tests/shard_cpu.py, pinned to the
+    oracle's blocks in test_shard.py)."""
+    torch = pytest.importorskip("torch")
+    from bzip2_amd import shard as S
+    from tests.shard_cpu import cuts_whole
+
+    rnd = random.Random(level)
+    for name, data in _shard_inputs().items():
+        want = cuts_whole(data, level)
+        n = len(data)
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+        be = S.GpuBackend(level)
+        for trial in range(3):
+            k = rnd.choice([1, 2, 4, 8])
+            bnd = [0] + sorted(rnd.sample(range(1, n), k - 1)) + [n]
+            msg, cuts = None, []
+            for r, (a, b) in enumerate(zip(bnd, bnd[1:])):
+                c, msg = S.chain_piece(be, t[a:b], a, n, msg, final=(r == len(bnd) - 2))
+                cuts += c
+            assert cuts == want, (name, level, bnd)
+
+
+def _gpu_shard_worker(rank, world, port, cases, out):
+    import torch
+    import torch.distributed as dist
+
+    from bzip2_amd import shard as S
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        for key, (data, level, bnd) in cases.items():
+            t = torch.frombuffer(bytearray(data[bnd[rank]:bnd[rank + 1]]), dtype=torch.uint8).to("cuda")
+            res = S.compress_sharded(t, bnd[rank], len(data), level)
+            torch.cuda.synchronize()
+            if rank == 0:
+                out[key] = res.cpu().numpy().tobytes()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_sharded_stream_on_device(world):
+    """compress_sharded with the GPU backend (HIP path for cuts and compression), ranks sharing
+    cuda:0 over gloo: rank 0's stream equals the reference's stream of the whole input."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    rnd = random.Random(100 + world)
+    cases = {}
+    for name, data in _shard_inputs().items():
+        n = len(data)
+        for level in (1, 9):
+            bnd = [0] + sorted(rnd.sample(range(1, n), world - 1)) + [n]
+            cases[(name, level)] = (data, level, bnd)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_gpu_shard_worker, args=(world, port, cases, out), nprocs=world, join=True)
+    for key, (data, level, bnd) in cases.items():
+        assert out[key] == expected(data, level), (key, bnd)
