@@ -158,6 +158,8 @@ def main():
                                             if stage_ms["bwt"] > 0 else None}},
             "stages_ms": {k: round(v, 3) for k, v in stage_ms.items()},
             "sort_iterations": stats["sort_iterations"],
+            **({"shard_timing_s": __import__("bzip2_amd.shard", fromlist=["x"]).last_timing}
+               if mode == "stream" and os.environ.get("BZG_SHARD_TIMING") == "1" else {}),
             "gen_s": round(gen_s, 1),
         }
         pmc = pmc_traffic(a)

@@ -179,6 +179,7 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
       }
     }
   }
+  if (out == nullptr) return;  // chunk map only (seg_map_stage)
   // output words [t0 / 4, (t0 + tot + 3) / 4): interior ones whole, the two edge words
   // byte by byte (they are shared with the neighbouring tiles)
   const uint32_t nw = (lofs + tot + 3) >> 2;
@@ -639,7 +640,6 @@ void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t s
   uint32_t* tsum = ws.u32("seg_tsum", tiles + 64);
   uint32_t* scratch = ws.u32("seg_scan", scan_scratch_words(tiles) + 64);
   uint32_t* mtot = ws.u32("seg_m", 16);
-  uint8_t* blk = ws.u8("seg_blk", mcap + 64);
   uint32_t* cbits = ws.u32("seg_cbits", mcap / 32 + 64);
   k_run_starts<<<tiles, kT, 0, st>>>(d_in, n, tmax);
   HIP_OK(hipGetLastError());
@@ -648,7 +648,7 @@ void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t s
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
   HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
-  k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, blk, cbits, mtot + 8);
+  k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, nullptr, cbits, mtot + 8);
   HIP_OK(hipGetLastError());
 }
 

@@ -30,6 +30,8 @@ The GPU backend is the product path; tests inject a CPU stand-in backend (gloo, 
 from __future__ import annotations
 
 import ctypes
+import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -39,6 +41,17 @@ from . import BZG_FLAG_END_SEGMENT, BZG_FLAG_TAIL_MERGE, bound, bzg_stream_state
 
 TRAILER_MAGIC = 0x177245385090
 PIECE_MAX = 1_500_000_000  # bzg_seg_map region limit (32-bit RLE1 offsets)
+# BZG_SHARD_TIMING=1: synchronise after each step of compress_sharded and keep the host times
+# (seconds since the call started) in last_timing
+_TIMING = os.environ.get("BZG_SHARD_TIMING") == "1"
+last_timing: dict = {}
+
+
+def _mark(name: str, t0: float, dev) -> None:
+    if _TIMING:
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        last_timing[name] = round(time.perf_counter() - t0, 6)
 
 
 def nblock_max(level: int) -> int:
@@ -191,6 +204,8 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
     d's device, or on the CPU under gloo), the others None.  Shards are contiguous, in rank
     order and non-empty; n_total >= 1."""
     be = backend or GpuBackend(level, torch.cuda.current_stream().cuda_stream if d.is_cuda else 0)
+    t0 = time.perf_counter()
+    last_timing.clear()
     rank, world = (dist.get_rank(), dist.get_world_size()) if _dist_on() else (0, 1)
     gloo = _dist_on() and dist.get_backend() == "gloo"
     cdev = "cpu" if gloo or not d.is_cuda else d.device
@@ -205,6 +220,7 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
     first_p = first_run_start(d[:pieces[0][1]])
     if first_p < pieces[0][1]:
         be.map_region(d[first_p:pieces[0][1]])  # off the critical path
+    _mark("map", t0, d.device)
     msg = None
     if rank > 0:
         m = torch.empty(5, dtype=torch.int64, device=cdev)
@@ -220,6 +236,7 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
     if not last_rank:
         m = torch.tensor(list(msg) + [1], dtype=torch.int64, device=cdev)
         dist.send(m, rank + 1)
+    _mark("chain", t0, d.device)
 
     # 2. ownership and the bytes of each rank's range that live in later shards
     cnt = _all_gather_i64([len(cuts)], cdev)
@@ -269,11 +286,15 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
     for tgt, tmp in recv_fix:
         tgt.copy_(tmp)
 
+    _mark("halo", t0, d.device)
+
     # 3. compress the range
     if buf is not None:
         bits, nbits, nblk, crc = be.compress(buf, header=(lo == 0), final=(hi == n_total))
     else:
         bits, nbits, nblk, crc = torch.zeros(1, dtype=torch.uint8, device=d.device), 0, 0, 0
+
+    _mark("compress", t0, d.device)
 
     # 4. bit offsets, shift, gather to rank 0, trailer
     meta0 = _all_gather_i64([nbits, nblk, crc], cdev)
@@ -302,6 +323,7 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()
+    _mark("gather", t0, d.device)
     if rank != 0:
         return None
     o = 0
@@ -319,4 +341,5 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
     base = total_bits // 8
     final[base] |= tt[0]
     final[base + 1:base + tt.numel()] = tt[1:]
+    _mark("trailer", t0, d.device)
     return final
