@@ -292,25 +292,39 @@ __global__ void k_segment(const uint32_t* __restrict__ cbits,
   }
 }
 
-// Cut walk over one region of a sharded stream (one thread).  The region starts
+// Cut walk over one region of a sharded stream (one wave).  The region starts
 // at a chunk start of the stream with `fill_in` RLE1 bytes (< nblock_max) already in the open
 // block, so the first cut is the first chunk start at output position >= nblock_max - fill_in;
 // after that the rule is k_segment's.  qpos gets the cut positions followed by the region's last
 // chunk start; res = {ncuts, last chunk start, open-block fill at that chunk start}.
-__global__ void k_segment_fill(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ m_ptr,
-                               uint32_t nblock_max, uint32_t fill_in, int final_region,
-                               const uint32_t* __restrict__ last_len1_ptr, uint32_t* __restrict__ qpos,
-                               uint32_t* __restrict__ res, uint32_t max_cuts) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// A chunk is at most 5 RLE1 bytes, so the cut after s lies in [s + M, s + M + 4] (M =
+// nblock_max) and the (j+1)-th cut after s in [s + (j+1) M, s + (j+1) M + 4 j + 4].  Each round,
+// lane j loads the <= 10 bitmap words of that window for step j into LDS (all loads in
+// flight at once), then lane 0 resolves the 64 steps from LDS: one memory round trip per 64
+// cuts instead of one per cut.
+constexpr int kWalkWords = 10;
+__global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict__ cbits,
+                                                     const uint32_t* __restrict__ m_ptr, uint32_t nblock_max,
+                                                     uint32_t fill_in, int final_region,
+                                                     const uint32_t* __restrict__ last_len1_ptr,
+                                                     uint32_t* __restrict__ qpos, uint32_t* __restrict__ res,
+                                                     uint32_t max_cuts) {
+  __shared__ uint32_t win[64][kWalkWords];
+  __shared__ int64_t s_sh;
+  __shared__ int done_sh;
+  const uint32_t lane = threadIdx.x;
   const uint32_t m = *m_ptr;
   if (m == 0) {
-    res[0] = res[1] = 0;
-    res[2] = fill_in;
-    qpos[0] = 0;
+    if (lane == 0) {
+      res[0] = res[1] = 0;
+      res[2] = fill_in;
+      qpos[0] = 0;
+    }
     return;
   }
+  const uint32_t wend = (m + 31) >> 5;
   uint32_t last_start = 0;
-  {
+  if (lane == 0) {
     uint32_t w = (m - 1) >> 5;
     for (;;) {
       uint32_t bits = cbits[w] & (w == ((m - 1) >> 5) ? (0xffffffffu >> (31 - ((m - 1) & 31))) : ~0u);
@@ -320,24 +334,70 @@ __global__ void k_segment_fill(const uint32_t* __restrict__ cbits, const uint32_
     }
   }
   const uint32_t last_len1 = *last_len1_ptr;
-  int64_t s = -(int64_t)fill_in;  // output position of the open block's start
-  uint32_t b = 0;
-  for (;;) {
-    const int64_t t = s + (int64_t)nblock_max;
-    uint32_t p = (t <= 0) ? 0u : (t < (int64_t)m ? next_chunk_start(cbits, (uint32_t)t, m) : m);
-    if (p < m && final_region && p == last_start && last_len1) p = m;
-    if (p >= m) break;
-    if (b >= max_cuts) {  // cannot happen with the host's sizing; keep the walk finite
-      res[0] = 0xffffffffu;
-      return;
-    }
-    qpos[b++] = p;
-    s = p;
+  uint32_t b = 0;  // cuts so far (lane 0)
+  if (lane == 0) {
+    s_sh = -(int64_t)fill_in;  // output position of the open block's start
+    done_sh = 0;
   }
-  qpos[b] = last_start;
-  res[0] = b;
-  res[1] = last_start;
-  res[2] = (uint32_t)((int64_t)last_start - s);
+  __syncthreads();
+  while (!done_sh) {
+    const int64_t s = s_sh;
+    {
+      const int64_t lo = s + (int64_t)(lane + 1) * nblock_max;
+      const int64_t w0 = lo < 0 ? 0 : (lo >> 5);
+#pragma unroll
+      for (int k = 0; k < kWalkWords; k++) {
+        const int64_t w = w0 + k;
+        win[lane][k] = (w < (int64_t)wend) ? cbits[w] : 0u;
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+      int64_t cur = s;
+      int done = 0;
+      for (uint32_t j = 0; j < 64 && !done; j++) {
+        const int64_t lo = s + (int64_t)(j + 1) * nblock_max;
+        const int64_t w0 = lo < 0 ? 0 : (lo >> 5);
+        const int64_t t = cur + (int64_t)nblock_max;
+        uint32_t p = m;
+        if (t <= 0) {
+          p = 0;
+        } else if (t < (int64_t)m) {
+          const int64_t tw = t >> 5;
+          for (int64_t w = tw; w < w0 + kWalkWords && w < (int64_t)wend; w++) {
+            uint32_t bits = win[j][w - w0];
+            if (w == tw) bits &= ~0u << (t & 31);
+            if (bits) {
+              p = (uint32_t)((w << 5) + __builtin_ctz(bits));
+              break;
+            }
+          }
+          if (p > m) p = m;
+        }
+        if (p < m && final_region && p == last_start && last_len1) p = m;
+        if (p >= m) {
+          done = 1;
+          break;
+        }
+        if (b >= max_cuts) {  // cannot happen with the host's sizing; keep the walk finite
+          res[0] = 0xffffffffu;
+          done = 2;
+          break;
+        }
+        qpos[b++] = p;
+        cur = p;
+      }
+      s_sh = cur;
+      done_sh = done;
+      if (done == 1) {
+        qpos[b] = last_start;
+        res[0] = b;
+        res[1] = last_start;
+        res[2] = (uint32_t)((int64_t)last_start - cur);
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // CRC helpers: MSB-first polynomial 0x04C11DB7.
