@@ -40,6 +40,9 @@ def parse():
     p.add_argument("--level", type=int, default=9)
     p.add_argument("--cpu-sample", type=int, default=300_000_000, help="bytes for the CPU reference timing")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="threads for the multi-core reference baseline (the box's CPU share is 16)")
+    p.add_argument("--cpu-mt-sample", type=int, default=640_000_000, help="bytes for the multi-core timing")
     p.add_argument("--no-h2h", action="store_true", help="skip the host-to-host region (profiling runs)")
     p.add_argument("--mode", choices=["stream", "independent"], default=None,
                    help="stream: the ranks' inputs are consecutive shards of ONE .bz2 stream, gathered on "
@@ -241,6 +244,23 @@ def cpu_and_parity(data, a, d_in):
         t = time.perf_counter()
         ref_out = O.orc_compress(sample, a.level)
         cpu_s = time.perf_counter() - t
+    mt = None
+    if O.has_ref() and a.cpu_threads > 1:
+        # N threads, each compressing a contiguous 1/N shard as its own stream
+        # (aggregate MB/s only; no single stream comes out of it)
+        from concurrent.futures import ThreadPoolExecutor
+
+        nt = min(a.cpu_threads, os.cpu_count() or 1)
+        m = min(a.cpu_mt_sample, len(data))
+        step = -(-m // nt)
+        shards = [data[i:min(m, i + step)] for i in range(0, m, step)]
+        with ThreadPoolExecutor(nt) as ex:
+            t = time.perf_counter()
+            list(ex.map(lambda x: O.ref_compress(x, a.level), shards))
+            mt_s = time.perf_counter() - t
+        mt = {"value": round(m / mt_s / 1e6, 3), "unit": "MB/s", "cores": nt, "kind": "reference",
+              "sample": f"first {m} B of the rank-0 input as {len(shards)} independent "
+                        f"BZ2_bzBuffToBuffCompress -{a.level} streams on {nt} threads, {mt_s:.1f} s"}
     cap = B.bound(n)
     d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
     nb, _, _ = B.compress_device(d_in.data_ptr(), n, a.level, d_out.data_ptr(), cap)
@@ -252,6 +272,7 @@ def cpu_and_parity(data, a, d_in):
                                    f"{cpu_s:.1f} s"},
         "parity": {"sample_bytes": n, "bit_exact": gpu_sample == ref_out, "against": kind,
                    "out_bytes": len(ref_out)},
+        **({"cpu_baseline_multicore": mt} if mt else {}),
     }
 
 
