@@ -200,8 +200,9 @@ def _all_gather_i64(vals, device):
 
 def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int, backend=None):
     """Compress input[shard_start, shard_start + len(d)) as this rank's shard of one stream of
-    n_total bytes.  Every rank calls it (without a process group: one rank holding it all); rank 0 returns the whole .bz2 stream (a uint8 tensor on
-    d's device, or on the CPU under gloo), the others None.  Shards are contiguous, in rank
+    n_total bytes.  Every rank calls it (without a process group: one rank holding it all);
+    rank 0 returns the whole .bz2 stream (a uint8 tensor on d's device, or on the CPU under
+    gloo), the others None.  Shards are contiguous, in rank
     order and non-empty; n_total >= 1."""
     be = backend or GpuBackend(level, torch.cuda.current_stream().cuda_stream if d.is_cuda else 0)
     t0 = time.perf_counter()
