@@ -430,3 +430,51 @@ def test_sharded_stream_on_device(world):
     mp.spawn(_gpu_shard_worker, args=(world, port, cases, out), nprocs=world, join=True)
     for key, (data, level, bnd) in cases.items():
         assert out[key] == expected(data, level), (key, bnd)
+
+
+def _gpu_shard_big_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+
+    from bzip2_amd import shard as S
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cases = {
+            # one run across every shard boundary (the host run arithmetic over 255-byte chunks)
+            "byte_a": (lambda: torch.full((200_000_000,), 0x61, dtype=torch.uint8, device="cuda"), 9),
+            "text": (lambda: torch.frombuffer(bytearray(datagen.text(60_000_000, 0x5EED0003)),
+                                              dtype=torch.uint8).to("cuda"), 9),
+        }
+        for key, (make, level) in cases.items():
+            full = make()
+            n = full.numel()
+            bnd = [n * r // world for r in range(world + 1)]
+            if key == "text":  # a boundary right inside the first block's last run of bytes
+                bnd[1] = 899_000
+            res = S.compress_sharded(full[bnd[rank]:bnd[rank + 1]], bnd[rank], n, level)
+            torch.cuda.synchronize()
+            if rank == 0:
+                out[key] = res.cpu().numpy().tobytes()
+            del full
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_stream_on_device_large():
+    """Three ranks on one GPU over gloo: 200 MB of one byte and 60 MB of text at -9, sharded,
+    against the reference's stream of the whole input."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_gpu_shard_big_worker, args=(3, port, out), nprocs=3, join=True)
+    assert out["byte_a"] == expected(b"a" * 200_000_000, 9)
+    assert out["text"] == expected(datagen.text(60_000_000, 0x5EED0003), 9)
