@@ -299,9 +299,11 @@ __global__ void k_segment(const uint32_t* __restrict__ cbits,
 // chunk start; res = {ncuts, last chunk start, open-block fill at that chunk start}.
 // A chunk is at most 5 RLE1 bytes, so the cut after s lies in [s + M, s + M + 4] (M =
 // nblock_max) and the (j+1)-th cut after s in [s + (j+1) M, s + (j+1) M + 4 j + 4].  Each round,
-// lane j loads the <= 10 bitmap words of that window for step j into LDS (all loads in
-// flight at once), then lane 0 resolves the 64 steps from LDS: one memory round trip per 64
-// cuts instead of one per cut.
+// lane j loads the <= 10 bitmap words of that window for step j into LDS (all loads in flight
+// at once).  The 64 steps are then resolved optimistically: every remaining step is assumed to
+// cut exactly M after the previous cut (true whenever a chunk starts there, as on text); a
+// ballot finds the first step where that fails, the steps before it are written in parallel,
+// and that one step is resolved from its window.
 constexpr int kWalkWords = 10;
 __global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict__ cbits,
                                                      const uint32_t* __restrict__ m_ptr, uint32_t nblock_max,
@@ -310,8 +312,6 @@ __global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ qpos, uint32_t* __restrict__ res,
                                                      uint32_t max_cuts) {
   __shared__ uint32_t win[64][kWalkWords];
-  __shared__ int64_t s_sh;
-  __shared__ int done_sh;
   const uint32_t lane = threadIdx.x;
   const uint32_t m = *m_ptr;
   if (m == 0) {
@@ -323,8 +323,9 @@ __global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict_
     return;
   }
   const uint32_t wend = (m + 31) >> 5;
-  uint32_t last_start = 0;
-  if (lane == 0) {
+  const int64_t M = (int64_t)nblock_max;
+  uint32_t last_start = 0;  // every lane computes it (uniform)
+  {
     uint32_t w = (m - 1) >> 5;
     for (;;) {
       uint32_t bits = cbits[w] & (w == ((m - 1) >> 5) ? (0xffffffffu >> (31 - ((m - 1) & 31))) : ~0u);
@@ -333,17 +334,13 @@ __global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict_
       --w;
     }
   }
-  const uint32_t last_len1 = *last_len1_ptr;
-  uint32_t b = 0;  // cuts so far (lane 0)
-  if (lane == 0) {
-    s_sh = -(int64_t)fill_in;  // output position of the open block's start
-    done_sh = 0;
-  }
-  __syncthreads();
-  while (!done_sh) {
-    const int64_t s = s_sh;
+  const bool tail_rule = final_region && *last_len1_ptr;
+  int64_t s = -(int64_t)fill_in;  // output position of the open block's start (uniform)
+  uint32_t b = 0;                 // cuts so far (uniform)
+  int done = 0;                   // 1: walk ended, 2: more than max_cuts
+  while (!done) {
     {
-      const int64_t lo = s + (int64_t)(lane + 1) * nblock_max;
+      const int64_t lo = s + (int64_t)(lane + 1) * M;
       const int64_t w0 = lo < 0 ? 0 : (lo >> 5);
 #pragma unroll
       for (int k = 0; k < kWalkWords; k++) {
@@ -352,20 +349,38 @@ __global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict_
       }
     }
     __syncthreads();
-    if (lane == 0) {
-      int64_t cur = s;
-      int done = 0;
-      for (uint32_t j = 0; j < 64 && !done; j++) {
-        const int64_t lo = s + (int64_t)(j + 1) * nblock_max;
+    int64_t cur = s;
+    uint32_t j = 0;
+    while (j < 64 && !done) {
+      bool ok = false;
+      int64_t tl = 0;
+      if (lane >= j) {
+        tl = cur + (int64_t)(lane - j + 1) * M;
+        if (tl >= 0 && tl < (int64_t)m && !(tail_rule && tl == (int64_t)last_start) && b + (lane - j) < max_cuts) {
+          const int64_t lo = s + (int64_t)(lane + 1) * M;
+          const int64_t k = (tl >> 5) - (lo < 0 ? 0 : (lo >> 5));
+          ok = k >= 0 && k < kWalkWords && ((win[lane][k] >> (tl & 31)) & 1u);
+        }
+      }
+      const uint64_t bad = __ballot(!ok) & (~0ull << j);
+      const uint32_t f = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+      if (ok && lane < f) qpos[b + (lane - j)] = (uint32_t)tl;
+      if (f > j) {
+        cur += (int64_t)(f - j) * M;
+        b += f - j;
+        j = f;
+      }
+      if (f < 64) {  // step f from its window
+        const int64_t lo = s + (int64_t)(f + 1) * M;
         const int64_t w0 = lo < 0 ? 0 : (lo >> 5);
-        const int64_t t = cur + (int64_t)nblock_max;
+        const int64_t t = cur + M;
         uint32_t p = m;
         if (t <= 0) {
           p = 0;
         } else if (t < (int64_t)m) {
           const int64_t tw = t >> 5;
           for (int64_t w = tw; w < w0 + kWalkWords && w < (int64_t)wend; w++) {
-            uint32_t bits = win[j][w - w0];
+            uint32_t bits = win[f][w - w0];
             if (w == tw) bits &= ~0u << (t & 31);
             if (bits) {
               p = (uint32_t)((w << 5) + __builtin_ctz(bits));
@@ -374,29 +389,31 @@ __global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict_
           }
           if (p > m) p = m;
         }
-        if (p < m && final_region && p == last_start && last_len1) p = m;
+        if (p < m && tail_rule && p == last_start) p = m;
         if (p >= m) {
           done = 1;
-          break;
-        }
-        if (b >= max_cuts) {  // cannot happen with the host's sizing; keep the walk finite
-          res[0] = 0xffffffffu;
+        } else if (b >= max_cuts) {  // cannot happen with the host's sizing; keeps the walk finite
           done = 2;
-          break;
+        } else {
+          if (lane == 0) qpos[b] = p;
+          b++;
+          cur = p;
+          j = f + 1;
         }
-        qpos[b++] = p;
-        cur = p;
-      }
-      s_sh = cur;
-      done_sh = done;
-      if (done == 1) {
-        qpos[b] = last_start;
-        res[0] = b;
-        res[1] = last_start;
-        res[2] = (uint32_t)((int64_t)last_start - cur);
       }
     }
-    __syncthreads();
+    __syncthreads();  // the next round overwrites win
+    s = cur;
+  }
+  if (lane == 0) {
+    if (done == 2) {
+      res[0] = 0xffffffffu;
+    } else {
+      qpos[b] = last_start;
+      res[0] = b;
+      res[1] = last_start;
+      res[2] = (uint32_t)((int64_t)last_start - s);
+    }
   }
 }
 
