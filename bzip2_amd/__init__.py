@@ -44,6 +44,7 @@ ENGINE_EXPORTS = [
     "bzg_stream_init", "bzg_compress_device", "bzg_compress_host", "bzg_compress_host_stream",
     "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_stage_code_lengths", "bzg_last_stats",
     "bzg_release", "bzg_device_ok", "bzg_periodic_origptr", "bzg_seg_map", "bzg_seg_walk",
+    "bzg_find_magics",
 ]
 
 
@@ -117,6 +118,7 @@ def lib() -> ctypes.CDLL:
         L.bzg_last_stats.argtypes = [ctypes.POINTER(bzg_stats)]
         L.bzg_periodic_origptr.argtypes = [vp, ctypes.c_int32]
         L.bzg_seg_map.argtypes = [vp, u64, ci, vp]
+        L.bzg_find_magics.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64), vp]
         L.bzg_seg_walk.argtypes = [u32, ci, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.bzg_periodic_origptr.restype = ctypes.c_int32
         _lib = L
@@ -237,6 +239,23 @@ def seg_walk(fill_in: int, final_region: bool, max_cuts: int):
     if rc != BZ_OK:
         raise BzError(rc, "bzg_seg_walk")
     return [int(cuts[i]) for i in range(nc.value)], lc.value, lf.value
+
+
+def find_magics(d_ptr: int, n: int, stream_ptr: int = 0):
+    """bzg_find_magics on a device buffer: sorted [(bit_offset, kind)], kind 0 = block header,
+    1 = end of stream."""
+    L = lib()
+    cnt = ctypes.c_uint64(0)
+    cap = n // 4096 + 1024
+    while True:
+        out = (ctypes.c_uint64 * cap)()
+        rc = L.bzg_find_magics(ctypes.c_void_p(d_ptr), n, out, cap, ctypes.byref(cnt), ctypes.c_void_p(stream_ptr or None))
+        if rc == BZ_OUTBUFF_FULL:
+            cap = cnt.value
+            continue
+        if rc != BZ_OK:
+            raise BzError(rc, "bzg_find_magics")
+        return [(out[i] >> 1, out[i] & 1) for i in range(cnt.value)]
 
 
 def code_lengths(tables, max_len: int = 17):

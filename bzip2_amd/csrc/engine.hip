@@ -337,6 +337,23 @@ int bzg_seg_walk(uint32_t fill_in, int final_region, uint64_t* cuts, uint32_t ma
   }
 }
 
+int bzg_find_magics(const void* d_in, uint64_t n, uint64_t* out, uint64_t cap, uint64_t* count, void* stream) {
+  if ((n && !d_in) || !count || (cap && !out)) return BZ_PARAM_ERROR;
+  Engine& e = engine();
+  std::lock_guard<std::mutex> g(e.mu);
+  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
+  try {
+    std::vector<uint64_t> f;
+    find_magics_stage((const uint8_t*)d_in, n, f, s);
+    *count = f.size();
+    for (uint64_t i = 0; i < f.size() && i < cap; i++) out[i] = f[i];
+    return f.size() > cap ? BZ_OUTBUFF_FULL : BZ_OK;
+  } catch (const HipFailure& f) {
+    return f.err == hipErrorOutOfMemory ? BZ_MEM_ERROR : BZ_CONFIG_ERROR;
+  }
+}
+
 int bzg_compress_host(const void* src, uint64_t n, int level, void* dst, uint64_t dst_cap, uint64_t* dst_len) {
   if (level < 1 || level > 9 || (n && !src) || !dst || !dst_len) return BZ_PARAM_ERROR;
   Engine& e = engine();

@@ -61,6 +61,9 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
                 bool tail_merge, Rle1Result& res, hipStream_t st);
 // in-use maps, nInUse and primitive periods of res.nblocks blocks given res.blk / res.boff
 void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st);
+// bit offsets of the block-header / end-of-stream magics of a .bz2 stream, sorted, as
+// 2 * offset + kind (magic.hip)
+uint64_t find_magics_stage(const uint8_t* d_in, uint64_t n, std::vector<uint64_t>& found, hipStream_t st);
 // one region of a sharded stream: RLE1 chunk map, then block cuts for a given
 // open-block fill at the region start (input offsets relative to the region)
 void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t st);

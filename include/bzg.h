@@ -101,6 +101,14 @@ typedef struct {
 int bzg_seg_map(const void *d_in, uint64_t n, int level, void *stream);
 int bzg_seg_walk(uint32_t fill_in, int final_region, uint64_t *cuts, uint32_t max_cuts, uint32_t *ncuts,
                  uint64_t *last_chunk, uint32_t *last_fill);
+/* Block boundaries of an existing .bz2 stream (the prerequisite of
+ * block-parallel decoding): every bit offset of d_in[0, n) (device memory) where a block-header
+ * magic 0x314159265359 or the end-of-stream magic 0x177245385090 starts, ascending, as
+ * out[i] = 2 * bit_offset + kind (kind 0 = block header, 1 = end of stream); bit 0 is the MSB of
+ * byte 0.  Magics that occur by chance inside block data are reported too, as the reference's
+ * scan reports them.  *count = the number found; BZ_OUTBUFF_FULL when it exceeds cap (out holds
+ * the first cap).  Replaces the bit-serial scan of bzip2recover.c:360-395. */
+int bzg_find_magics(const void *d_in, uint64_t n, uint64_t *out, uint64_t cap, uint64_t *count, void *stream);
 void bzg_last_stats(bzg_stats *out);
 
 /* Release the engine's device memory (it is re-acquired on the next call). */
