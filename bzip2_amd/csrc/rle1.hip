@@ -231,71 +231,12 @@ __global__ void __launch_bounds__(kT) k_chunk_inpos(const uint8_t* __restrict__ 
   }
 }
 
-// Smallest chunk start >= t (t < m), or m if none.
-__device__ uint32_t next_chunk_start(const uint32_t* __restrict__ cbits, uint32_t t, uint32_t m) {
-  uint32_t w = t >> 5;
-  uint32_t bits = cbits[w] & (~0u << (t & 31));
-  const uint32_t wend = (m + 31) >> 5;
-  while (bits == 0) {
-    if (++w >= wend) return m;
-    bits = cbits[w];
-  }
-  uint32_t p = (w << 5) + (uint32_t)__builtin_ctz(bits);
-  return p < m ? p : m;
-}
-
-// Sequential block-cut chain (one thread).  See file header for the rule.
-__global__ void k_segment(const uint32_t* __restrict__ cbits,
-                          const uint32_t* __restrict__ m_ptr, uint64_t n, uint32_t nblock_max,
-                          int final_batch, int tail_merge, const uint32_t* __restrict__ last_len1_ptr,
-                          uint32_t* __restrict__ boff, uint32_t* __restrict__ nblocks, uint32_t max_blocks) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const uint32_t m = *m_ptr;
-  const uint32_t last_chunk_len1 = *last_len1_ptr;
-  uint32_t b = 0, s = 0;
-  if (m == 0) {
-    boff[0] = 0;
-    *nblocks = 0;
-    return;
-  }
-  // out position of the last chunk start (for the tail-merge rule)
-  uint32_t last_start = 0;
-  {
-    uint32_t w = (m - 1) >> 5;
-    for (;;) {
-      uint32_t bits = cbits[w] & (w == ((m - 1) >> 5) ? (0xffffffffu >> (31 - ((m - 1) & 31))) : ~0u);
-      if (bits) { last_start = (w << 5) + 31 - (uint32_t)__builtin_clz(bits); break; }
-      if (w == 0) break;
-      --w;
-    }
-  }
-  for (;;) {
-    boff[b] = s;
-    uint32_t t = s + nblock_max;
-    uint32_t p = (t < m) ? next_chunk_start(cbits, t, m) : m;
-    if (p < m && final_batch && tail_merge && p == last_start && last_chunk_len1) p = m;
-    if (p >= m) {
-      if (final_batch) {
-        boff[b + 1] = m;
-        *nblocks = b + 1;
-      } else {
-        *nblocks = b;  // block b is incomplete; it restarts the next batch at its input start
-      }
-      return;
-    }
-    if (b + 1 >= max_blocks) {  // cannot happen with the host's sizing; keep the grid finite
-      *nblocks = 0xffffffffu;
-      return;
-    }
-    ++b;
-    s = p;
-  }
-}
-
-// Cut walk over one region of a sharded stream (one wave).  The region starts
+// Block-cut walk (one wave), for a batch (fill 0) and for one region of a sharded stream
+// (SURVEY.md 8e).  The region starts
 // at a chunk start of the stream with `fill_in` RLE1 bytes (< nblock_max) already in the open
 // block, so the first cut is the first chunk start at output position >= nblock_max - fill_in;
-// after that the rule is k_segment's.  qpos gets the cut positions followed by the region's last
+// after that, a cut is the first chunk start >= the previous cut + nblock_max (file header);
+// with final_region, the last chunk never starts a block when it is 1 byte (FINISH).  qpos gets the cut positions followed by the region's last
 // chunk start; res = {ncuts, last chunk start, open-block fill at that chunk start}.
 // A chunk is at most 5 RLE1 bytes, so the cut after s lies in [s + M, s + M + 4] (M =
 // nblock_max) and the (j+1)-th cut after s in [s + (j+1) M, s + (j+1) M + 4 j + 4].  Each round,
@@ -414,6 +355,26 @@ __global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict_
       res[1] = last_start;
       res[2] = (uint32_t)((int64_t)last_start - s);
     }
+  }
+}
+
+// Block offsets from k_segment_fill's cuts (written at boff + 1): boff[0] = 0; a final batch
+// closes its last block at m, a non-final one leaves the block after the last cut open (it
+// restarts the next batch from its input start).
+__global__ void k_segment_finish(const uint32_t* __restrict__ m_ptr, const uint32_t* __restrict__ res,
+                                 int final_batch, uint32_t* __restrict__ boff, uint32_t* __restrict__ nblocks) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t m = *m_ptr, ncut = res[0];
+  boff[0] = 0;
+  if (ncut == 0xffffffffu) {
+    *nblocks = 0xffffffffu;
+  } else if (m == 0) {
+    *nblocks = 0;
+  } else if (final_batch) {
+    boff[ncut + 1] = m;
+    *nblocks = ncut + 1;
+  } else {
+    *nblocks = ncut;
   }
 }
 
@@ -656,8 +617,11 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, blk, cbits, mtot + 8);
   HIP_OK(hipGetLastError());
 
-  k_segment<<<1, 64, 0, st>>>(cbits, mtot, n, nblock_max, final_batch ? 1 : 0, tail_merge ? 1 : 0,
-                              mtot + 8, boff, nbl, max_blocks);
+  // the cut walk of k_segment_fill from fill 0 (cuts into boff[1..]), then boff/nblocks
+  k_segment_fill<<<1, 64, 0, st>>>(cbits, mtot, nblock_max, 0u, (final_batch && tail_merge) ? 1 : 0, mtot + 8,
+                                   boff + 1, mtot + 12, max_blocks - 1);
+  HIP_OK(hipGetLastError());
+  k_segment_finish<<<1, 64, 0, st>>>(mtot, mtot + 12, final_batch ? 1 : 0, boff, nbl);
   HIP_OK(hipGetLastError());
   uint32_t hv[2];
   HIP_OK(hipMemcpyAsync(hv, mtot, 4, hipMemcpyDeviceToHost, st));
