@@ -93,11 +93,14 @@ def main():
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
 
+    last_stream = [None]
+
     def step():
         if mode == "stream":
             from bzip2_amd import shard
 
             res = shard.compress_sharded(d_in, rank * a.bytes, world * a.bytes, a.level)
+            last_stream[0] = res
             return res.numel() / world if res is not None else 0  # per-rank share of the one stream
         nb, cons, _ = B.compress_device(d_in.data_ptr(), len(data), a.level, d_out.data_ptr(), cap, stream_ptr=sp)
         return nb
@@ -165,6 +168,21 @@ def main():
                if mode == "stream" and os.environ.get("BZG_SHARD_TIMING") == "1" else {}),
             "gen_s": round(gen_s, 1),
         }
+        if mode == "stream" and last_stream[0] is not None:
+            # structure of the gathered stream (outside the timed region): every block header and
+            # the end-of-stream magic where the bit count puts them (bzg_find_magics)
+            from bzip2_amd import shard
+
+            fs = last_stream[0].to("cuda")  # on the host under the gloo rehearsal
+            found = B.find_magics(fs.data_ptr(), fs.numel())
+            heads = [o for o, k in found if k == 0]
+            meta = shard.last_meta
+            result["stream_check"] = {
+                "bytes": fs.numel(), "blocks": meta["blocks"], "block_magics_found": len(heads),
+                "first_block_at_bit_32": bool(heads) and heads[0] == 32,
+                "eos_at_payload_end": (meta["bits"], 1) in found,
+                "ok": bool(heads) and heads[0] == 32 and len(heads) >= meta["blocks"] and (meta["bits"], 1) in found,
+            }
         pmc = pmc_traffic(a)
         if pmc is not None:
             rl = result["roofline"]

@@ -45,6 +45,7 @@ PIECE_MAX = 1_500_000_000  # bzg_seg_map region limit (32-bit RLE1 offsets)
 # (seconds since the call started) in last_timing
 _TIMING = os.environ.get("BZG_SHARD_TIMING") == "1"
 last_timing: dict = {}
+last_meta: dict = {}  # rank 0: blocks and payload bits of the last stream
 
 
 def _mark(name: str, t0: float, dev) -> None:
@@ -337,6 +338,7 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
         k = meta0[r][1] % 32
         combined = (((combined << k) | (combined >> (32 - k))) & 0xFFFFFFFF) if k else combined
         combined ^= meta0[r][2]
+    last_meta.update(blocks=sum(m[1] for m in meta0), bits=total_bits, combined_crc=combined)
     tr = ((TRAILER_MAGIC << 32) | combined).to_bytes(10, "big")
     tt = shift_bits(torch.tensor(list(tr), dtype=torch.uint8, device=cdev), 80, total_bits % 8)
     base = total_bits // 8
