@@ -1,6 +1,7 @@
 """Multi-rank logic of bench.py on CPU (gloo, world size 2): every rank reports the slowest
-rank's time, the job value counts every rank's bytes, and ranks compress distinct objects
-(independent streams shard with no data-path collective)."""
+rank's time, the job value counts every rank's bytes, and ranks hold distinct inputs (their
+shards of one stream in `--mode stream`, the default for N > 1, or independent streams in
+`--mode independent`).  The sharded stream itself is tested in test_shard.py."""
 import os
 import socket
 
