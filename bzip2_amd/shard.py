@@ -132,15 +132,21 @@ class GpuBackend:
         return out[:(nbits + 7) // 8], nbits, st.blocks_done, st.combined_crc
 
 
-def chain_piece(be, d: torch.Tensor, s: int, n_total: int, msg, final: bool, mapped: bool = False):
+def piece_info(d: torch.Tensor):
+    """(first byte, last byte, first run start) of a piece: device reads done before the chain."""
+    return int(d[0]), int(d[-1]), first_run_start(d)
+
+
+def chain_piece(be, d: torch.Tensor, s: int, n_total: int, msg, final: bool, mapped: bool = False, info=None):
     """Step 1 for one piece d = input[s, s + len(d)).  msg: None at the stream start, else the open
-    chunk (t, fill, byte, covered) with t + covered == s.  Returns (global cuts, message on)."""
+    chunk (t, fill, byte, covered) with t + covered == s.  `mapped`: bzg_seg_map already ran on
+    d[first run start:]; `info`: piece_info(d) if already known.  Returns (global cuts, message
+    on)."""
     mx = nblock_max(be.level)
     e = s + d.numel()
     last_pos = n_total - 1
     cuts: list = []
-    d0 = int(d[0])
-    p = first_run_start(d)
+    d0, dlast, p = info if info is not None else piece_info(d)
     if msg is None:
         t, fill = s, 0
     else:
@@ -165,7 +171,7 @@ def chain_piece(be, d: torch.Tensor, s: int, n_total: int, msg, final: bool, map
     cuts += [x + c for c in rc]
     if final:
         return cuts, None
-    return cuts, (x + lc, lf, int(d[-1]), e - (x + lc))
+    return cuts, (x + lc, lf, dlast, e - (x + lc))
 
 
 def shift_bits(buf: torch.Tensor, nbits: int, sh: int) -> torch.Tensor:
@@ -219,7 +225,8 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
 
     # 1. block cuts, rank after rank
     pieces = [(o, min(PIECE_MAX, n - o)) for o in range(0, n, PIECE_MAX)]
-    first_p = first_run_start(d[:pieces[0][1]])
+    info0 = piece_info(d[:pieces[0][1]])  # device reads off the chain's critical path
+    first_p = info0[2]
     if first_p < pieces[0][1]:
         be.map_region(d[first_p:pieces[0][1]])  # off the critical path
     _mark("map", t0, d.device)
@@ -233,7 +240,8 @@ def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int
     last_rank = rank == world - 1
     for i, (o, ln) in enumerate(pieces):
         c, msg = chain_piece(be, d[o:o + ln], shard_start + o, n_total, msg,
-                             final=last_rank and i == len(pieces) - 1, mapped=(i == 0 and first_p < ln))
+                             final=last_rank and i == len(pieces) - 1, mapped=(i == 0 and first_p < ln),
+                             info=info0 if i == 0 else None)
         cuts += c
     if not last_rank:
         m = torch.tensor(list(msg) + [1], dtype=torch.int64, device=cdev)
