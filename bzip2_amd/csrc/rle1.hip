@@ -157,7 +157,8 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
       else bits1 |= 1u << (pos & 31);
     }
     const uint32_t lp = pos - t0 + lofs;
-    if (b.r <= 3) {
+    if (out == nullptr) {  // chunk map only (seg_map_stage): no block bytes
+    } else if (b.r <= 3) {
       ob[lp] = v[k];
       if (b.r == 3 && b.last) ob[lp + 1] = 0;
     } else if (b.last) {
