@@ -44,6 +44,8 @@ def parse():
                    help="threads for the multi-core reference baseline (the box's CPU share is 16)")
     p.add_argument("--cpu-mt-sample", type=int, default=640_000_000, help="bytes for the multi-core timing")
     p.add_argument("--no-h2h", action="store_true", help="skip the host-to-host region (profiling runs)")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the secondary lines (BASELINE configs 4 and 5, long-repeat text)")
     p.add_argument("--mode", choices=["stream", "independent"], default=None,
                    help="stream: the ranks' inputs are consecutive shards of ONE .bz2 stream, gathered on "
                         "rank 0 (bzip2_amd/shard.py; default for N > 1); independent: one stream per rank")
@@ -195,10 +197,99 @@ def main():
             result["host_to_host"] = host_to_host(data, a, cap)
         if not a.no_cpu:
             result.update(cpu_and_parity(data, a, d_in))
+        if not a.no_extra and mode == "independent":
+            result["secondary"] = extra_configs(a, d_in, d_out, cap, no_cpu=a.no_cpu)
         print(json.dumps(result), flush=True)
     if dist:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+
+
+def time_device(d, n, level, d_out, cap, steps, warmup=1):
+    """ms per call of bzg_compress_device on n device-resident bytes, and the last stats."""
+    sp = torch.cuda.current_stream().cuda_stream
+    for _ in range(warmup):
+        nb, _, _ = B.compress_device(d.data_ptr(), n, level, d_out.data_ptr(), cap, stream_ptr=sp)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        nb, _, _ = B.compress_device(d.data_ptr(), n, level, d_out.data_ptr(), cap, stream_ptr=sp)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) * 1e3 / steps, nb, B.last_stats()
+
+
+def line_for(name, n, level, ms, nb, st, workload):
+    rho = st["rle_bytes"] / n
+    c = nb / n
+    b_alg = 1.0 + 25.0 * rho + 3.0 * c
+    return {"workload": workload, "bytes": n, "level": level, "value": round(n / ms / 1e3, 2), "unit": "MB/s",
+            "ms_per_step": round(ms, 3), "bz2_ratio": round(c, 5), "rle1_rho": round(rho, 5),
+            "blocks": st["nblocks"], "sort_unsorted": st["sort_unsorted"],
+            "stages_ms": {k: round(st[k + "_ms"], 3) for k in ("rle1", "bwt", "mtf", "code")},
+            "roofline": {"bound": "hbm", "b_alg_per_byte": round(b_alg, 4),
+                         "achieved": round(n * b_alg / (ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(n * b_alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 5)}}
+
+
+def sample_parity(d, n, level, no_cpu):
+    """GPU stream of d[:n] against the reference's (pinned child, timed) -> dict."""
+    from tests import oracles as O
+
+    cap = B.bound(n)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    nb, _, _ = B.compress_device(d.data_ptr(), n, level, out.data_ptr(), cap)
+    torch.cuda.synchronize()
+    got = out[:nb].cpu().numpy().tobytes()
+    if no_cpu or not O.has_ref():
+        return {"sample_bytes": n, "bit_exact": got == O.orc_compress(d[:n].cpu().numpy().tobytes(), level),
+                "against": "port"}
+    cpu_s, ref = run_cpu_child(d[:n].cpu().numpy().tobytes(), level, sorted(os.sched_getaffinity(0))[:1])
+    return {"sample_bytes": n, "bit_exact": got == ref, "against": "reference",
+            "cpu_baseline": {"value": round(n / cpu_s / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "reference",
+                             "sample": f"first {n} B, BZ2_bzBuffToBuffCompress -{level}, pinned child"}}
+
+
+def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False):
+    """Secondary lines (never `value`): BASELINE configs 4 and 5 at full size (4 GiB, device
+    resident; bzg_compress_device cuts them into 1.5e9-byte batches), and enwik-like text with
+    long duplicated passages (the sorter's deep-group path)."""
+    res = {}
+    n4 = 1 << 32
+    level = 9
+    d = torch.full((n4,), 0x61, dtype=torch.uint8, device="cuda")
+    cap = B.bound(n4)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    ms, nb, st = time_device(d, n4, level, out, cap, steps=2)
+    res["single_byte_4gib"] = line_for("single", n4, level, ms, nb, st, "4 GiB of byte 0x61 (BASELINE config 4), -9")
+    res["single_byte_4gib"]["parity"] = sample_parity(d, 256 << 20, level, no_cpu)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0005)
+    d = torch.randint(0, 256, (n4,), dtype=torch.uint8, device="cuda", generator=g)
+    ms, nb, st = time_device(d, n4, level, out, cap, steps=2)
+    res["random_4gib"] = line_for("random", n4, level, ms, nb, st,
+                                  "4 GiB of seeded PRNG bytes (torch Philox, seed 0x5EED0005; BASELINE config 5), -9")
+    res["random_4gib"]["parity"] = sample_parity(d, 32 << 20, level, no_cpu)
+    del d, out
+    torch.cuda.empty_cache()
+    # long repeats: 25% of the text overwritten by copies of earlier passages (2 kB .. 200 kB)
+    n = d_text.numel()
+    dr = d_text.clone()
+    rng = __import__("random").Random(0x5EED0009)
+    covered = 0
+    while covered < n // 4:
+        ln = rng.randint(2_000, 200_000)
+        dst = rng.randrange(1_000_000, n - ln)
+        src = rng.randrange(0, dst - ln) if rng.random() < 0.5 else max(0, dst - rng.randint(ln, 4 * ln))
+        dr[dst:dst + ln] = dr[src:src + ln].clone()
+        covered += ln
+    ms, nb, st = time_device(dr, n, level, d_out_text, cap_text, steps=2)
+    res["long_repeat_text"] = line_for("long_repeat", n, level, ms, nb, st,
+                                       f"the main workload with 25% overwritten by copies of earlier passages "
+                                       f"(2-200 kB), {n} B, -9")
+    res["long_repeat_text"]["parity"] = sample_parity(dr, 64 << 20, level, no_cpu)
+    del dr
+    torch.cuda.empty_cache()
+    return res
 
 
 def pmc_traffic(a):
@@ -246,17 +337,77 @@ def host_to_host(data, a, cap):
             "api": "BZ2_bzBuffToBuffCompress, pageable host buffers (H2D + kernels + D2H)"}
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_child(path: str, level: int, cpus: str) -> None:
+    """`bench.py --cpu-child`: the reference CPU path (oracle/_ref, the reference's own
+    blocksort.c/compress.c build) timed in a child process pinned to `cpus` (no GPU touched).
+    One cpu: one BZ2_bzBuffToBuffCompress of the whole sample, output kept beside it for the
+    parity check; k cpus: k threads, each compressing a contiguous 1/k of the sample as its own
+    stream."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from tests import oracles as O
+
+    cs = sorted(int(c) for c in cpus.split(","))
+    os.sched_setaffinity(0, cs)
+    data = open(path, "rb").read()
+    nt = len(cs)
+    if nt == 1:
+        t = time.perf_counter()
+        out = O.ref_compress(data, level)
+        dt = time.perf_counter() - t
+        open(path + ".ref", "wb").write(out)
+    else:
+        step = -(-len(data) // nt)
+        shards = [data[i:i + step] for i in range(0, len(data), step)]
+        with ThreadPoolExecutor(nt) as ex:
+            t = time.perf_counter()
+            list(ex.map(lambda x: O.ref_compress(x, level), shards))
+            dt = time.perf_counter() - t
+    print(json.dumps({"seconds": dt, "bytes": len(data), "threads": nt}), flush=True)
+
+
+def run_cpu_child(sample: bytes, level: int, cpus) -> tuple:
+    """Times the reference on `sample` in a pinned child (taskset when present); returns
+    (seconds, reference output or None)."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        path = os.path.join(td, "sample.bin")
+        open(path, "wb").write(sample)
+        cl = ",".join(str(c) for c in cpus)
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", path, str(level), cl]
+        if shutil.which("taskset"):
+            cmd = ["taskset", "-c", cl] + cmd
+        r = subprocess.run(cmd, capture_output=True, text=True, check=True, timeout=600)
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        ref = open(path + ".ref", "rb").read() if os.path.exists(path + ".ref") else None
+        return res["seconds"], ref
+
+
 def cpu_and_parity(data, a, d_in):
-    """Reference CPU timing on a bounded sample, and GPU-vs-reference bytes on it."""
+    """Reference CPU timing on a bounded sample (pinned child processes), and GPU-vs-reference
+    bytes on the 1-core sample."""
     from tests import oracles as O
 
     n = min(a.cpu_sample, len(data))
     sample = data[:n]
+    allowed = sorted(os.sched_getaffinity(0))
+    model = cpu_model()
     if O.has_ref():
         kind = "reference"
-        t = time.perf_counter()
-        ref_out = O.ref_compress(sample, a.level)
-        cpu_s = time.perf_counter() - t
+        cpu_s, ref_out = run_cpu_child(sample, a.level, allowed[:1])
     else:
         kind = "port"
         t = time.perf_counter()
@@ -264,21 +415,13 @@ def cpu_and_parity(data, a, d_in):
         cpu_s = time.perf_counter() - t
     mt = None
     if O.has_ref() and a.cpu_threads > 1:
-        # N threads, each compressing a contiguous 1/N shard as its own stream
-        # (aggregate MB/s only; no single stream comes out of it)
-        from concurrent.futures import ThreadPoolExecutor
-
-        nt = min(a.cpu_threads, os.cpu_count() or 1)
+        cs = allowed[:a.cpu_threads]
         m = min(a.cpu_mt_sample, len(data))
-        step = -(-m // nt)
-        shards = [data[i:min(m, i + step)] for i in range(0, m, step)]
-        with ThreadPoolExecutor(nt) as ex:
-            t = time.perf_counter()
-            list(ex.map(lambda x: O.ref_compress(x, a.level), shards))
-            mt_s = time.perf_counter() - t
-        mt = {"value": round(m / mt_s / 1e6, 3), "unit": "MB/s", "cores": nt, "kind": "reference",
-              "sample": f"first {m} B of the rank-0 input as {len(shards)} independent "
-                        f"BZ2_bzBuffToBuffCompress -{a.level} streams on {nt} threads, {mt_s:.1f} s"}
+        mt_s, _ = run_cpu_child(data[:m], a.level, cs)
+        mt = {"value": round(m / mt_s / 1e6, 3), "unit": "MB/s", "cores": len(cs), "kind": "reference",
+              "cpu_model": model, "pinned_cpus": f"{cs[0]}..{cs[-1]}" if len(cs) > 1 else str(cs[0]),
+              "sample": f"first {m} B of the rank-0 input as {len(cs)} independent "
+                        f"BZ2_bzBuffToBuffCompress -{a.level} streams on {len(cs)} pinned threads, {mt_s:.1f} s"}
     cap = B.bound(n)
     d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
     nb, _, _ = B.compress_device(d_in.data_ptr(), n, a.level, d_out.data_ptr(), cap)
@@ -286,8 +429,9 @@ def cpu_and_parity(data, a, d_in):
     gpu_sample = d_out[:nb].cpu().numpy().tobytes()
     return {
         "cpu_baseline": {"value": round(n / cpu_s / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": kind,
+                         "cpu_model": model, "pinned_cpus": str(allowed[0]),
                          "sample": f"first {n} B of the rank-0 input, BZ2_bzBuffToBuffCompress -{a.level}, "
-                                   f"{cpu_s:.1f} s"},
+                                   f"{cpu_s:.1f} s in a child process pinned to one core (taskset)"},
         "parity": {"sample_bytes": n, "bit_exact": gpu_sample == ref_out, "against": kind,
                    "out_bytes": len(ref_out)},
         **({"cpu_baseline_multicore": mt} if mt else {}),
@@ -295,4 +439,7 @@ def cpu_and_parity(data, a, d_in):
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 5 and sys.argv[1] == "--cpu-child":
+        cpu_child(sys.argv[2], int(sys.argv[3]), sys.argv[4])
+    else:
+        main()

@@ -657,7 +657,7 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
   HIP_OK(hipStreamSynchronize(st));
   const uint64_t end_bits = total_bits + (final_batch ? 80 : 0);
   const uint64_t need = ceil_div64(end_bits, 32) * 4 + 8;
-  if (need > out_cap) throw HipFailure(hipErrorOutOfMemory);
+  if (need > out_cap) throw OutBuffFull{};
   HIP_OK(hipMemsetAsync(out, 0, need, st));
   if (carry.carry_bits) HIP_OK(hipMemcpyAsync(out, &carry.carry_byte, 1, hipMemcpyHostToDevice, st));
   if (nb > 0) {

@@ -24,6 +24,9 @@ struct HipFailure {
   hipError_t err;
   explicit HipFailure(hipError_t e) : err(e) {}
 };
+// The caller's output buffer cannot hold the coded stream (BZ_OUTBUFF_FULL); distinct from a
+// device allocation failure (HipFailure(hipErrorOutOfMemory) -> BZ_MEM_ERROR).
+struct OutBuffFull {};
 
 // Format constants (reference bzlib_private.h:139-152).
 constexpr int kMaxAlpha = 258;

@@ -1,8 +1,13 @@
 // engine.hip -- orchestration of the device pipeline and the bzg_* C ABI (include/bzg.h).
 //
-// One engine per process (device 0 of the process's visible devices; one process per GPU),
-// guarded by a mutex: bzlib streams from several host threads are serialised on it.
+// Engines are pooled per device (EnginePool): every call leases one engine of the calling
+// thread's current device, so host threads compress concurrently on separate HIP streams and
+// device buffers.
 #include <algorithm>
+#include <condition_variable>
+#include <memory>
+#include <new>
+#include <vector>
 #include <cstring>
 #include <exception>
 #include <mutex>
@@ -41,9 +46,16 @@ void* Workspace::get(const std::string& name, size_t bytes) {
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipFree(b.p));
     total_ -= b.bytes;
+    b.p = nullptr;
+    b.bytes = 0;
   }
   const size_t grow = bytes + bytes / 8;  // headroom so small growth does not realloc
-  HIP_OK(hipMalloc(&b.p, grow));
+  void* p = nullptr;
+  if (hipMalloc(&p, grow) != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky error of the failed allocation
+    throw HipFailure(hipErrorOutOfMemory);
+  }
+  b.p = p;
   b.bytes = grow;
   total_ += grow;
   return b.p;
@@ -84,34 +96,25 @@ const uint32_t* Workspace::xpow2_table() {
 }
 
 // ---------------------------------------------------------------- engine
+// An engine is one device's HIP streams, events and workspaces.  It serves one call at a
+// time.  Engines live in a pool keyed by device (EnginePool below): a call leases a free
+// engine of its device, creates one while the device has fewer than the cap, or waits.
+// Streams of several host threads therefore run on separate HIP streams and device buffers,
+// as the reference keeps all compression state per bz_stream (bzlib.c:144-207).
 struct Engine {
-  std::mutex mu;
-  bool init = false;
-  bool ok = false;
+  int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // the second half of a batch's block sort
   Workspace ws;
   Workspace ws2;
-  Workspace wseg;  // the mapped region of a sharded stream (bzg_seg_map / bzg_seg_walk)
-  const uint8_t* seg_in = nullptr;
-  uint64_t seg_n = 0;
-  int seg_level = 0;
-  hipStream_t seg_stream = nullptr;
   hipEvent_t ev[6];
   hipEvent_t ev2;
-  bzg_stats last{};
 
-  bool ensure() {
-    if (init) return ok;
-    init = true;
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ok = false;
-    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return ok = false;
-    if (hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking) != hipSuccess) return ok = false;
-    for (auto& e : ev)
-      if (hipEventCreate(&e) != hipSuccess) return ok = false;
-    if (hipEventCreateWithFlags(&ev2, hipEventDisableTiming) != hipSuccess) return ok = false;
-    return ok = true;
+  explicit Engine(int dev) : device(dev) {
+    HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    for (auto& e : ev) HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipEventCreateWithFlags(&ev2, hipEventDisableTiming));
   }
 
   // The block sort of a batch.  Large batches are sorted as two halves of their blocks on two
@@ -138,8 +141,7 @@ struct Engine {
     HIP_OK(hipStreamWaitEvent(stream2, ev2, 0));
     SortStats sb;
     std::exception_ptr err;
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
+    const int dev = device;
     std::thread th([&] {
       try {
         HIP_OK(hipSetDevice(dev));  // the current device is per host thread
@@ -165,9 +167,9 @@ struct Engine {
     }
   }
 
-  // Compress one batch.  Throws HipFailure on device errors.
+  // Compress one batch.  Throws HipFailure on device errors, OutBuffFull when out_cap is short.
   void batch(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
-             uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s) {
+             uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
     const int level = st->level;
     const bool end_seg = flags & BZG_FLAG_END_SEGMENT;
     const bool tail_merge = (flags & BZG_FLAG_TAIL_MERGE) && end_seg;
@@ -230,16 +232,200 @@ struct Engine {
     last.sort_iterations = (uint32_t)ss.iterations;
     last.rle_bytes = nb ? hboff[nb] : 0;
     last.sort_unsorted = ss.unsorted_elems;
+    if (nb) {
+      std::vector<uint32_t> nm(nb);
+      HIP_OK(hipMemcpy(nm.data(), m.nmtf, 4 * nb, hipMemcpyDeviceToHost));
+      for (uint32_t x : nm) last.mtf_symbols += x;
+    }
   }
-};
 
-static Engine& engine() {
-  static Engine* e = new Engine();  // never destroyed: device teardown order at exit is unsafe
-  return *e;
-}
+  // bzg_compress_device's contract: inputs larger than kMaxBatch are cut into batches; the
+  // non-final batches emit complete blocks and the rest is resubmitted.
+  void compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
+                uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last);
+};
 
 // Largest batch handled in one pass: keeps every block/slot offset in 32 bits.
 static constexpr uint64_t kMaxBatch = 1500ull * 1000 * 1000;
+
+void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
+                      uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
+  uint64_t done_in = 0, done_out = 0;
+  bzg_stats acc{};
+  for (;;) {
+    const uint64_t left = n - done_in;
+    const bool last_piece = left <= kMaxBatch;
+    const uint64_t take = last_piece ? left : kMaxBatch;
+    const unsigned f = last_piece ? flags : 0u;
+    uint64_t ob = 0, cons = 0;
+    bzg_stats one{};
+    batch(d_in + done_in, take, f, st, d_out + done_out, out_cap - done_out, &ob, &cons, s, one);
+    acc.rle1_ms += one.rle1_ms;
+    acc.bwt_ms += one.bwt_ms;
+    acc.mtf_ms += one.mtf_ms;
+    acc.code_ms += one.code_ms;
+    acc.total_ms += one.total_ms;
+    acc.nblocks += one.nblocks;
+    acc.sort_iterations = std::max(acc.sort_iterations, one.sort_iterations);
+    acc.rle_bytes += one.rle_bytes;
+    acc.sort_unsorted += one.sort_unsorted;
+    acc.mtf_symbols += one.mtf_symbols;
+    done_in += cons;
+    done_out += ob;
+    if (last_piece) break;
+    if (cons == 0) throw HipFailure(hipErrorUnknown);  // cannot happen: kMaxBatch holds many blocks
+  }
+  *out_bytes = done_out;
+  *consumed = done_in;
+  last = acc;
+}
+
+// Makes `dev` the calling thread's current device for the scope and restores the caller's.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) HIP_OK(hipSetDevice(dev));
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
+class EnginePool {
+ public:
+  static constexpr int kMaxDev = 64;
+
+  int devices() {
+    std::call_once(once_, [&] {
+      int n = 0;
+      ndev_ = hipGetDeviceCount(&n) == hipSuccess ? std::min(n, kMaxDev) : 0;
+      const char* c = getenv("BZG_ENGINES_PER_DEVICE");
+      cap_ = c ? std::max(1, atoi(c)) : 4;
+    });
+    return ndev_;
+  }
+
+  // A free engine of device `dev` (created on demand up to the per-device cap, else waits).
+  Engine* acquire(int dev) {
+    if (dev < 0 || dev >= devices()) throw HipFailure(hipErrorInvalidDevice);
+    std::unique_lock<std::mutex> g(mu_);
+    for (;;) {
+      if (!idle_[dev].empty()) {
+        Engine* e = idle_[dev].back();
+        idle_[dev].pop_back();
+        return e;
+      }
+      if (count_[dev] < cap_) {
+        count_[dev]++;
+        g.unlock();
+        try {
+          DeviceScope ds(dev);
+          return new Engine(dev);  // never destroyed: device teardown order at exit is unsafe
+        } catch (...) {
+          g.lock();
+          count_[dev]--;
+          cv_.notify_one();
+          throw;
+        }
+      }
+      cv_.wait(g);
+    }
+  }
+
+  void release(Engine* e) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      idle_[e->device].push_back(e);
+    }
+    cv_.notify_one();
+  }
+
+  // Frees the device memory of every idle engine (engines in use keep theirs).
+  void release_idle_memory() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int d = 0; d < ndev_; d++)
+      for (Engine* e : idle_[d]) {
+        DeviceScope ds(e->device);
+        (void)hipStreamSynchronize(e->stream);
+        (void)hipStreamSynchronize(e->stream2);
+        e->ws.release_all();
+        e->ws2.release_all();
+      }
+  }
+
+ private:
+  std::once_flag once_;
+  int ndev_ = 0, cap_ = 4;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Engine*> idle_[kMaxDev];
+  int count_[kMaxDev] = {};
+};
+
+static EnginePool& pool() {
+  static EnginePool* p = new EnginePool();
+  return *p;
+}
+
+// One engine of a device for the duration of a call, with the device made current.
+struct Lease {
+  Engine* e;
+  DeviceScope ds;
+  explicit Lease(int dev) : e(pool().acquire(dev)), ds(dev) {}
+  ~Lease() { pool().release(e); }
+  Engine* operator->() const { return e; }
+  Lease(const Lease&) = delete;
+  Lease& operator=(const Lease&) = delete;
+};
+
+// The calling thread's current HIP device (device pointers handed to the engine live there).
+static int current_device() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) d = 0;
+  return d;
+}
+
+// Device errors to bzlib codes: device allocation failure -> BZ_MEM_ERROR, a short caller
+// output buffer -> BZ_OUTBUFF_FULL, anything else on the device -> BZ_CONFIG_ERROR.
+template <typename F>
+static int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const OutBuffFull&) {
+    return BZ_OUTBUFF_FULL;
+  } catch (const HipFailure& x) {
+    return x.err == hipErrorOutOfMemory ? BZ_MEM_ERROR : BZ_CONFIG_ERROR;
+  } catch (const ResolverFailure&) {
+    return BZ_CONFIG_ERROR;
+  } catch (const std::bad_alloc&) {
+    return BZ_MEM_ERROR;
+  }
+}
+
+static std::mutex g_stats_mu;
+static bzg_stats g_last{};
+static void publish_stats(const bzg_stats& s) {
+  std::lock_guard<std::mutex> g(g_stats_mu);
+  g_last = s;
+}
+
+// State of the sharded-stream chunk map (bzg_seg_map / bzg_seg_walk): one per process, since a
+// rank drives one region at a time; kept on its own engine so the walk finds the map.
+struct SegState {
+  std::mutex mu;
+  Engine* e = nullptr;
+  const uint8_t* in = nullptr;
+  uint64_t n = 0;
+  int level = 0;
+  hipStream_t stream = nullptr;
+};
+static SegState& seg_state() {
+  static SegState* s = new SegState();
+  return *s;
+}
 
 }  // namespace bzg
 
@@ -255,188 +441,137 @@ void bzg_stream_init(bzg_stream_state* st, int level) {
 uint64_t bzg_bound(uint64_t n) { return n + n / 50 + (n / 100000 + 2) * 64 + 4096; }
 
 int bzg_device_ok(void) {
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  return e.ensure() ? 1 : 0;
+  if (pool().devices() <= 0) return 0;
+  const int rc = guarded([&] {
+    Lease L(current_device());
+    return BZ_OK;
+  });
+  return rc == BZ_OK ? 1 : 0;
 }
 
 int bzg_compress_device(const void* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, void* d_out,
                         uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, void* stream) {
   if (!st || !out_bytes || !consumed || st->level < 1 || st->level > 9 || (n && !d_in) || !d_out)
     return BZ_PARAM_ERROR;
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ensure()) return BZ_CONFIG_ERROR;
-  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
-  try {
-    // Split oversized inputs: non-final passes emit complete blocks, the rest is resubmitted.
-    uint64_t done_in = 0, done_out = 0;
-    uint8_t* out = (uint8_t*)d_out;
-    for (;;) {
-      const uint64_t left = n - done_in;
-      const bool last_piece = left <= kMaxBatch;
-      const uint64_t take = last_piece ? left : kMaxBatch;
-      const unsigned f = last_piece ? flags : 0u;
-      uint64_t ob = 0, cons = 0;
-      e.batch((const uint8_t*)d_in + done_in, take, f, st, out + done_out, out_cap - done_out, &ob, &cons, s);
-      done_in += cons;
-      done_out += ob;
-      if (last_piece) break;
-      if (cons == 0) return BZ_MEM_ERROR;  // cannot happen: kMaxBatch holds many blocks
-    }
-    *out_bytes = done_out;
-    *consumed = done_in;
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  return guarded([&] {
+    Lease L(current_device());
+    hipStream_t s = stream ? (hipStream_t)stream : L->stream;
+    bzg_stats last{};
+    L->compress((const uint8_t*)d_in, n, flags, st, (uint8_t*)d_out, out_cap, out_bytes, consumed, s, last);
+    publish_stats(last);
     return BZ_OK;
-  } catch (const HipFailure& f) {
-    return f.err == hipErrorOutOfMemory ? BZ_OUTBUFF_FULL : BZ_CONFIG_ERROR;
-  } catch (const ResolverFailure&) {
-    return BZ_CONFIG_ERROR;
-  }
+  });
 }
 
 int bzg_seg_map(const void* d_in, uint64_t n, int level, void* stream) {
   if (level < 1 || level > 9 || (n && !d_in) || n > kMaxBatch) return BZ_PARAM_ERROR;
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ensure()) return BZ_CONFIG_ERROR;
-  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
-  try {
-    seg_map_stage(e.wseg, (const uint8_t*)d_in, n, s);
-    e.seg_in = (const uint8_t*)d_in;
-    e.seg_n = n;
-    e.seg_level = level;
-    e.seg_stream = s;
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  SegState& S = seg_state();
+  std::lock_guard<std::mutex> g(S.mu);
+  S.in = nullptr;
+  return guarded([&] {
+    const int dev = current_device();
+    if (!S.e || S.e->device != dev) {
+      DeviceScope ds(dev);
+      S.e = new Engine(dev);  // one per process, never destroyed
+    }
+    DeviceScope ds(dev);
+    hipStream_t s = stream ? (hipStream_t)stream : S.e->stream;
+    seg_map_stage(S.e->ws, (const uint8_t*)d_in, n, s);
+    S.in = (const uint8_t*)d_in;
+    S.n = n;
+    S.level = level;
+    S.stream = s;
     return BZ_OK;
-  } catch (const HipFailure& f) {
-    e.seg_in = nullptr;
-    return f.err == hipErrorOutOfMemory ? BZ_MEM_ERROR : BZ_CONFIG_ERROR;
-  }
+  });
 }
 
 int bzg_seg_walk(uint32_t fill_in, int final_region, uint64_t* cuts, uint32_t max_cuts, uint32_t* ncuts,
                  uint64_t* last_chunk, uint32_t* last_fill) {
   if (!ncuts || !last_chunk || !last_fill || (max_cuts && !cuts)) return BZ_PARAM_ERROR;
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ensure()) return BZ_CONFIG_ERROR;
-  if (!e.seg_in && e.seg_n) return BZ_PARAM_ERROR;  // no successful bzg_seg_map
-  if (fill_in >= 100000u * (uint32_t)e.seg_level - 19u) return BZ_PARAM_ERROR;
-  try {
+  SegState& S = seg_state();
+  std::lock_guard<std::mutex> g(S.mu);
+  if (!S.e || (!S.in && S.n)) return BZ_PARAM_ERROR;  // no successful bzg_seg_map
+  if (fill_in >= 100000u * (uint32_t)S.level - 19u) return BZ_PARAM_ERROR;
+  return guarded([&] {
+    DeviceScope ds(S.e->device);
     std::vector<uint64_t> c;
     uint64_t lc = 0;
     uint32_t lf = fill_in;
-    seg_walk_stage(e.wseg, e.seg_in, e.seg_n, e.seg_level, fill_in, final_region != 0, c, lc, lf, e.seg_stream);
+    seg_walk_stage(S.e->ws, S.in, S.n, S.level, fill_in, final_region != 0, c, lc, lf, S.stream);
     if (c.size() > max_cuts) return BZ_OUTBUFF_FULL;
     for (size_t i = 0; i < c.size(); i++) cuts[i] = c[i];
     *ncuts = (uint32_t)c.size();
     *last_chunk = lc;
     *last_fill = lf;
     return BZ_OK;
-  } catch (const HipFailure& f) {
-    return f.err == hipErrorOutOfMemory ? BZ_MEM_ERROR : BZ_CONFIG_ERROR;
-  }
+  });
 }
 
 int bzg_find_magics(const void* d_in, uint64_t n, uint64_t* out, uint64_t cap, uint64_t* count, void* stream) {
   if ((n && !d_in) || !count || (cap && !out)) return BZ_PARAM_ERROR;
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ensure()) return BZ_CONFIG_ERROR;
-  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
-  try {
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  return guarded([&] {
+    Lease L(current_device());
+    hipStream_t s = stream ? (hipStream_t)stream : L->stream;
     std::vector<uint64_t> f;
     find_magics_stage((const uint8_t*)d_in, n, f, s);
     *count = f.size();
     for (uint64_t i = 0; i < f.size() && i < cap; i++) out[i] = f[i];
     return f.size() > cap ? BZ_OUTBUFF_FULL : BZ_OK;
-  } catch (const HipFailure& f) {
-    return f.err == hipErrorOutOfMemory ? BZ_MEM_ERROR : BZ_CONFIG_ERROR;
-  }
+  });
+}
+
+// Host buffers through one leased engine: staging, compression and copy-out all happen under
+// the lease, so concurrent callers never share staging buffers.
+static int host_call(const void* src, uint64_t n, unsigned flags, bzg_stream_state* st, void* dst, uint64_t dst_cap,
+                     uint64_t* dst_len, uint64_t* consumed) {
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  return guarded([&] {
+    Lease L(current_device());
+    const uint64_t cap = bzg_bound(n);
+    uint8_t* din = L->ws.u8("host_in", n + 16);
+    uint8_t* dout = L->ws.u8("host_out", cap);
+    if (n) HIP_OK(hipMemcpyAsync(din, src, n, hipMemcpyHostToDevice, L->stream));
+    uint64_t ob = 0, cons = 0;
+    bzg_stats last{};
+    L->compress(din, n, flags, st, dout, cap, &ob, &cons, L->stream, last);
+    publish_stats(last);
+    if (ob > dst_cap) return BZ_OUTBUFF_FULL;
+    if (ob) HIP_OK(hipMemcpyAsync(dst, dout, ob, hipMemcpyDeviceToHost, L->stream));
+    HIP_OK(hipStreamSynchronize(L->stream));
+    *dst_len = ob;
+    if (consumed) *consumed = cons;
+    return BZ_OK;
+  });
 }
 
 int bzg_compress_host(const void* src, uint64_t n, int level, void* dst, uint64_t dst_cap, uint64_t* dst_len) {
   if (level < 1 || level > 9 || (n && !src) || !dst || !dst_len) return BZ_PARAM_ERROR;
-  Engine& e = engine();
-  {
-    std::lock_guard<std::mutex> g(e.mu);
-    if (!e.ensure()) return BZ_CONFIG_ERROR;
-  }
-  const uint64_t cap = bzg_bound(n);
-  uint8_t *din = nullptr, *dout = nullptr;
-  int rc = BZ_OK;
-  try {
-    std::lock_guard<std::mutex> g(e.mu);
-    din = e.ws.u8("host_in", n + 16);
-    dout = e.ws.u8("host_out", cap);
-    if (n) HIP_OK(hipMemcpyAsync(din, src, n, hipMemcpyHostToDevice, e.stream));
-  } catch (const HipFailure&) {
-    return BZ_MEM_ERROR;
-  }
   bzg_stream_state st;
   bzg_stream_init(&st, level);
-  uint64_t ob = 0, cons = 0;
   const unsigned flags = BZG_FLAG_END_SEGMENT | BZG_FLAG_TRAILER | (n ? BZG_FLAG_TAIL_MERGE : 0u);
-  rc = bzg_compress_device(din, n, flags, &st, dout, cap, &ob, &cons, nullptr);
-  if (rc != BZ_OK) return rc;
-  if (ob > dst_cap) return BZ_OUTBUFF_FULL;
-  try {
-    std::lock_guard<std::mutex> g(e.mu);
-    HIP_OK(hipMemcpyAsync(dst, dout, ob, hipMemcpyDeviceToHost, e.stream));
-    HIP_OK(hipStreamSynchronize(e.stream));
-  } catch (const HipFailure&) {
-    return BZ_CONFIG_ERROR;
-  }
-  *dst_len = ob;
-  return BZ_OK;
+  return host_call(src, n, flags, &st, dst, dst_cap, dst_len, nullptr);
 }
 
 int bzg_compress_host_stream(const void* src, uint64_t n, unsigned flags, bzg_stream_state* st, void* dst,
                              uint64_t dst_cap, uint64_t* dst_len, uint64_t* consumed) {
-  if (!st || !dst || !dst_len || !consumed || (n && !src)) return BZ_PARAM_ERROR;
-  Engine& e = engine();
-  {
-    std::lock_guard<std::mutex> g(e.mu);
-    if (!e.ensure()) return BZ_CONFIG_ERROR;
-  }
-  const uint64_t cap = bzg_bound(n);
-  uint8_t *din = nullptr, *dout = nullptr;
-  try {
-    std::lock_guard<std::mutex> g(e.mu);
-    din = e.ws.u8("host_in", n + 16);
-    dout = e.ws.u8("host_out", cap);
-    if (n) HIP_OK(hipMemcpyAsync(din, src, n, hipMemcpyHostToDevice, e.stream));
-  } catch (const HipFailure&) {
-    return BZ_MEM_ERROR;
-  }
-  uint64_t ob = 0;
-  int rc = bzg_compress_device(din, n, flags, st, dout, cap, &ob, consumed, nullptr);
-  if (rc != BZ_OK) return rc;
-  if (ob > dst_cap) return BZ_OUTBUFF_FULL;
-  try {
-    std::lock_guard<std::mutex> g(e.mu);
-    if (ob) HIP_OK(hipMemcpyAsync(dst, dout, ob, hipMemcpyDeviceToHost, e.stream));
-    HIP_OK(hipStreamSynchronize(e.stream));
-  } catch (const HipFailure&) {
-    return BZ_CONFIG_ERROR;
-  }
-  *dst_len = ob;
-  return BZ_OK;
+  if (!st || !dst || !dst_len || !consumed || (n && !src) || st->level < 1 || st->level > 9) return BZ_PARAM_ERROR;
+  // the stream state advances only if the call succeeds
+  bzg_stream_state work = *st;
+  const int rc = host_call(src, n, flags, &work, dst, dst_cap, dst_len, consumed);
+  if (rc == BZ_OK) *st = work;
+  return rc;
 }
 
 void bzg_last_stats(bzg_stats* out) {
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (out) *out = e.last;
+  std::lock_guard<std::mutex> g(g_stats_mu);
+  if (out) *out = g_last;
 }
 
 void bzg_release(void) {
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (e.init && e.ok) {
-    (void)hipDeviceSynchronize();
-    e.ws.release_all();
-    e.ws2.release_all();
-  }
+  if (pool().devices() > 0) pool().release_idle_memory();
 }
 
 int32_t bzg_periodic_origptr(const uint8_t* block, int32_t n) {
@@ -451,9 +586,15 @@ int32_t bzg_periodic_origptr(const uint8_t* block, int32_t n) {
 // ---------------------------------------------------------------- per-stage entry points
 int bzg_stage_rle1(const void* src, uint64_t n, int level, int tail_merge, uint8_t* blocks, uint64_t blocks_cap,
                    uint32_t* offsets, uint32_t* crcs, uint32_t* nblocks, uint32_t max_blocks) {
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  Lease* lp = nullptr;
+  try {
+    lp = new Lease(current_device());
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+  std::unique_ptr<Lease> lease(lp);
+  Engine& e = *lease->e;
   try {
     uint8_t* din = e.ws.u8("stage_in", n + 16);
     HIP_OK(hipMemcpy(din, src, n, hipMemcpyHostToDevice));
@@ -477,9 +618,15 @@ int bzg_stage_rle1(const void* src, uint64_t n, int level, int tail_merge, uint8
 }
 
 int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, uint8_t* bwt_out, int32_t* origptr) {
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  Lease* lp = nullptr;
+  try {
+    lp = new Lease(current_device());
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+  std::unique_ptr<Lease> lease(lp);
+  Engine& e = *lease->e;
   try {
     if (nb == 0) return BZ_OK;
     const uint32_t total = offsets[nb];
@@ -511,9 +658,15 @@ int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, u
 
 int bzg_stage_mtf(const uint8_t* bwt_in, const uint32_t* offsets, uint32_t nb, uint16_t* mtfv, uint32_t* mtf_offsets,
                   uint32_t* nmtf, uint32_t* freq) {
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  Lease* lp = nullptr;
+  try {
+    lp = new Lease(current_device());
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+  std::unique_ptr<Lease> lease(lp);
+  Engine& e = *lease->e;
   try {
     if (nb == 0) return BZ_OK;
     const uint32_t total = offsets[nb];
@@ -539,9 +692,15 @@ int bzg_stage_mtf(const uint8_t* bwt_in, const uint32_t* offsets, uint32_t nb, u
 
 int bzg_stage_code_lengths(const uint32_t* freq, const int32_t* alpha, uint32_t ntables, int max_len,
                            uint8_t* lens) {
-  Engine& e = engine();
-  std::lock_guard<std::mutex> g(e.mu);
-  if (!e.ensure()) return BZ_CONFIG_ERROR;
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  Lease* lp = nullptr;
+  try {
+    lp = new Lease(current_device());
+  } catch (const HipFailure&) {
+    return BZ_CONFIG_ERROR;
+  }
+  std::unique_ptr<Lease> lease(lp);
+  Engine& e = *lease->e;
   if (ntables == 0) return BZ_OK;
   for (uint32_t t = 0; t < ntables; t++)
     if (alpha[t] < 2 || alpha[t] > kMaxAlpha) return BZ_PARAM_ERROR;

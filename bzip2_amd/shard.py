@@ -113,7 +113,9 @@ class GpuBackend:
         seg_map(d.data_ptr(), d.numel(), self.level, self.sp)
 
     def walk(self, fill: int, final: bool, n: int):
-        return seg_walk(fill, final, n // nblock_max(self.level) + 8)
+        # RLE1 can grow the input by 5/4 (runs of exactly 4 bytes): size the cut list as the
+        # device sizes its own (rle1.hip seg_walk_stage: n + n/4 + 64 RLE1 bytes at most)
+        return seg_walk(fill, final, (n + n // 4 + 64) // nblock_max(self.level) + 8)
 
     def compress(self, d: torch.Tensor, header: bool, final: bool):
         """Returns (bytes tensor holding `nbits` bits MSB-first, nbits, blocks, combined CRC)."""
@@ -162,7 +164,9 @@ def chain_piece(be, d: torch.Tensor, s: int, n_total: int, msg, final: bool, map
     if p == d.numel():
         return cuts, (None if final else (t, fill, d0, e - t))
     fill += chunk_size(x - t)  # the run ends at x, a run start
-    if fill >= mx and x != last_pos:
+    if x == last_pos:  # the stream's last byte never opens a block: it joins the open one
+        return cuts, None
+    if fill >= mx:
         cuts.append(x)
         fill = 0
     if not mapped:

@@ -29,6 +29,7 @@ def chunks(d: np.ndarray):
 
 def walk(starts, lens, sizes, level, fill, final):
     mx = nblock_max(level)
+    assert fill < mx, "bzg_seg_walk rejects fill_in >= nblockMAX (BZ_PARAM_ERROR)"
     outpos = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     s = -fill
     cuts = []

@@ -281,6 +281,76 @@ def test_streaming_chunked_and_flush():
     assert B.stream_compress(chunks, 2, flush_after=(0, 1)) == O.ref_stream_compress(chunks, 2, flush_after=(0, 1))
 
 
+def test_concurrent_streams_four_threads():
+    """Four host threads at once, each running BZ2_bzBuffToBuffCompress and chunked
+    BZ2_bzCompress loops on its own inputs (the reference is reentrant per bz_stream,
+    bzlib.c:144-207): every output equals the reference's for that thread's input."""
+    import threading
+
+    if not O.has_ref():
+        pytest.skip("needs oracle/_ref for the streaming reference")
+    inputs = [datagen.text(1_300_000 + 97_000 * t, 300 + t) + datagen.random_bytes(50_000 * t, t) for t in range(4)]
+    want_b2b = [O.ref_compress(x, 1 + t) for t, x in enumerate(inputs)]
+    chunks = [[x[i:i + 70_000] for i in range(0, len(x), 70_000)] for x in inputs]
+    want_stream = [O.ref_stream_compress(c, 9 - t) for t, c in enumerate(chunks)]
+    errors = []
+
+    def work(t):
+        try:
+            for _ in range(3):
+                got = B.buff_to_buff_compress(inputs[t], 1 + t)
+                assert got == want_b2b[t], f"thread {t}: BuffToBuff differs"
+                got = B.stream_compress(chunks[t], 9 - t)
+                assert got == want_stream[t], f"thread {t}: bzCompress differs"
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+
+
+def test_device_oom_is_mem_error():
+    """A device allocation failure is BZ_MEM_ERROR (not BZ_OUTBUFF_FULL, which would tell a
+    BuffToBuff caller to retry with a bigger destination); a short destination is
+    BZ_OUTBUFF_FULL."""
+    data = datagen.text(300_000, 5)
+    L = B.lib()
+    dst = ctypes.create_string_buffer(100)
+    dl = ctypes.c_uint(100)
+    assert L.BZ2_bzBuffToBuffCompress(dst, ctypes.byref(dl), data, len(data), 9, 0, 30) == B.BZ_OUTBUFF_FULL
+    torch = pytest.importorskip("torch")
+    n = 1_200_000_000
+    d_in = torch.zeros(n, dtype=torch.uint8, device="cuda")  # real buffers: kernels that run read in bounds
+    cap = B.bound(n)
+    d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    B.lib().bzg_release()
+    hog = []
+    try:
+        for chunk in (8 << 30, 1 << 30, 128 << 20):  # leave the engine no room for its workspace
+            while True:
+                try:
+                    hog.append(torch.empty(chunk, dtype=torch.uint8, device="cuda"))
+                except RuntimeError:
+                    break
+        st = B.bzg_stream_state()
+        L.bzg_stream_init(ctypes.byref(st), 9)
+        ob, cons = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        rc = L.bzg_compress_device(ctypes.c_void_p(d_in.data_ptr()), n, B.BZG_FLAG_END_SEGMENT | B.BZG_FLAG_TRAILER,
+                                   ctypes.byref(st), ctypes.c_void_p(d_out.data_ptr()), cap, ctypes.byref(ob),
+                                   ctypes.byref(cons), None)
+        assert rc == B.BZ_MEM_ERROR, rc
+    finally:
+        del hog
+        torch.cuda.empty_cache()
+    del d_in, d_out
+    torch.cuda.empty_cache()
+    assert B.buff_to_buff_compress(data, 9) == expected(data, 9)  # the engine recovers
+
+
 def test_round_trip_large_properties():
     """At bench-like sizes: decode(encode(x)) == x with the system bzip2 decoder, and the
     stream equals the reference's on a 4 MB slice."""

@@ -29,6 +29,10 @@ def _inputs():
         "text_run_text": txt[:90_000] + b"q" * 150_000 + txt[90_000:200_000],
         "one_byte": b"z" * 900_000,
         "tail_len1": b"k" * 25_000 * 4 + b"x",  # ends with a 1-byte chunk
+        # the first run ends at the stream's last byte with the open block already full there
+        # (-1: 19996 chunks of 255 fill 99,980 bytes; the last chunk brings it past nblockMAX)
+        "full_then_last": b"a" * (255 * 19996 + 4) + b"b",
+        "runs_of_4": b"aaaabbbb" * 60_000,  # RLE1 grows the input by 5/4
     }
 
 
