@@ -1,4 +1,5 @@
-// bzlib_api.cpp -- the 24 exports of libbz2.def (reference libbz2.def:4-27) over the GPU engine.
+// bzlib_api.cpp -- the core stream exports of libbz2.def (reference libbz2.def:4-27) over the
+// GPU engine; the stdio / zlib-style exports are in bzfile.cpp, decompression in decode.cpp.
 //
 // Compression keeps the reference's streaming contract (bzlib.c:144-474): BZ_RUN returns
 // BZ_RUN_OK iff progress was made, BZ_FLUSH / BZ_FINISH move the stream into FLUSHING /
@@ -203,415 +204,5 @@ int BZ2_bzBuffToBuffCompress(char* dest, unsigned int* destLen, char* source, un
 }
 
 const char* BZ2_bzlibVersion(void) { return "1.0.6x, 16-Aug-2018"; }
-
-// ------------------------------------------------------------------ FILE* layer
-// Restates bzlib.c:943-1301 over the stream functions above and the decoder.
-struct BzFile {
-  FILE* handle;
-  char buf[BZ_MAX_UNUSED];
-  int bufN;
-  bool writing;
-  bz_stream strm;
-  int lastErr;
-  bool initialisedOk;
-};
-
-#define BZ_SETERR(eee)                    \
-  do {                                    \
-    if (bzerror != nullptr) *bzerror = eee; \
-    if (bzf != nullptr) bzf->lastErr = eee; \
-  } while (0)
-
-static bool my_feof(FILE* f) {
-  int c = fgetc(f);
-  if (c == EOF) return true;
-  ungetc(c, f);
-  return false;
-}
-
-BZFILE* BZ2_bzWriteOpen(int* bzerror, FILE* f, int blockSize100k, int verbosity, int workFactor) {
-  BzFile* bzf = nullptr;
-  BZ_SETERR(BZ_OK);
-  if (f == nullptr || blockSize100k < 1 || blockSize100k > 9 || workFactor < 0 || workFactor > 250 ||
-      verbosity < 0 || verbosity > 4) {
-    BZ_SETERR(BZ_PARAM_ERROR);
-    return nullptr;
-  }
-  if (ferror(f)) {
-    BZ_SETERR(BZ_IO_ERROR);
-    return nullptr;
-  }
-  bzf = (BzFile*)std::malloc(sizeof(BzFile));
-  if (bzf == nullptr) {
-    BZ_SETERR(BZ_MEM_ERROR);
-    return nullptr;
-  }
-  BZ_SETERR(BZ_OK);
-  bzf->initialisedOk = false;
-  bzf->bufN = 0;
-  bzf->handle = f;
-  bzf->writing = true;
-  bzf->strm.bzalloc = nullptr;
-  bzf->strm.bzfree = nullptr;
-  bzf->strm.opaque = nullptr;
-  if (workFactor == 0) workFactor = 30;
-  int ret = BZ2_bzCompressInit(&bzf->strm, blockSize100k, verbosity, workFactor);
-  if (ret != BZ_OK) {
-    BZ_SETERR(ret);
-    std::free(bzf);
-    return nullptr;
-  }
-  bzf->strm.avail_in = 0;
-  bzf->initialisedOk = true;
-  return bzf;
-}
-
-void BZ2_bzWrite(int* bzerror, BZFILE* b, void* buf, int len) {
-  BzFile* bzf = (BzFile*)b;
-  BZ_SETERR(BZ_OK);
-  if (bzf == nullptr || buf == nullptr || len < 0) {
-    BZ_SETERR(BZ_PARAM_ERROR);
-    return;
-  }
-  if (!bzf->writing) {
-    BZ_SETERR(BZ_SEQUENCE_ERROR);
-    return;
-  }
-  if (ferror(bzf->handle)) {
-    BZ_SETERR(BZ_IO_ERROR);
-    return;
-  }
-  if (len == 0) {
-    BZ_SETERR(BZ_OK);
-    return;
-  }
-  bzf->strm.avail_in = (unsigned)len;
-  bzf->strm.next_in = (char*)buf;
-  for (;;) {
-    bzf->strm.avail_out = BZ_MAX_UNUSED;
-    bzf->strm.next_out = bzf->buf;
-    int ret = BZ2_bzCompress(&bzf->strm, BZ_RUN);
-    if (ret != BZ_RUN_OK) {
-      BZ_SETERR(ret);
-      return;
-    }
-    if (bzf->strm.avail_out < BZ_MAX_UNUSED) {
-      size_t n = BZ_MAX_UNUSED - bzf->strm.avail_out;
-      size_t n2 = fwrite(bzf->buf, 1, n, bzf->handle);
-      if (n != n2 || ferror(bzf->handle)) {
-        BZ_SETERR(BZ_IO_ERROR);
-        return;
-      }
-    }
-    if (bzf->strm.avail_in == 0) {
-      BZ_SETERR(BZ_OK);
-      return;
-    }
-  }
-}
-
-void BZ2_bzWriteClose64(int* bzerror, BZFILE* b, int abandon, unsigned int* nbytes_in_lo32,
-                        unsigned int* nbytes_in_hi32, unsigned int* nbytes_out_lo32, unsigned int* nbytes_out_hi32) {
-  BzFile* bzf = (BzFile*)b;
-  if (bzf == nullptr) {
-    BZ_SETERR(BZ_OK);
-    return;
-  }
-  if (!bzf->writing) {
-    BZ_SETERR(BZ_SEQUENCE_ERROR);
-    return;
-  }
-  if (ferror(bzf->handle)) {
-    BZ_SETERR(BZ_IO_ERROR);
-    return;
-  }
-  if (nbytes_in_lo32) *nbytes_in_lo32 = 0;
-  if (nbytes_in_hi32) *nbytes_in_hi32 = 0;
-  if (nbytes_out_lo32) *nbytes_out_lo32 = 0;
-  if (nbytes_out_hi32) *nbytes_out_hi32 = 0;
-  if (!abandon && bzf->lastErr == BZ_OK) {
-    for (;;) {
-      bzf->strm.avail_out = BZ_MAX_UNUSED;
-      bzf->strm.next_out = bzf->buf;
-      int ret = BZ2_bzCompress(&bzf->strm, BZ_FINISH);
-      if (ret != BZ_FINISH_OK && ret != BZ_STREAM_END) {
-        BZ_SETERR(ret);
-        return;
-      }
-      if (bzf->strm.avail_out < BZ_MAX_UNUSED) {
-        size_t n = BZ_MAX_UNUSED - bzf->strm.avail_out;
-        size_t n2 = fwrite(bzf->buf, 1, n, bzf->handle);
-        if (n != n2 || ferror(bzf->handle)) {
-          BZ_SETERR(BZ_IO_ERROR);
-          return;
-        }
-      }
-      if (ret == BZ_STREAM_END) break;
-    }
-  }
-  if (!abandon && !ferror(bzf->handle)) {
-    fflush(bzf->handle);
-    if (ferror(bzf->handle)) {
-      BZ_SETERR(BZ_IO_ERROR);
-      return;
-    }
-  }
-  if (nbytes_in_lo32) *nbytes_in_lo32 = bzf->strm.total_in_lo32;
-  if (nbytes_in_hi32) *nbytes_in_hi32 = bzf->strm.total_in_hi32;
-  if (nbytes_out_lo32) *nbytes_out_lo32 = bzf->strm.total_out_lo32;
-  if (nbytes_out_hi32) *nbytes_out_hi32 = bzf->strm.total_out_hi32;
-  BZ_SETERR(BZ_OK);
-  BZ2_bzCompressEnd(&bzf->strm);
-  std::free(bzf);
-}
-
-void BZ2_bzWriteClose(int* bzerror, BZFILE* b, int abandon, unsigned int* nbytes_in, unsigned int* nbytes_out) {
-  BZ2_bzWriteClose64(bzerror, b, abandon, nbytes_in, nullptr, nbytes_out, nullptr);
-}
-
-BZFILE* BZ2_bzReadOpen(int* bzerror, FILE* f, int verbosity, int small, void* unused, int nUnused) {
-  BzFile* bzf = nullptr;
-  BZ_SETERR(BZ_OK);
-  if (f == nullptr || (small != 0 && small != 1) || verbosity < 0 || verbosity > 4 ||
-      (unused == nullptr && nUnused != 0) || (unused != nullptr && (nUnused < 0 || nUnused > BZ_MAX_UNUSED))) {
-    BZ_SETERR(BZ_PARAM_ERROR);
-    return nullptr;
-  }
-  if (ferror(f)) {
-    BZ_SETERR(BZ_IO_ERROR);
-    return nullptr;
-  }
-  bzf = (BzFile*)std::malloc(sizeof(BzFile));
-  if (bzf == nullptr) {
-    BZ_SETERR(BZ_MEM_ERROR);
-    return nullptr;
-  }
-  BZ_SETERR(BZ_OK);
-  bzf->initialisedOk = false;
-  bzf->handle = f;
-  bzf->bufN = 0;
-  bzf->writing = false;
-  bzf->strm.bzalloc = nullptr;
-  bzf->strm.bzfree = nullptr;
-  bzf->strm.opaque = nullptr;
-  while (nUnused > 0) {
-    bzf->buf[bzf->bufN++] = *(char*)unused;
-    unused = (char*)unused + 1;
-    nUnused--;
-  }
-  int ret = BZ2_bzDecompressInit(&bzf->strm, verbosity, small);
-  if (ret != BZ_OK) {
-    BZ_SETERR(ret);
-    std::free(bzf);
-    return nullptr;
-  }
-  bzf->strm.avail_in = (unsigned)bzf->bufN;
-  bzf->strm.next_in = bzf->buf;
-  bzf->initialisedOk = true;
-  return bzf;
-}
-
-void BZ2_bzReadClose(int* bzerror, BZFILE* b) {
-  BzFile* bzf = (BzFile*)b;
-  BZ_SETERR(BZ_OK);
-  if (bzf == nullptr) {
-    BZ_SETERR(BZ_OK);
-    return;
-  }
-  if (bzf->writing) {
-    BZ_SETERR(BZ_SEQUENCE_ERROR);
-    return;
-  }
-  if (bzf->initialisedOk) (void)BZ2_bzDecompressEnd(&bzf->strm);
-  std::free(bzf);
-}
-
-int BZ2_bzRead(int* bzerror, BZFILE* b, void* buf, int len) {
-  BzFile* bzf = (BzFile*)b;
-  BZ_SETERR(BZ_OK);
-  if (bzf == nullptr || buf == nullptr || len < 0) {
-    BZ_SETERR(BZ_PARAM_ERROR);
-    return 0;
-  }
-  if (bzf->writing) {
-    BZ_SETERR(BZ_SEQUENCE_ERROR);
-    return 0;
-  }
-  if (len == 0) {
-    BZ_SETERR(BZ_OK);
-    return 0;
-  }
-  bzf->strm.avail_out = (unsigned)len;
-  bzf->strm.next_out = (char*)buf;
-  for (;;) {
-    if (ferror(bzf->handle)) {
-      BZ_SETERR(BZ_IO_ERROR);
-      return 0;
-    }
-    if (bzf->strm.avail_in == 0 && !my_feof(bzf->handle)) {
-      size_t n = fread(bzf->buf, 1, BZ_MAX_UNUSED, bzf->handle);
-      if (ferror(bzf->handle)) {
-        BZ_SETERR(BZ_IO_ERROR);
-        return 0;
-      }
-      bzf->bufN = (int)n;
-      bzf->strm.avail_in = (unsigned)bzf->bufN;
-      bzf->strm.next_in = bzf->buf;
-    }
-    int ret = BZ2_bzDecompress(&bzf->strm);
-    if (ret != BZ_OK && ret != BZ_STREAM_END) {
-      BZ_SETERR(ret);
-      return 0;
-    }
-    if (ret == BZ_OK && my_feof(bzf->handle) && bzf->strm.avail_in == 0 && bzf->strm.avail_out > 0) {
-      BZ_SETERR(BZ_UNEXPECTED_EOF);
-      return 0;
-    }
-    if (ret == BZ_STREAM_END) {
-      BZ_SETERR(BZ_STREAM_END);
-      return len - (int)bzf->strm.avail_out;
-    }
-    if (bzf->strm.avail_out == 0) {
-      BZ_SETERR(BZ_OK);
-      return len;
-    }
-  }
-}
-
-void BZ2_bzReadGetUnused(int* bzerror, BZFILE* b, void** unused, int* nUnused) {
-  BzFile* bzf = (BzFile*)b;
-  if (bzf == nullptr) {
-    BZ_SETERR(BZ_PARAM_ERROR);
-    return;
-  }
-  if (bzf->lastErr != BZ_STREAM_END) {
-    BZ_SETERR(BZ_SEQUENCE_ERROR);
-    return;
-  }
-  if (unused == nullptr || nUnused == nullptr) {
-    BZ_SETERR(BZ_PARAM_ERROR);
-    return;
-  }
-  BZ_SETERR(BZ_OK);
-  *nUnused = (int)bzf->strm.avail_in;
-  *unused = bzf->strm.next_in;
-}
-
-int BZ2_bzBuffToBuffDecompress(char* dest, unsigned int* destLen, char* source, unsigned int sourceLen, int small,
-                               int verbosity) {
-  if (dest == nullptr || destLen == nullptr || source == nullptr || (small != 0 && small != 1) || verbosity < 0 ||
-      verbosity > 4)
-    return BZ_PARAM_ERROR;
-  bz_stream strm;
-  strm.bzalloc = nullptr;
-  strm.bzfree = nullptr;
-  strm.opaque = nullptr;
-  int ret = BZ2_bzDecompressInit(&strm, verbosity, small);
-  if (ret != BZ_OK) return ret;
-  strm.next_in = source;
-  strm.next_out = dest;
-  strm.avail_in = sourceLen;
-  strm.avail_out = *destLen;
-  ret = BZ2_bzDecompress(&strm);
-  if (ret == BZ_OK) {
-    const bool eof = strm.avail_out > 0;
-    BZ2_bzDecompressEnd(&strm);
-    return eof ? BZ_UNEXPECTED_EOF : BZ_OUTBUFF_FULL;
-  }
-  if (ret != BZ_STREAM_END) {
-    BZ2_bzDecompressEnd(&strm);
-    return ret;
-  }
-  *destLen -= strm.avail_out;
-  BZ2_bzDecompressEnd(&strm);
-  return BZ_OK;
-}
-
-// zlib-style helpers (bzlib.c:1445-1628)
-static BZFILE* bzopen_or_bzdopen(const char* path, int fd, const char* mode, int open_mode) {
-  int bzerr;
-  char unused[BZ_MAX_UNUSED];
-  int blockSize100k = 9;
-  int writing = 0;
-  char mode2[10] = "";
-  FILE* fp = nullptr;
-  BZFILE* bzfp = nullptr;
-  int verbosity = 0, workFactor = 30, smallMode = 0, nUnused = 0;
-  if (mode == nullptr) return nullptr;
-  while (*mode) {
-    switch (*mode) {
-      case 'r': writing = 0; break;
-      case 'w': writing = 1; break;
-      case 's': smallMode = 1; break;
-      default:
-        if (*mode >= '0' && *mode <= '9') blockSize100k = *mode - '0';
-    }
-    mode++;
-  }
-  std::strcat(mode2, writing ? "w" : "r");
-  std::strcat(mode2, "b");
-  if (open_mode == 0) {
-    if (path == nullptr || std::strcmp(path, "") == 0) fp = writing ? stdout : stdin;
-    else fp = fopen(path, mode2);
-  } else {
-    fp = fdopen(fd, mode2);
-  }
-  if (fp == nullptr) return nullptr;
-  if (writing) {
-    if (blockSize100k < 1) blockSize100k = 1;
-    if (blockSize100k > 9) blockSize100k = 9;
-    bzfp = BZ2_bzWriteOpen(&bzerr, fp, blockSize100k, verbosity, workFactor);
-  } else {
-    bzfp = BZ2_bzReadOpen(&bzerr, fp, verbosity, smallMode, unused, nUnused);
-  }
-  if (bzfp == nullptr) {
-    if (fp != stdin && fp != stdout) fclose(fp);
-    return nullptr;
-  }
-  return bzfp;
-}
-
-BZFILE* BZ2_bzopen(const char* path, const char* mode) { return bzopen_or_bzdopen(path, -1, mode, 0); }
-BZFILE* BZ2_bzdopen(int fd, const char* mode) { return bzopen_or_bzdopen(nullptr, fd, mode, 1); }
-
-int BZ2_bzread(BZFILE* b, void* buf, int len) {
-  int bzerr;
-  if (((BzFile*)b)->lastErr == BZ_STREAM_END) return 0;
-  int nread = BZ2_bzRead(&bzerr, b, buf, len);
-  return (bzerr == BZ_OK || bzerr == BZ_STREAM_END) ? nread : -1;
-}
-
-int BZ2_bzwrite(BZFILE* b, void* buf, int len) {
-  int bzerr;
-  BZ2_bzWrite(&bzerr, b, buf, len);
-  return bzerr == BZ_OK ? len : -1;
-}
-
-int BZ2_bzflush(BZFILE*) { return 0; }
-
-void BZ2_bzclose(BZFILE* b) {
-  int bzerr;
-  if (b == nullptr) return;
-  FILE* fp = ((BzFile*)b)->handle;
-  if (((BzFile*)b)->writing) {
-    BZ2_bzWriteClose(&bzerr, b, 0, nullptr, nullptr);
-    if (bzerr != BZ_OK) BZ2_bzWriteClose(nullptr, b, 1, nullptr, nullptr);
-  } else {
-    BZ2_bzReadClose(&bzerr, b);
-  }
-  if (fp != stdin && fp != stdout) fclose(fp);
-}
-
-static const char* kErrStr[] = {"OK",         "SEQUENCE_ERROR", "PARAM_ERROR",    "MEM_ERROR",
-                                "DATA_ERROR", "DATA_ERROR_MAGIC", "IO_ERROR",     "UNEXPECTED_EOF",
-                                "OUTBUFF_FULL", "CONFIG_ERROR", "???",            "???",
-                                "???",        "???",            "???",            "???"};
-
-const char* BZ2_bzerror(BZFILE* b, int* errnum) {
-  int err = ((BzFile*)b)->lastErr;
-  if (err > 0) err = 0;
-  *errnum = err;
-  return kErrStr[err * -1];
-}
 
 }  // extern "C"

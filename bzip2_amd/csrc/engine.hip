@@ -259,7 +259,22 @@ void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_strea
     const unsigned f = last_piece ? flags : 0u;
     uint64_t ob = 0, cons = 0;
     bzg_stats one{};
-    batch(d_in + done_in, take, f, st, d_out + done_out, out_cap - done_out, &ob, &cons, s, one);
+    // the packer ORs 32-bit words: a batch whose destination is not 4-byte aligned (any batch
+    // after the first of a split input, or a caller's odd pointer) is coded into an aligned
+    // workspace buffer and copied behind the previous batch's bytes
+    uint8_t* dst = d_out + done_out;
+    uint64_t cap = out_cap - done_out;
+    const bool misaligned = ((uintptr_t)dst & 3u) != 0;
+    uint8_t* bdst = dst;
+    if (misaligned) {
+      cap = std::min<uint64_t>(cap, take + take / 50 + (take / 100000 + 2) * 64 + 4096);  // bzg_bound(take)
+      bdst = ws.u8("batch_out", cap + 16);
+    }
+    batch(d_in + done_in, take, f, st, bdst, cap, &ob, &cons, s, one);
+    if (misaligned && ob) {
+      HIP_OK(hipMemcpyAsync(dst, bdst, ob, hipMemcpyDeviceToDevice, s));
+      HIP_OK(hipStreamSynchronize(s));
+    }
     acc.rle1_ms += one.rle1_ms;
     acc.bwt_ms += one.bwt_ms;
     acc.mtf_ms += one.mtf_ms;

@@ -126,3 +126,93 @@ def test_periodic_resolver_matches_reference(lib):
         cases.append(w * rng.randint(2, 300))
     for blk in cases:
         assert B.periodic_origptr(blk) == O.ref_blocksort(blk)[1], (blk[:12], len(blk))
+
+
+def _libc():
+    c = ctypes.CDLL(None)
+    c.fopen.restype = ctypes.c_void_p
+    c.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    c.fclose.argtypes = [ctypes.c_void_p]
+    return c
+
+
+def _file_api(lib):
+    vp, ip = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)
+    lib.BZ2_bzReadOpen.restype = vp
+    lib.BZ2_bzReadOpen.argtypes = [ip, vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int]
+    lib.BZ2_bzRead.argtypes = [ip, vp, vp, ctypes.c_int]
+    lib.BZ2_bzReadClose.argtypes = [ip, vp]
+    lib.BZ2_bzReadGetUnused.argtypes = [ip, vp, ctypes.POINTER(vp), ip]
+    lib.BZ2_bzopen.restype = vp
+    lib.BZ2_bzopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    lib.BZ2_bzread.argtypes = [vp, vp, ctypes.c_int]
+    lib.BZ2_bzclose.argtypes = [vp]
+    lib.BZ2_bzerror.restype = ctypes.c_char_p
+    lib.BZ2_bzerror.argtypes = [vp, ip]
+    lib.BZ2_bzWriteOpen.restype = vp
+    lib.BZ2_bzWriteOpen.argtypes = [ip, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    return lib
+
+
+@pytest.mark.parametrize("i", [1, 2, 3])
+def test_file_api_reads_reference_golden(lib, i, tmp_path):
+    """BZ2_bzopen / BZ2_bzread / BZ2_bzerror / BZ2_bzclose (bzlib.c:1445-1628) and
+    BZ2_bzReadOpen / bzRead / ReadGetUnused (bzlib.c:1149-1300) on the shipped goldens, with
+    trailing bytes after the stream handed back as 'unused'."""
+    L = _file_api(lib)
+    g = os.path.join(ROOT, "tests", "golden")
+    want = open(os.path.join(g, f"sample{i}.ref"), "rb").read()
+    b = L.BZ2_bzopen(os.path.join(g, f"sample{i}.bz2").encode(), b"rb")
+    assert b
+    out = bytearray()
+    buf = ctypes.create_string_buffer(7777)
+    while True:
+        n = L.BZ2_bzread(b, buf, 7777)
+        assert n >= 0
+        if n == 0:
+            break
+        out += buf.raw[:n]
+    err = ctypes.c_int(1)
+    assert L.BZ2_bzerror(b, ctypes.byref(err)) == b"OK" and err.value == 0  # STREAM_END (>0) reads as OK
+    L.BZ2_bzclose(b)
+    assert bytes(out) == want
+    # trailing garbage comes back through BZ2_bzReadGetUnused
+    p = tmp_path / "s.bz2"
+    p.write_bytes(open(os.path.join(g, f"sample{i}.bz2"), "rb").read() + b"TRAILER")
+    c = _libc()
+    f = c.fopen(str(p).encode(), b"rb")
+    e = ctypes.c_int(0)
+    h = L.BZ2_bzReadOpen(ctypes.byref(e), f, 0, 0, None, 0)
+    assert h and e.value == B.BZ_OK
+    got = bytearray()
+    big = ctypes.create_string_buffer(1 << 20)
+    while e.value == B.BZ_OK:
+        n = L.BZ2_bzRead(ctypes.byref(e), h, big, 1 << 20)
+        got += big.raw[:n]
+    assert e.value == B.BZ_STREAM_END and bytes(got) == want
+    un, nun = ctypes.c_void_p(), ctypes.c_int(0)
+    L.BZ2_bzReadGetUnused(ctypes.byref(e), h, ctypes.byref(un), ctypes.byref(nun))
+    assert e.value == B.BZ_OK and ctypes.string_at(un, nun.value) == b"TRAILER"
+    L.BZ2_bzReadClose(ctypes.byref(e), h)
+    assert e.value == B.BZ_OK
+    c.fclose(f)
+
+
+def test_file_api_argument_errors(lib, tmp_path):
+    L = _file_api(lib)
+    e = ctypes.c_int(0)
+    assert not L.BZ2_bzReadOpen(ctypes.byref(e), None, 0, 0, None, 0) and e.value == B.BZ_PARAM_ERROR
+    c = _libc()
+    p = tmp_path / "x"
+    p.write_bytes(b"")
+    f = c.fopen(str(p).encode(), b"rb")
+    assert not L.BZ2_bzReadOpen(ctypes.byref(e), f, 0, 2, None, 0) and e.value == B.BZ_PARAM_ERROR  # small
+    assert not L.BZ2_bzReadOpen(ctypes.byref(e), f, 0, 0, None, 3) and e.value == B.BZ_PARAM_ERROR  # unused
+    assert not L.BZ2_bzWriteOpen(ctypes.byref(e), f, 10, 0, 30) and e.value == B.BZ_PARAM_ERROR  # level
+    h = L.BZ2_bzReadOpen(ctypes.byref(e), f, 0, 0, None, 0)
+    buf = ctypes.create_string_buffer(16)
+    assert L.BZ2_bzRead(ctypes.byref(e), h, buf, 16) == 0 and e.value == B.BZ_UNEXPECTED_EOF  # empty file
+    L.BZ2_bzReadGetUnused(ctypes.byref(e), h, ctypes.byref(ctypes.c_void_p()), ctypes.byref(ctypes.c_int()))
+    assert e.value == B.BZ_SEQUENCE_ERROR  # only after STREAM_END
+    L.BZ2_bzReadClose(ctypes.byref(e), h)
+    c.fclose(f)

@@ -351,6 +351,45 @@ def test_device_oom_is_mem_error():
     assert B.buff_to_buff_compress(data, 9) == expected(data, 9)  # the engine recovers
 
 
+def test_file_api_write_matches_reference(tmp_path):
+    """BZ2_bzWriteOpen / BZ2_bzWrite in 5000-byte pieces (the CLI's pattern, bzip2.c:329-427) /
+    BZ2_bzWriteClose64 write the reference's RUN...FINISH stream; BZ2_bzopen("w") / bzwrite /
+    bzclose likewise at -9."""
+    if not O.has_ref():
+        pytest.skip("needs oracle/_ref for the streaming reference")
+    from tests.test_abi import _file_api, _libc
+
+    L = _file_api(B.lib())
+    L.BZ2_bzWrite.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    u = ctypes.POINTER(ctypes.c_uint)
+    L.BZ2_bzWriteClose64.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_int, u, u, u, u]
+    L.BZ2_bzwrite.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    data = datagen.text(1_234_567, 77)
+    pieces = [data[i:i + 5000] for i in range(0, len(data), 5000)]
+    c = _libc()
+    p = tmp_path / "w.bz2"
+    f = c.fopen(str(p).encode(), b"wb")
+    e = ctypes.c_int(0)
+    h = L.BZ2_bzWriteOpen(ctypes.byref(e), f, 3, 0, 0)
+    assert h and e.value == B.BZ_OK
+    for x in pieces:
+        L.BZ2_bzWrite(ctypes.byref(e), h, x, len(x))
+        assert e.value == B.BZ_OK
+    cnt = [ctypes.c_uint(0) for _ in range(4)]
+    L.BZ2_bzWriteClose64(ctypes.byref(e), h, 0, *[ctypes.byref(x) for x in cnt])
+    assert e.value == B.BZ_OK
+    c.fclose(f)
+    want = O.ref_stream_compress(pieces, 3)
+    assert p.read_bytes() == want
+    assert (cnt[0].value, cnt[1].value, cnt[2].value, cnt[3].value) == (len(data), 0, len(want), 0)
+    q = tmp_path / "z.bz2"
+    b = L.BZ2_bzopen(str(q).encode(), b"w9")
+    for x in pieces:
+        assert L.BZ2_bzwrite(b, x, len(x)) == len(x)
+    L.BZ2_bzclose(b)
+    assert q.read_bytes() == O.ref_stream_compress(pieces, 9)
+
+
 def test_round_trip_large_properties():
     """At bench-like sizes: decode(encode(x)) == x with the system bzip2 decoder, and the
     stream equals the reference's on a 4 MB slice."""
@@ -400,6 +439,32 @@ def test_device_api_with_torch_buffers():
     torch.cuda.synchronize()
     assert consumed == len(data)
     assert bytes(d_out[:nbytes].cpu().numpy().tobytes()) == expected(data, 9)
+
+
+def test_device_api_split_batches_unaligned_output():
+    """One bzg_compress_device call larger than the engine's batch limit (1.5e9 bytes): the
+    input is cut into batches inside the call and each batch's bits land right behind the
+    previous batch's bytes, whatever their alignment; also a caller output pointer that is not
+    4-byte aligned."""
+    torch = pytest.importorskip("torch")
+    data = datagen.text(2_000_000, 93)
+    d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+    cap = B.bound(len(data))
+    buf = torch.zeros(cap + 8, dtype=torch.uint8, device="cuda")
+    nb, cons, _ = B.compress_device(d_in.data_ptr(), len(data), 9, buf.data_ptr() + 3, cap)
+    torch.cuda.synchronize()
+    assert cons == len(data) and buf[3:3 + nb].cpu().numpy().tobytes() == expected(data, 9)
+    n = 1_600_000_000  # two batches; RLE1 makes it 1.6e9 * 5 / 255 block bytes
+    d_in = torch.full((n,), 0x61, dtype=torch.uint8, device="cuda")
+    cap = B.bound(n)
+    out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    nb, cons, _ = B.compress_device(d_in.data_ptr(), n, 9, out.data_ptr(), cap)
+    torch.cuda.synchronize()
+    assert cons == n
+    got = out[:nb].cpu().numpy().tobytes()
+    del d_in, out
+    torch.cuda.empty_cache()
+    assert got == expected(b"a" * n, 9)
 
 
 def test_device_api_continuation_batches():
