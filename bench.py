@@ -44,6 +44,9 @@ def parse():
                    help="threads for the multi-core reference baseline (the box's CPU share is 16)")
     p.add_argument("--cpu-mt-sample", type=int, default=640_000_000, help="bytes for the multi-core timing")
     p.add_argument("--no-h2h", action="store_true", help="skip the host-to-host region (profiling runs)")
+    p.add_argument("--repeat-frac", type=float, default=0.0,
+                   help="overwrite this fraction of the text with copies of earlier passages (profiling the "
+                        "long-repeat path; the default workload has none)")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the secondary lines (BASELINE configs 4 and 5, long-repeat text)")
     p.add_argument("--mode", choices=["stream", "independent"], default=None,
@@ -90,6 +93,9 @@ def main():
     data = datagen.text(a.bytes, rank_seed(rank))
     gen_s = time.time() - t0
     d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+    if a.repeat_frac > 0:
+        add_repeats(d_in, a.repeat_frac)
+        data = d_in.cpu().numpy().tobytes()
     cap = B.bound(len(data))
     d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
@@ -249,6 +255,22 @@ def sample_parity(d, n, level, no_cpu):
                              "sample": f"first {n} B, BZ2_bzBuffToBuffCompress -{level}, pinned child"}}
 
 
+def add_repeats(d, frac: float, seed: int = 0x5EED0009) -> None:
+    """Overwrites about frac of d (in place, on the device) with copies of earlier passages of
+    2 kB .. 200 kB: enwik-like long repeats (templates, reverted revisions)."""
+    import random
+
+    n = d.numel()
+    rng = random.Random(seed)
+    covered = 0
+    while covered < int(n * frac):
+        ln = rng.randint(2_000, 200_000)
+        dst = rng.randrange(1_000_000, n - ln)
+        src = rng.randrange(0, dst - ln) if rng.random() < 0.5 else max(0, dst - rng.randint(ln, 4 * ln))
+        d[dst:dst + ln] = d[src:src + ln].clone()
+        covered += ln
+
+
 def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False):
     """Secondary lines (never `value`): BASELINE configs 4 and 5 at full size (4 GiB, device
     resident; bzg_compress_device cuts them into 1.5e9-byte batches), and enwik-like text with
@@ -274,14 +296,7 @@ def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False):
     # long repeats: 25% of the text overwritten by copies of earlier passages (2 kB .. 200 kB)
     n = d_text.numel()
     dr = d_text.clone()
-    rng = __import__("random").Random(0x5EED0009)
-    covered = 0
-    while covered < n // 4:
-        ln = rng.randint(2_000, 200_000)
-        dst = rng.randrange(1_000_000, n - ln)
-        src = rng.randrange(0, dst - ln) if rng.random() < 0.5 else max(0, dst - rng.randint(ln, 4 * ln))
-        dr[dst:dst + ln] = dr[src:src + ln].clone()
-        covered += ln
+    add_repeats(dr, 0.25)
     ms, nb, st = time_device(dr, n, level, d_out_text, cap_text, steps=2)
     res["long_repeat_text"] = line_for("long_repeat", n, level, ms, nb, st,
                                        f"the main workload with 25% overwritten by copies of earlier passages "

@@ -1218,6 +1218,46 @@ __global__ void k_s2_bounds(const uint32_t* __restrict__ cscan, uint32_t total, 
   if (c < 6) out[c] = cscan[(size_t)(c + 1) * total] - cscan[(size_t)c * total];
 }
 
+// ---------------------------------------------------------------- S2 lists in block order
+// The S1 passes append S2 groups pass after pass, each pass sweeping every block, so a list
+// is ~a dozen sparse sweeps: the groups in flight at once would span dozens of blocks, whose
+// texts do not fit an XCD's L2 together.  Before S2 the lists are counting-sorted by unit
+// (block), so the groups in flight come from one or two blocks (order inside a unit is
+// immaterial: every group is sorted on its own slots).
+// Lanes of a wave sharing a unit reserve consecutive counts with one atomic per unit.
+__device__ __forceinline__ uint32_t unit_reserve(uint32_t* __restrict__ ctr, uint32_t unit, bool act) {
+  uint64_t left = __ballot(act);
+  uint32_t pos = 0;
+  const uint32_t lane = __lane_id();
+  while (left) {
+    const int leader = __ffsll((unsigned long long)left) - 1;
+    const uint32_t lu = (uint32_t)__shfl((int)unit, leader, 64);
+    const uint64_t m = __ballot(act && unit == lu) & left;
+    uint32_t base = 0;
+    if (lane == (uint32_t)leader) base = atomicAdd(&ctr[lu], (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if ((m >> lane) & 1ull) pos = base + (uint32_t)__popcll(m & lanemask_lt());
+    left &= ~m;
+  }
+  return pos;
+}
+
+__global__ void k_unit_count(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < n;
+  (void)unit_reserve(cnt, act ? L[i].unit : 0u, act);
+}
+
+__global__ void k_unit_scatter(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ cursor,
+                               Grp* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < n;
+  Grp g{0, 0, 0, 0};
+  if (act) g = L[i];
+  const uint32_t p = unit_reserve(cursor, g.unit, act);
+  if (act) out[p] = g;
+}
+
 // ---------------------------------------------------------------- fallback glue
 __global__ void k_fb_flag(const Grp* __restrict__ D, uint32_t n, uint32_t* __restrict__ uflag, uint32_t* __restrict__ mind) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1433,6 +1473,19 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   {
     ClsLists N{};
     for (int c = 0; c < 6; c++) N.l[c] = ws.typed<Grp>("sort_s2n" + std::to_string(c), ccap[c]);
+    {  // block order for the first S2 round (see k_unit_count)
+      uint32_t* ucnt = ws.u32("sort_ucnt", nb + 64);
+      for (int c = 0; c < 6; c++) {
+        if (ncls[c] < 2) continue;
+        HIP_OK(hipMemsetAsync(ucnt, 0, 4 * (size_t)nb, st));
+        k_unit_count<<<grid(ncls[c]), kT, 0, st>>>(C.l[c], ncls[c], ucnt);
+        HIP_OK(hipGetLastError());
+        scan_u32(ScanOp::Sum, true, ucnt, ucnt, nb, nullptr, scratch, st);
+        k_unit_scatter<<<grid(ncls[c]), kT, 0, st>>>(C.l[c], ncls[c], ucnt, N.l[c]);
+        HIP_OK(hipGetLastError());
+        std::swap(C.l[c], N.l[c]);
+      }
+    }
     const size_t max_s2 = ccap[3] + ccap[4] + ccap[5];
     uint32_t* ccnt2 = ws.u32("sort_s2cnt", 6 * max_s2 + 16);
     uint32_t* scratch2 = ws.u32("sort_s2scan", scan_scratch_words(6 * max_s2 + 16) + 64);

@@ -559,6 +559,8 @@ void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0
     read_counters();
     const uint32_t totalL = hc[0];
     if (revisited) *revisited += totalL;
+    static const bool debug = getenv("BZG_DEBUG") != nullptr;
+    if (debug) fprintf(stderr, "[bzg sort S3] iter %d: h=%u groups=%u elems=%u\n", iters, h, nL, totalL);
     HIP_OK(hipMemsetAsync(gmap, 0, (size_t)totalL * 4, st));
     k_mark_groups<<<grid(nL), kT, 0, st>>>(P, nL, gmap);
     HIP_OK(hipGetLastError());
