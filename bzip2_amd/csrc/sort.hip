@@ -17,7 +17,7 @@
 //       each rotation are gathered, a bitonic network in registers sorts the segment by
 //       (run start, key, index), unique rotations write SA / BWT byte / origPtr, and tied
 //       runs repeat with the next 8 characters (2-8: rank counting on 16 characters).
-//   S3  groups still equal after kDWave characters (long repeats) or S1 buckets still larger
+//   S3  groups still equal after B.dwave characters (long repeats) or S1 buckets still larger
 //       than kBig after kDBig characters go to prefix doubling (sortdbl.hip) over ISA ranks
 //       built for the affected blocks only.
 #include <algorithm>
@@ -39,7 +39,6 @@ constexpr uint32_t kBig = 256;        // buckets larger than this are split by S
 constexpr uint32_t kDTile = BZG_DTILE;  // rotations per workgroup in an S1 pass
 constexpr uint32_t kPerT = kDTile / kT;
 constexpr uint32_t kDBig = 16;        // S1 byte passes stop at this depth (then doubling)
-constexpr uint32_t kDWave = 1024;     // S2 rounds stop at this depth (then doubling)
 #ifndef BZG_SG
 #define BZG_SG 2048
 #endif
@@ -744,7 +743,7 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
   for (;;) {
     const uint64_t live = __ballot(!done);
     if (live == 0) break;
-    if (d >= kDWave) {  // still tied after kDWave characters: leave to the doubling fallback
+    if (d >= B.dwave) {  // still tied after B.dwave characters: leave to the doubling fallback
       if (!done) {
         const uint64_t mates = match_byte(cls, live);
         const uint32_t r = (uint32_t)__popcll(mates & lanemask_lt());
@@ -911,7 +910,7 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
 #pragma unroll
     for (int r = 0; r < kPer; r++) any |= live[r];
     if (__ballot(any) == 0) break;
-    const bool deep = depth >= kDWave;
+    const bool deep = depth >= B.dwave;
     if constexpr (kBatch) {
       uint32_t raw[kPer][5], qq[kPer];
 #pragma unroll
@@ -939,7 +938,7 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
       }
     }
     wave_sync();
-    if (deep) {  // still tied after kDWave characters: leave to the doubling fallback
+    if (deep) {  // still tied after B.dwave characters: leave to the doubling fallback
 #pragma unroll
       for (int r = 0; r < kPer; r++)
         if (live[r]) {
@@ -1136,10 +1135,10 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     }
     if (__ballot(any_tied) == 0) break;
     depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
-    if (++round >= kRounds || depth >= kDWave) {
+    if (++round >= kRounds || depth >= B.dwave) {
       if constexpr (kEmit) {
         static_assert(kSeg == 64, "one group per wave");
-        if (depth < kDWave) {
+        if (depth < B.dwave) {
           uint32_t* cc = Lk[w];  // per-class counters, then the record cursor
           if (lane < 8) cc[lane] = 0;
           wave_sync();
@@ -1261,10 +1260,15 @@ __global__ void k_unit_scatter(const Grp* __restrict__ L, uint32_t n, uint32_t* 
 // ---------------------------------------------------------------- fallback glue
 __global__ void k_fb_flag(const Grp* __restrict__ D, uint32_t n, uint32_t* __restrict__ uflag, uint32_t* __restrict__ mind) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n) return;
-  const Grp gr = D[g];
-  uflag[gr.unit] = 1;
-  atomicMin(mind, grp_depth(gr));
+  uint32_t d = 0xffffffffu;
+  if (g < n) {
+    const Grp gr = D[g];
+    if (uflag[gr.unit] == 0) uflag[gr.unit] = 1;  // read first: most lanes find it set
+    d = grp_depth(gr);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) d = min(d, (uint32_t)__shfl_xor((int)d, o, 64));
+  if (__lane_id() == 0 && d != 0xffffffffu) atomicMin(mind, d);
 }
 
 // Deep groups whose data is in the alternate buffer move to the primary SA; the doubling
@@ -1343,6 +1347,13 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   B.sk2 = ws.u32("sort_sk2", S + 16);
   B.text = r.blk;
   B.units = units;
+  {
+    static const uint32_t dwave = [] {
+      const char* e = getenv("BZG_DWAVE");
+      return e ? (uint32_t)std::max(16, atoi(e)) : 1024u;
+    }();
+    B.dwave = dwave;
+  }
   // class lists: a class-c bucket holds more than kClsMax[c-1] rotations
   ClsLists C{};
   size_t ccap[kNCls];
@@ -1557,7 +1568,17 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     HIP_OK(hipGetLastError());
     k_fb_group_isa<<<n_deep, kT, 0, st>>>(L0, B);
     HIP_OK(hipGetLastError());
-    if (debug) fprintf(stderr, "[bzg sort S3] deep groups=%u units=%zu h0=%u\n", n_deep, fb_units.size(), h0);
+    if (debug) {
+      std::vector<Grp> hd(n_deep);
+      HIP_OK(hipMemcpy(hd.data(), L0, sizeof(Grp) * n_deep, hipMemcpyDeviceToHost));
+      uint64_t tot = 0, mx = 0;
+      for (const Grp& g : hd) {
+        tot += g.size;
+        mx = std::max<uint64_t>(mx, g.size);
+      }
+      fprintf(stderr, "[bzg sort S3] deep groups=%u elems=%llu max=%llu units=%zu h0=%u\n", n_deep,
+              (unsigned long long)tot, (unsigned long long)mx, fb_units.size(), h0);
+    }
     doubling_sort(ws, B, L0, n_deep, h0, &dbl_iters, &dbl_elems, st);
     k_unit_out<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B.sa, r.blk, bwt);
     HIP_OK(hipGetLastError());

@@ -31,6 +31,7 @@ struct SortBufs {
   uint32_t *sk, *sk2;  // S1 key caches beside sa / sa2: the next characters, most significant first
   const uint8_t* text;
   const Unit* units;
+  uint32_t dwave;  // S2 gives a tied group to the doubling fallback (S3) at this depth
 };
 
 // Largest g with P[g] <= x (P is an exclusive prefix, P[0] = 0).

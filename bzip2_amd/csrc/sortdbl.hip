@@ -509,12 +509,20 @@ __global__ void __launch_bounds__(kT) k_equal(const Grp* __restrict__ G, uint32_
 void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0, uint32_t h, int* iterations,
                    uint64_t* revisited, hipStream_t st) {
   if (nL0 == 0) return;
-  // element total of the initial list bounds every later list
-  std::vector<Grp> hg(nL0);
-  HIP_OK(hipMemcpyAsync(hg.data(), L0, sizeof(Grp) * nL0, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  // element total of the initial list bounds every later list (summed on the device)
   uint64_t T = 0;
-  for (const Grp& g : hg) T += g.size;
+  {
+    uint32_t* sz = ws.u32("dbl_P", (size_t)nL0 + 16);
+    uint32_t* tot0 = ws.u32("dbl_T0", 16);
+    uint32_t* scr = ws.u32("dbl_scan", scan_scratch_words((size_t)nL0 + 16) + 64);
+    k_group_sizes<<<(unsigned)ceil_div64(nL0, kT), kT, 0, st>>>(L0, nL0, sz);
+    HIP_OK(hipGetLastError());
+    scan_u32(ScanOp::Sum, true, sz, sz, nL0, tot0, scr, st);
+    uint32_t t32 = 0;
+    HIP_OK(hipMemcpyAsync(&t32, tot0, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    T = t32;
+  }
   const size_t lcap = T / 2 + nL0 + 16;
   const size_t bigcap = T / kSmall + nL0 + 16;
   Grp* L = ws.typed<Grp>("dbl_L", lcap);

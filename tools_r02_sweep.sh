@@ -1,0 +1,17 @@
+#!/bin/bash
+# BZG_DWAVE sweep on the main and long-repeat workloads (bench lines + one debug trace each)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+T=$1; O=gpurun_out/$T; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "bwt or long_repeat or periodic" > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for dw in ${DWAVES:-1024 256 128 64}; do
+  for rf in 0 0.25; do
+    echo "dwave $dw rf $rf $(date)"
+    BZG_DWAVE=$dw timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu --no-h2h --no-extra --repeat-frac $rf > $O/b_${dw}_${rf}.json 2> $O/b_${dw}_${rf}.err || { echo "bench failed"; tail -5 $O/b_${dw}_${rf}.err; exit 1; }
+    python3 -c "import json;d=json.load(open('$O/b_${dw}_${rf}.json'));print(d['value'],d['stages_ms'])"
+  done
+done
+BZG_DEBUG=1 BZG_ONE_STREAM=1 BZG_DWAVE=128 timeout -k 10 300 python bench.py --steps 1 --warmup 0 --no-cpu --no-h2h --no-extra --repeat-frac 0.25 > $O/debug_rep.json 2> $O/debug_rep.err || exit 1
+BZG_ONE_STREAM=1 BZG_DWAVE=128 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_rep -o run -- python bench.py --steps 1 --warmup 1 --no-cpu --no-h2h --no-extra --repeat-frac 0.25 > $O/prof_rep.log 2>&1 || { echo "trace rep failed"; exit 1; }
+echo "done $(date)"
