@@ -683,6 +683,248 @@ __global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, con
   }
 }
 
+// ---- packed S1 groups finished in LDS (k_s1p): a tile holds all the groups whose element
+// prefix falls in a kSG window (< 2 kSG rotations).  The tile stays in LDS while byte passes
+// split its big segments (> kBig rotations); each pass counts (segment, character) bins with
+// LDS atomics, scans them and moves every element of a big segment to its bucket inside the
+// tile.  A bucket of one is final (SA, BWT byte, origPtr); a bucket of 2..kBig rotations goes
+// to the S2 class list of its size (its rotations stored at their slots of the primary SA);
+// a bucket still larger than kBig after kDLds characters goes to the doubling fallback.  So
+// the rotations of a packed group are read from HBM once and written once, whatever the
+// number of passes; the text is gathered 4 characters at a time per rotation.
+constexpr uint32_t kPE = 2 * kSG;                 // elements per tile
+constexpr uint32_t kPT = 512;                     // threads
+constexpr uint32_t kPPer = kPE / kPT;             // elements per thread
+constexpr uint32_t kPSeg = kPE / (kBig + 1) + 2;  // big segments at once (>= kSGrp)
+constexpr uint32_t kDLds = 64;                    // depth at which a big bucket goes deep
+static_assert(kPSeg >= kSGrp, "the initial groups of a tile are big segments");
+
+struct S1pLds {
+  uint32_t v[kPE];                 // rotation at each tile position
+  uint32_t key[kPE];               // its next characters, most significant first
+  uint8_t seg[kPE];                // big segment of the position, 0xff once settled
+  uint32_t cnt[kPSeg * 256];       // (segment, character) bin counts
+  uint32_t cur[kPSeg * 256];       // bin bases (tile positions)
+  uint8_t nseg[kPSeg * 256];       // next segment of a bin: 0..kPSeg-1, 0xfe settled
+  // segment tables (current and next): tile start, size, depth, valid key bytes, slot delta
+  // (global slot = tile position + delta), unit
+  uint32_t sstart[2][kPSeg], ssize[2][kPSeg], sdepth[2][kPSeg], scache[2][kPSeg], sdelta[2][kPSeg], sunit[2][kPSeg];
+  uint32_t ntoff[kPSeg], nlen[kPSeg];  // unit text offset / length of the current segments
+  uint32_t segb[kPSeg];             // scan value at each segment's first bin
+  uint32_t nbig[2];
+  uint32_t sh[kPT / 64];
+};
+
+// Appends n groups of class c (wave-aggregated).  app[c] holds the next free list index.
+__device__ __forceinline__ void cls_append(const ClsLists& C, uint32_t* __restrict__ app, bool act, uint32_t c,
+                                           const Grp& g) {
+#pragma unroll
+  for (uint32_t k = 0; k < 6; k++) {
+    const uint32_t p = wave_append(app + k, act && c == k);
+    if (act && c == k) C.l[k][p] = g;
+  }
+}
+
+__global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+                                            const uint32_t* __restrict__ last, SortBufs B, SortOut O, ClsLists C,
+                                            uint32_t* __restrict__ app) {
+  __shared__ S1pLds S;
+  const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t i0 = first[t];
+  if (i0 == 0xffffffffu) return;
+  const uint32_t ni = min(last[t], i0 + kSGrp) - i0;
+  const uint32_t tid = threadIdx.x;
+  // ---- load the tile's groups: segment tables 0 and every element's rotation and key
+  if (tid < ni) {
+    const Grp g = SG[i0 + tid];
+    S.ssize[0][tid] = g.size;
+    S.sdepth[0][tid] = grp_depth(g);
+    S.scache[0][tid] = (g.flags & kGrpIdent) ? 0u : grp_cache(g);
+    S.sunit[0][tid] = g.unit;
+    S.sdelta[0][tid] = g.start;  // fixed below
+    S.sstart[0][tid] = g.flags;  // flags, replaced by the tile start below
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t o = 0;
+    for (uint32_t j = 0; j < ni; j++) {
+      const uint32_t fl = S.sstart[0][j];
+      S.sstart[0][j] = o;
+      S.sdelta[0][j] -= o;
+      S.ssize[0][j] |= (fl & (kGrpIdent | kGrpAlt)) << 30;  // source buffer bits, stripped below
+      o += S.ssize[0][j] & 0x3fffffffu;
+    }
+    S.nbig[0] = ni;
+  }
+  __syncthreads();
+  if (tid < ni) {
+    const Unit U = B.units[S.sunit[0][tid]];
+    S.ntoff[tid] = U.toff;
+    S.nlen[tid] = U.len;
+  }
+  uint32_t n = 0;
+  for (uint32_t j = 0; j < ni; j++) n += S.ssize[0][j] & 0x3fffffffu;
+  for (uint32_t j = 0; j < ni; j++) {  // elements of group j (reads of the source slots, coalesced)
+    const uint32_t sz = S.ssize[0][j] & 0x3fffffffu, st = S.sstart[0][j], fl = S.ssize[0][j] >> 30;
+    const uint32_t slot0 = st + S.sdelta[0][j];
+    const uint32_t* src = (fl & (kGrpAlt << 0)) ? B.sa2 : B.sa;
+    const uint32_t* srck = (fl & kGrpAlt) ? B.sk2 : B.sk;
+    const bool ident = fl & kGrpIdent;
+    const bool cached = S.scache[0][j] != 0;
+    for (uint32_t e = tid; e < sz; e += kPT) {
+      S.v[st + e] = ident ? e : src[slot0 + e];
+      S.key[st + e] = cached ? srck[slot0 + e] : 0u;
+      S.seg[st + e] = (uint8_t)j;
+    }
+  }
+  __syncthreads();
+  if (tid < ni) S.ssize[0][tid] &= 0x3fffffffu;
+  __syncthreads();
+  const Unit* __restrict__ units = B.units;
+  uint32_t cur_t = 0;
+  for (;;) {
+    const uint32_t nb = S.nbig[cur_t];
+    if (nb == 0) break;
+    for (uint32_t b = tid; b < nb * 256; b += kPT) S.cnt[b] = 0;
+    __syncthreads();
+    // ---- count: every element of a big segment takes its next character
+    uint32_t vv[kPPer], kk[kPPer], rk[kPPer];
+    uint8_t sg[kPPer];
+#pragma unroll
+    for (int i = 0; i < (int)kPPer; i++) {
+      const uint32_t p = i * kPT + tid;
+      sg[i] = p < n ? S.seg[p] : (uint8_t)0xff;
+      vv[i] = p < n ? S.v[p] : 0u;
+      kk[i] = p < n ? S.key[p] : 0u;
+    }
+    // refill empty caches: 4 characters from the text (loads issued before use)
+    uint32_t q[kPPer];
+#pragma unroll
+    for (int i = 0; i < (int)kPPer; i++) {
+      q[i] = 0;
+      if (sg[i] != 0xff && S.scache[cur_t][sg[i]] == 0) {
+        const uint32_t len = S.nlen[sg[i]];
+        q[i] = cyc_pos(vv[i], S.sdepth[cur_t][sg[i]], len);
+        kk[i] = ld_u32(B.text + S.ntoff[sg[i]] + q[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < (int)kPPer; i++) {
+      if (sg[i] != 0xff && S.scache[cur_t][sg[i]] == 0) {
+        const uint32_t len = S.nlen[sg[i]];
+        kk[i] = q[i] + 4 <= len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.ntoff[sg[i]], len, q[i]);
+      }
+      if (sg[i] != 0xff) rk[i] = atomicAdd(&S.cnt[sg[i] * 256u + (kk[i] >> 24)], 1u);
+    }
+    __syncthreads();
+    // ---- bins -> tile positions: one exclusive scan over all bins (segments are contiguous in
+    // the tile and listed in tile order, so a bin's base is its segment start plus the counts of
+    // the segment's lower bins = the scan minus the counts of the lower segments)
+    {
+      constexpr uint32_t kB = (kPSeg * 256 + kPT - 1) / kPT;
+      uint32_t c[kB], sum = 0;
+#pragma unroll
+      for (int x = 0; x < (int)kB; x++) {
+        const uint32_t b = tid * kB + x;
+        c[x] = b < nb * 256 ? S.cnt[b] : 0u;
+        sum += c[x];
+      }
+      uint32_t run = block_incl_sum(sum, S.sh, (uint32_t*)nullptr) - sum;
+#pragma unroll
+      for (int x = 0; x < (int)kB; x++) {
+        const uint32_t b = tid * kB + x;
+        if (b < nb * 256) S.cur[b] = run;
+        run += c[x];
+      }
+    }
+    __syncthreads();
+    // segment j's bins start at scan value sum_{j' < j} ssize[j']; shift to its tile start
+    if (tid < nb) S.segb[tid] = S.cur[tid * 256];
+    __syncthreads();
+    for (uint32_t b = tid; b < nb * 256; b += kPT) {
+      const uint32_t j = b >> 8;
+      S.cur[b] = S.cur[b] - S.segb[j] + S.sstart[cur_t][j];
+    }
+    __syncthreads();
+    // ---- classify the bins: settled (S2 / final / deep) or a big segment of the next pass
+    const uint32_t nxt = cur_t ^ 1u;
+    if (tid == 0) S.nbig[nxt] = 0;
+    __syncthreads();
+    for (uint32_t b = tid; b < nb * 256; b += kPT) {
+      const uint32_t c = S.cnt[b];
+      uint8_t ns = 0xfe;
+      if (c > kBig) {
+        const uint32_t j = b >> 8, d = S.sdepth[cur_t][j] + 1;
+        if (d < kDLds) {
+          const uint32_t k = atomicAdd(&S.nbig[nxt], 1u);  // < kPSeg: each holds > kBig of < kPE
+          S.sstart[nxt][k] = S.cur[b];
+          S.ssize[nxt][k] = c;
+          S.sdepth[nxt][k] = d;
+          S.scache[nxt][k] = S.scache[cur_t][j] ? S.scache[cur_t][j] - 1 : 3u;
+          S.sdelta[nxt][k] = S.sdelta[cur_t][j];
+          S.sunit[nxt][k] = S.sunit[cur_t][j];
+          ns = (uint8_t)k;
+        }
+      }
+      S.nseg[b] = ns;
+    }
+    __syncthreads();
+    // ---- move: every element of a big segment to its bucket position
+    uint32_t np[kPPer];
+#pragma unroll
+    for (int i = 0; i < (int)kPPer; i++) {
+      if (sg[i] == 0xff) continue;
+      const uint32_t b = sg[i] * 256u + (kk[i] >> 24);
+      np[i] = S.cur[b] + rk[i];
+      rk[i] = b;
+      S.v[np[i]] = vv[i];
+      S.key[np[i]] = kk[i] << 8;
+      S.seg[np[i]] = S.nseg[b] == 0xfe ? (uint8_t)0xff : S.nseg[b];
+    }
+    // ---- settle: finals, and the rotations of S2 / deep groups to the primary SA
+#pragma unroll
+    for (int i = 0; i < (int)kPPer; i++) {
+      if (sg[i] == 0xff) continue;
+      const uint32_t b = rk[i];
+      if (S.nseg[b] != 0xfe) continue;
+      const uint32_t j = b >> 8;
+      const uint32_t slot = np[i] + S.sdelta[cur_t][j];
+      if (S.cnt[b] == 1) {
+        const uint32_t u = S.sunit[cur_t][j];
+        emit_final(B, O, units[u], u, slot, vv[i], true);
+      } else {
+        B.sa[slot] = vv[i];
+      }
+    }
+    // one group record per bin of 2.. rotations (S2 class list, or deep)
+    for (uint32_t b0 = 0; b0 < nb * 256; b0 += kPT) {
+      const uint32_t b = b0 + tid;
+      const bool in = b < nb * 256;
+      const uint32_t c = in ? S.cnt[b] : 0u;
+      const bool grp = in && c >= 2 && S.nseg[b] == 0xfe;
+      const uint32_t j = b >> 8;
+      Grp g{0, 0, 0, 0};
+      uint32_t cl = 0xffu;
+      if (grp) {
+        const uint32_t d = S.sdepth[cur_t][j] + 1;
+        g = Grp{S.cur[b] + S.sdelta[cur_t][j], c, S.sunit[cur_t][j], grp_flags(0u, d, 0u)};
+        cl = c <= kBig ? size_cls(c) : kClsDeep;
+      }
+      cls_append(C, app, grp && cl < 6u, cl, g);
+      const uint32_t dp = wave_append(O.n_deep, grp && cl == kClsDeep);
+      if (grp && cl == kClsDeep) O.deep[dp] = g;
+    }
+    __syncthreads();
+    cur_t = nxt;
+  }
+}
+
+// app[c] = first free index of S2 class list c after this pass's tiled emissions
+__global__ void k_app_init(const uint32_t* __restrict__ bounds, ClsLists C, uint32_t* __restrict__ app) {
+  const uint32_t c = threadIdx.x;
+  if (c < 6) app[c] = C.base[c] + (bounds[c + 1] - bounds[c]);
+}
+
 // out[c] = start of class c in the class-major scan (c < kNCls), out[kNCls] = total.
 __global__ void k_cls_bounds(const uint32_t* __restrict__ cscan, uint32_t nTot, const uint32_t* __restrict__ total,
                              uint32_t* __restrict__ out) {
@@ -1386,13 +1628,17 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* srec = ws.u32("sort_rec", S / 2 + 64);  // packed-pass bucket records
   uint32_t* scratch =
       ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[6])) + 64);
-  uint32_t hc[32];
+  uint32_t hc[48];
   auto read_counters = [&]() {
     HIP_OK(hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
   };
   auto grid = [](uint64_t n) { return (unsigned)std::max<uint64_t>(1, ceil_div64(n, kT)); };
   static const bool debug = getenv("BZG_DEBUG") != nullptr;
+  static const bool use_s1p = [] {  // packed groups finished in LDS (k_s1p); 0: one pass per kernel (k_s1s)
+    const char* e = getenv("BZG_S1P");
+    return !e || atoi(e) != 0;
+  }();
 
   HIP_OK(hipMemsetAsync(cnt, 0, 64 * 4, st));
   k_init_units<<<grid(nb), kT, 0, st>>>(units, nb, B, O, C, cnt);
@@ -1421,7 +1667,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     read_counters();
     const uint32_t ntl = n7 ? hc[17] : 0;
     const uint32_t nT = n6 ? ceil_div(hc[18], kSG) : 0;
-    const uint32_t nTot = n7 + nT;
+    // class-major scan over the tiled groups (and, on the k_s1s path, the packed tiles)
+    const uint32_t nTot = use_s1p ? n7 : n7 + nT;
     if (debug) {
       fprintf(stderr, "[bzg sort S1] pass %d: tiled groups=%u tiles=%u | packed groups=%u elems=%u tiles=%u\n", passes,
               n7, ntl, n6, n6 ? hc[18] : 0, nT);
@@ -1431,8 +1678,10 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipMemsetAsync(first, 0xff, (size_t)nT * 4, st));
       k_tile_first<<<grid(n6), kT, 0, st>>>(P, n6, first, last);
       HIP_OK(hipGetLastError());
-      k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
-      HIP_OK(hipGetLastError());
+      if (!use_s1p) {
+        k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
+        HIP_OK(hipGetLastError());
+      }
     }
     if (n7) {
       k_s1_hist<<<ntl, kT, 0, st>>>(cur7, n7, TP, B, hist);
@@ -1440,9 +1689,12 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_s1_off<<<n7, kT, 0, st>>>(cur7, nTot, TP, hist, tot, ccnt, O.deep, O.n_deep);
       HIP_OK(hipGetLastError());
     }
-    scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * nTot, cnt + 16, scratch, st);
-    k_cls_bounds<<<1, 64, 0, st>>>(ccnt, nTot, cnt + 16, cnt + 8);
-    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemsetAsync(cnt + 8, 0, 9 * 4, st));
+    if (nTot) {
+      scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * nTot, cnt + 16, scratch, st);
+      k_cls_bounds<<<1, 64, 0, st>>>(ccnt, nTot, cnt + 16, cnt + 8);
+      HIP_OK(hipGetLastError());
+    }
     ClsLists Cp = C;
     for (int c = 0; c < 6; c++) Cp.base[c] = ncls[c];
     Cp.l[6] = nxt6;
@@ -1454,12 +1706,19 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_s1_single<<<n7, kT, 0, st>>>(cur7, B, tot);
       HIP_OK(hipGetLastError());
     }
-    if (nT) {
+    if (nT && !use_s1p) {
       k_s1s_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(cur6, first, last, P, nT, O, srec, nrec, ccnt, nTot, n7, Cp);
       HIP_OK(hipGetLastError());
     }
+    // S2 lists after the tiled emissions; the packed tiles append behind them
+    k_app_init<<<1, 64, 0, st>>>(cnt + 8, Cp, cnt + 32);
+    HIP_OK(hipGetLastError());
+    if (nT && use_s1p) {
+      k_s1p<<<nT, kPT, 0, st>>>(cur6, first, last, B, O, Cp, cnt + 32);
+      HIP_OK(hipGetLastError());
+    }
     read_counters();
-    for (int c = 0; c < 6; c++) ncls[c] += hc[8 + c + 1] - hc[8 + c];
+    for (int c = 0; c < 6; c++) ncls[c] = hc[32 + c];
     n6 = hc[8 + 7] - hc[8 + 6];
     n7 = hc[8 + 8] - hc[8 + 7];
     std::swap(cur6, nxt6);
@@ -1570,14 +1829,18 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     HIP_OK(hipGetLastError());
     if (debug) {
       std::vector<Grp> hd(n_deep);
-      HIP_OK(hipMemcpy(hd.data(), L0, sizeof(Grp) * n_deep, hipMemcpyDeviceToHost));
-      uint64_t tot = 0, mx = 0;
+      HIP_OK(hipMemcpyAsync(hd.data(), L0, sizeof(Grp) * n_deep, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      uint64_t tot = 0, mx = 0, hist[5] = {0, 0, 0, 0, 0};
       for (const Grp& g : hd) {
         tot += g.size;
         mx = std::max<uint64_t>(mx, g.size);
+        hist[std::min<uint32_t>(g.size, 4)]++;
       }
-      fprintf(stderr, "[bzg sort S3] deep groups=%u elems=%llu max=%llu units=%zu h0=%u\n", n_deep,
-              (unsigned long long)tot, (unsigned long long)mx, fb_units.size(), h0);
+      fprintf(stderr, "[bzg sort S3] deep groups=%u elems=%llu max=%llu sizes 0:%llu 1:%llu 2:%llu 3:%llu 4+:%llu units=%zu h0=%u\n",
+              n_deep, (unsigned long long)tot, (unsigned long long)mx, (unsigned long long)hist[0],
+              (unsigned long long)hist[1], (unsigned long long)hist[2], (unsigned long long)hist[3],
+              (unsigned long long)hist[4], fb_units.size(), h0);
     }
     doubling_sort(ws, B, L0, n_deep, h0, &dbl_iters, &dbl_elems, st);
     k_unit_out<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B.sa, r.blk, bwt);
