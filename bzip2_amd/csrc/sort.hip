@@ -709,7 +709,7 @@ struct S1pLds {
   // segment tables (current and next): tile start, size, depth, valid key bytes, slot delta
   // (global slot = tile position + delta), unit
   uint32_t sstart[2][kPSeg], ssize[2][kPSeg], sdepth[2][kPSeg], scache[2][kPSeg], sdelta[2][kPSeg], sunit[2][kPSeg];
-  uint32_t ntoff[kPSeg], nlen[kPSeg];  // unit text offset / length of the current segments
+  uint32_t stoff[2][kPSeg], slen[2][kPSeg];  // text offset / length of the segment's unit
   uint32_t segb[kPSeg];             // scan value at each segment's first bin
   uint32_t nbig[2];
   uint32_t sh[kPT / 64];
@@ -759,8 +759,8 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
   __syncthreads();
   if (tid < ni) {
     const Unit U = B.units[S.sunit[0][tid]];
-    S.ntoff[tid] = U.toff;
-    S.nlen[tid] = U.len;
+    S.stoff[0][tid] = U.toff;
+    S.slen[0][tid] = U.len;
   }
   uint32_t n = 0;
   for (uint32_t j = 0; j < ni; j++) n += S.ssize[0][j] & 0x3fffffffu;
@@ -803,16 +803,16 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
     for (int i = 0; i < (int)kPPer; i++) {
       q[i] = 0;
       if (sg[i] != 0xff && S.scache[cur_t][sg[i]] == 0) {
-        const uint32_t len = S.nlen[sg[i]];
+        const uint32_t len = S.slen[cur_t][sg[i]];
         q[i] = cyc_pos(vv[i], S.sdepth[cur_t][sg[i]], len);
-        kk[i] = ld_u32(B.text + S.ntoff[sg[i]] + q[i]);
+        kk[i] = ld_u32(B.text + S.stoff[cur_t][sg[i]] + q[i]);
       }
     }
 #pragma unroll
     for (int i = 0; i < (int)kPPer; i++) {
       if (sg[i] != 0xff && S.scache[cur_t][sg[i]] == 0) {
-        const uint32_t len = S.nlen[sg[i]];
-        kk[i] = q[i] + 4 <= len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.ntoff[sg[i]], len, q[i]);
+        const uint32_t len = S.slen[cur_t][sg[i]];
+        kk[i] = q[i] + 4 <= len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.stoff[cur_t][sg[i]], len, q[i]);
       }
       if (sg[i] != 0xff) rk[i] = atomicAdd(&S.cnt[sg[i] * 256u + (kk[i] >> 24)], 1u);
     }
@@ -863,6 +863,8 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
           S.scache[nxt][k] = S.scache[cur_t][j] ? S.scache[cur_t][j] - 1 : 3u;
           S.sdelta[nxt][k] = S.sdelta[cur_t][j];
           S.sunit[nxt][k] = S.sunit[cur_t][j];
+          S.stoff[nxt][k] = S.stoff[cur_t][j];
+          S.slen[nxt][k] = S.slen[cur_t][j];
           ns = (uint8_t)k;
         }
       }
