@@ -136,6 +136,8 @@ def main():
     ms_per_step = elapsed * 1000.0 / a.steps
     value = job_mbps(a.bytes, world, a.steps, elapsed)  # MB/s, whole job
 
+    if mode == "stream" and rank != 0:
+        stream_parity(None, d_in, a, world)  # sends this rank's shard to rank 0
     if rank == 0:
         ratio = out_bytes / a.bytes
         rho = stats["rle_bytes"] / a.bytes
@@ -177,20 +179,7 @@ def main():
             "gen_s": round(gen_s, 1),
         }
         if mode == "stream" and last_stream[0] is not None:
-            # structure of the gathered stream (outside the timed region): every block header and
-            # the end-of-stream magic where the bit count puts them (bzg_find_magics)
-            from bzip2_amd import shard
-
-            fs = last_stream[0].to("cuda")  # on the host under the gloo rehearsal
-            found = B.find_magics(fs.data_ptr(), fs.numel())
-            heads = [o for o, k in found if k == 0]
-            meta = shard.last_meta
-            result["stream_check"] = {
-                "bytes": fs.numel(), "blocks": meta["blocks"], "block_magics_found": len(heads),
-                "first_block_at_bit_32": bool(heads) and heads[0] == 32,
-                "eos_at_payload_end": (meta["bits"], 1) in found,
-                "ok": bool(heads) and heads[0] == 32 and len(heads) >= meta["blocks"] and (meta["bits"], 1) in found,
-            }
+            result["stream_check"] = stream_parity(last_stream[0], d_in, a, world)
         pmc = pmc_traffic(a)
         if pmc is not None:
             rl = result["roofline"]
@@ -209,6 +198,39 @@ def main():
     if dist:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+
+
+def stream_parity(stream, d_in, a, world):
+    """Outside the timed region: the sharded stream must equal, byte for byte, the plain
+    single-device bzg_compress_device call over the whole input (all shards gathered on rank 0),
+    i.e. the output does not depend on the rank count (SURVEY.md 4.3 determinism)."""
+    import torch.distributed as dist
+
+    rank = dist.get_rank() if world > 1 else 0
+    gloo = world > 1 and dist.get_backend() == "gloo"
+    if rank != 0:
+        dist.send(d_in.cpu() if gloo else d_in, 0)
+        return None
+    n = a.bytes
+    full = torch.empty(n * world, dtype=torch.uint8, device="cuda")
+    full[:n].copy_(d_in)
+    for r in range(1, world):
+        if gloo:
+            tmp = torch.empty(n, dtype=torch.uint8)
+            dist.recv(tmp, r)
+            full[r * n:(r + 1) * n].copy_(tmp)
+        else:
+            dist.recv(full[r * n:(r + 1) * n], r)
+    cap = B.bound(n * world)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    nb, _, _ = B.compress_device(full.data_ptr(), n * world, a.level, out.data_ptr(), cap)
+    torch.cuda.synchronize()
+    s = stream.to("cuda")
+    eq = nb == s.numel() and bool(torch.equal(out[:nb], s))
+    del full, out
+    torch.cuda.empty_cache()
+    return {"bytes": int(s.numel()), "ranks": world, "equals_single_device_stream": eq,
+            "against": f"bzg_compress_device over all {n * world} B on one device"}
 
 
 def time_device(d, n, level, d_out, cap, steps, warmup=1):

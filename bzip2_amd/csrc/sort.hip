@@ -992,7 +992,7 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
         const uint64_t mates = match_byte(cls, live);
         const uint32_t r = (uint32_t)__popcll(mates & lanemask_lt());
         B.sa[s0 + pos + r] = v;
-        if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, (uint32_t)__popcll(mates), unit, d << kGrpDepthShift};
+        if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, (uint32_t)__popcll(mates), unit, grp_flags(0u, d, 1u)};
       }
       break;
     }
@@ -1194,7 +1194,7 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
               rank += q < p;
             }
           B.sa[g.start + pos[r] + rank] = v[r];
-          if (rank == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + pos[r], cnt, g.unit, depth << kGrpDepthShift};
+          if (rank == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + pos[r], cnt, g.unit, grp_flags(0u, depth, 2u)};
         }
       break;
     }
@@ -1532,14 +1532,34 @@ __global__ void __launch_bounds__(kT) k_fb_group_isa(const Grp* __restrict__ L0,
 }
 
 // ISA of every slot of the listed units from the (complete, primary) SA: every rotation's own
-// slot; deep groups' members are overwritten afterwards by k_fb_group_isa.
-__global__ void __launch_bounds__(kT) k_fb_isa_all(const uint32_t* __restrict__ ulist, const Unit* __restrict__ units,
-                                                   SortBufs B) {
-  const Unit U = units[ulist[blockIdx.y]];
-  const uint32_t q = blockIdx.x * kT + threadIdx.x;
+// slot; deep groups' members are overwritten afterwards by k_fb_group_isa.  The ISA stores of a
+// unit scatter over its whole range, so all workgroups of unit u run on one XCD (hardware
+// workgroup w goes to XCD w % 8): its L2 merges the unit's scattered stores into full lines.
+// Grid: 8 * ceil(nu / 8) * chunks workgroups.
+__global__ void __launch_bounds__(kT) k_fb_isa_all(const uint32_t* __restrict__ ulist, uint32_t nu, uint32_t chunks,
+                                                   const Unit* __restrict__ units, SortBufs B) {
+  const uint32_t xcd = blockIdx.x % kNumXcd, rest = blockIdx.x / kNumXcd;
+  const uint32_t ui = (rest / chunks) * kNumXcd + xcd, ch = rest % chunks;
+  if (ui >= nu) return;
+  const Unit U = units[ulist[ui]];
+  const uint32_t q = ch * kT + threadIdx.x;
   if (q >= U.len) return;
   const uint32_t v = B.sa[U.sbase + q];
   B.isa[U.sbase + v] = U.sbase + q;
+}
+
+// BWT bytes of the slots of the deep groups (everything else was written when its rotation
+// was ordered), for aperiodic units; one workgroup per deep group.
+__global__ void __launch_bounds__(kT) k_deep_out(const Grp* __restrict__ L0, const Unit* __restrict__ units,
+                                                 const uint32_t* __restrict__ sa, const uint8_t* __restrict__ text,
+                                                 uint8_t* __restrict__ bwt) {
+  const Grp g = L0[blockIdx.x];
+  const Unit U = units[g.unit];
+  if (U.k != 1) return;  // periodic roots: the whole last column is written afterwards
+  for (uint32_t e = threadIdx.x; e < g.size; e += kT) {
+    const uint32_t v = sa[g.start + e];
+    bwt[U.toff + g.start + e - U.sbase] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
+  }
 }
 
 // Last column of the listed units from the SA (periodic roots repeated k times).
@@ -1823,9 +1843,26 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     uint32_t* ulist = ws.u32("sort_ulist", fb_units.size() + 16);
     HIP_OK(hipMemcpyAsync(ulist, fb_units.data(), 4 * fb_units.size(), hipMemcpyHostToDevice, st));
     Grp* L0 = ws.typed<Grp>("sort_L0", n_deep + 16);
+    if (debug) {  // sizes by source (cache bits of the deep entries: 1 k_tiny, 2 bsort tail, else S1)
+      std::vector<Grp> hd(n_deep);
+      HIP_OK(hipMemcpyAsync(hd.data(), O.deep, sizeof(Grp) * n_deep, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      uint64_t h[3][4] = {};
+      for (const Grp& g : hd) {
+        const uint32_t src = grp_cache(g) == 1 ? 0 : grp_cache(g) == 2 ? 1 : 2;
+        h[src][std::min<uint32_t>(g.size, 3)]++;
+      }
+      for (int k = 0; k < 3; k++)
+        fprintf(stderr, "[bzg sort S3] deep from %s: size0 %llu size1 %llu size2 %llu size3+ %llu\n",
+                k == 0 ? "tiny" : k == 1 ? "tail" : "s1", (unsigned long long)h[k][0], (unsigned long long)h[k][1],
+                (unsigned long long)h[k][2], (unsigned long long)h[k][3]);
+    }
     k_fb_copy<<<n_deep, kT, 0, st>>>(O.deep, L0, B);
     HIP_OK(hipGetLastError());
-    k_fb_isa_all<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B);
+    {
+      const uint32_t nu = (uint32_t)fb_units.size(), chunks = ceil_div(flen, kT);
+      k_fb_isa_all<<<kNumXcd * ceil_div(nu, kNumXcd) * chunks, kT, 0, st>>>(ulist, nu, chunks, units, B);
+    }
     HIP_OK(hipGetLastError());
     k_fb_group_isa<<<n_deep, kT, 0, st>>>(L0, B);
     HIP_OK(hipGetLastError());
@@ -1845,7 +1882,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
               (unsigned long long)hist[4], fb_units.size(), h0);
     }
     doubling_sort(ws, B, L0, n_deep, h0, &dbl_iters, &dbl_elems, st);
-    k_unit_out<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B.sa, r.blk, bwt);
+    k_deep_out<<<n_deep, kT, 0, st>>>(L0, units, B.sa, r.blk, bwt);
     HIP_OK(hipGetLastError());
     k_rank0_isa<<<grid(fb_units.size()), kT, 0, st>>>(ulist, (uint32_t)fb_units.size(), units, B.isa, rank0);
     HIP_OK(hipGetLastError());

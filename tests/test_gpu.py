@@ -615,6 +615,88 @@ def test_sharded_stream_on_device_large():
     assert out["text"] == expected(datagen.text(60_000_000, 0x5EED0003), 9)
 
 
+def _gpu_shard_1g_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+
+    from bzip2_amd import shard as S
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 1_000_000_000
+        data = datagen.text(n, 0x5EED0003)  # every rank generates the stream (seconds, in parallel)
+        bnd = [n * r // world for r in range(world + 1)]
+        t = torch.frombuffer(bytearray(data[bnd[rank]:bnd[rank + 1]]), dtype=torch.uint8).to("cuda")
+        res = S.compress_sharded(t, bnd[rank], n, 9)
+        torch.cuda.synchronize()
+        if rank == 0:
+            got = res.cpu().numpy().tobytes()
+            want = expected(data, 9)  # the reference build, about 35 s of one core
+            out["len"] = len(got)
+            out["eq"] = got == want
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_stream_1gb_config3():
+    """BASELINE config 3's path at its full size: 1e9 bytes of enwik9-class text at -9 sharded
+    over three ranks (gloo, all on this box's one GPU) through compress_sharded; rank 0's
+    gathered stream equals the reference's BZ2_bzBuffToBuffCompress of the whole 1e9 bytes."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_gpu_shard_1g_worker, args=(3, port, out), nprocs=3, join=True)
+    assert out["eq"], out["len"]
+
+
+def _nccl_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+
+    from bzip2_amd import shard as S
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    try:
+        data = datagen.text(30_000_000, 0x5EED0004) + b"x" * 5_000_000
+        n = len(data)
+        bnd = [n * r // world for r in range(world + 1)]
+        t = torch.frombuffer(bytearray(data[bnd[rank]:bnd[rank + 1]]), dtype=torch.uint8).to("cuda")
+        res = S.compress_sharded(t, bnd[rank], n, 9)  # device tensors through RCCL send/recv
+        torch.cuda.synchronize()
+        if rank == 0:
+            out["eq"] = res.cpu().numpy().tobytes() == expected(data, 9)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not __import__("torch").cuda.is_available() or __import__("torch").cuda.device_count() < 2,
+                    reason="the RCCL path needs two GPUs (one rank per GPU)")
+def test_sharded_stream_nccl_two_gpus():
+    """compress_sharded's device-tensor branch (RCCL send/recv/all_gather into slices of the
+    result), one rank per GPU."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_nccl_worker, args=(2, port, out), nprocs=2, join=True)
+    assert out["eq"]
+
+
 # ------------------------------------------------------------------ block boundaries (SURVEY.md 8f row 3)
 def test_find_magics_matches_scan():
     """bzg_find_magics against the CPU restatement of the bzip2recover scan (tests/magic_ref.py)
