@@ -58,6 +58,7 @@ struct SortOut {
   uint32_t* rank0;   // slot of rotation 0 relative to its unit
   Grp* deep;         // groups left for the doubling fallback
   uint32_t* n_deep;
+  unsigned long long* dbg;  // BZG_DEBUG counters (null otherwise)
 };
 
 struct ClsLists {
@@ -782,9 +783,14 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
   __syncthreads();
   const Unit* __restrict__ units = B.units;
   uint32_t cur_t = 0;
+  uint32_t npass = 0, nact = 0;
   for (;;) {
     const uint32_t nb = S.nbig[cur_t];
     if (nb == 0) break;
+    if (O.dbg && tid == 0) {
+      npass++;
+      for (uint32_t j = 0; j < nb; j++) nact += S.ssize[cur_t][j];
+    }
     for (uint32_t b = tid; b < nb * 256; b += kPT) S.cnt[b] = 0;
     __syncthreads();
     // ---- count: every element of a big segment takes its next character
@@ -918,6 +924,12 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
     }
     __syncthreads();
     cur_t = nxt;
+  }
+  if (O.dbg && tid == 0) {
+    atomicAdd(&O.dbg[0], 1ull);
+    atomicAdd(&O.dbg[1], (unsigned long long)npass);
+    atomicAdd(&O.dbg[2], (unsigned long long)nact);
+    atomicMax(&O.dbg[3], (unsigned long long)npass);
   }
 }
 
@@ -1517,18 +1529,24 @@ __global__ void k_fb_flag(const Grp* __restrict__ D, uint32_t n, uint32_t* __res
 
 // Deep groups whose data is in the alternate buffer move to the primary SA; the doubling
 // list gets the groups with their flags reset.  One workgroup per group.
-__global__ void __launch_bounds__(kT) k_fb_copy(const Grp* __restrict__ D, Grp* __restrict__ L0, SortBufs B) {
-  const Grp gr = D[blockIdx.x];
-  if (gr.flags & kGrpAlt)
-    for (uint32_t e = threadIdx.x; e < gr.size; e += kT) B.sa[gr.start + e] = B.sa2[gr.start + e];
-  if (threadIdx.x == 0) L0[blockIdx.x] = Grp{gr.start, gr.size, gr.unit, 0};
+// (The per-group kernels below stride over the groups: one workgroup per group could exceed
+// the 2^32 threads a launch may hold when there are tens of millions of deep groups.)
+__global__ void __launch_bounds__(kT) k_fb_copy(const Grp* __restrict__ D, uint32_t n, Grp* __restrict__ L0, SortBufs B) {
+  for (uint32_t g = blockIdx.x; g < n; g += gridDim.x) {
+    const Grp gr = D[g];
+    if (gr.flags & kGrpAlt)
+      for (uint32_t e = threadIdx.x; e < gr.size; e += kT) B.sa[gr.start + e] = B.sa2[gr.start + e];
+    if (threadIdx.x == 0) L0[g] = Grp{gr.start, gr.size, gr.unit, 0};
+  }
 }
 
 // Members of a deep group take the group's first slot as rank (after k_fb_isa_all).
-__global__ void __launch_bounds__(kT) k_fb_group_isa(const Grp* __restrict__ L0, SortBufs B) {
-  const Grp gr = L0[blockIdx.x];
-  const uint32_t sb = B.units[gr.unit].sbase;
-  for (uint32_t e = threadIdx.x; e < gr.size; e += kT) B.isa[sb + B.sa[gr.start + e]] = gr.start;
+__global__ void __launch_bounds__(kT) k_fb_group_isa(const Grp* __restrict__ L0, uint32_t n, SortBufs B) {
+  for (uint32_t g = blockIdx.x; g < n; g += gridDim.x) {
+    const Grp gr = L0[g];
+    const uint32_t sb = B.units[gr.unit].sbase;
+    for (uint32_t e = threadIdx.x; e < gr.size; e += kT) B.isa[sb + B.sa[gr.start + e]] = gr.start;
+  }
 }
 
 // ISA of every slot of the listed units from the (complete, primary) SA: every rotation's own
@@ -1550,15 +1568,17 @@ __global__ void __launch_bounds__(kT) k_fb_isa_all(const uint32_t* __restrict__ 
 
 // BWT bytes of the slots of the deep groups (everything else was written when its rotation
 // was ordered), for aperiodic units; one workgroup per deep group.
-__global__ void __launch_bounds__(kT) k_deep_out(const Grp* __restrict__ L0, const Unit* __restrict__ units,
+__global__ void __launch_bounds__(kT) k_deep_out(const Grp* __restrict__ L0, uint32_t n, const Unit* __restrict__ units,
                                                  const uint32_t* __restrict__ sa, const uint8_t* __restrict__ text,
                                                  uint8_t* __restrict__ bwt) {
-  const Grp g = L0[blockIdx.x];
-  const Unit U = units[g.unit];
-  if (U.k != 1) return;  // periodic roots: the whole last column is written afterwards
-  for (uint32_t e = threadIdx.x; e < g.size; e += kT) {
-    const uint32_t v = sa[g.start + e];
-    bwt[U.toff + g.start + e - U.sbase] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
+  for (uint32_t gi = blockIdx.x; gi < n; gi += gridDim.x) {
+    const Grp g = L0[gi];
+    const Unit U = units[g.unit];
+    if (U.k != 1) continue;  // periodic roots: the whole last column is written afterwards
+    for (uint32_t e = threadIdx.x; e < g.size; e += kT) {
+      const uint32_t v = sa[g.start + e];
+      bwt[U.toff + g.start + e - U.sbase] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
+    }
   }
 }
 
@@ -1632,6 +1652,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   O.bwt = bwt;
   O.rank0 = rank0;
   O.deep = ws.typed<Grp>("sort_deep", S / 2 + nb + 16);
+  O.dbg = nullptr;
+  if (getenv("BZG_DEBUG")) {
+    O.dbg = reinterpret_cast<unsigned long long*>(ws.u32("sort_dbg", 16));
+    HIP_OK(hipMemsetAsync(O.dbg, 0, 64, st));
+  }
   // counters: 0..7 class counts (init), 8..16 class bounds + total, 17 tiles, 18 packed total,
   // 19 n_deep, 20 min depth
   uint32_t* cnt = ws.u32("sort_cnt", 64);  // counters: see below; 24..29 S2 class sizes
@@ -1746,6 +1771,12 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     std::swap(cur6, nxt6);
     std::swap(cur7, nxt7);
   }
+  if (debug && O.dbg) {
+    unsigned long long d[4];
+    HIP_OK(hipMemcpyAsync(d, O.dbg, sizeof(d), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    fprintf(stderr, "[bzg sort S1] k_s1p tiles=%llu passes=%llu (max %llu) element-passes=%llu\n", d[0], d[1], d[3], d[2]);
+  }
   // ---- S2: every size class
   if (debug)
     fprintf(stderr, "[bzg sort S2] buckets by class: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", ncls[0],
@@ -1857,14 +1888,14 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
                 k == 0 ? "tiny" : k == 1 ? "tail" : "s1", (unsigned long long)h[k][0], (unsigned long long)h[k][1],
                 (unsigned long long)h[k][2], (unsigned long long)h[k][3]);
     }
-    k_fb_copy<<<n_deep, kT, 0, st>>>(O.deep, L0, B);
+    k_fb_copy<<<std::min<uint32_t>(n_deep, 1u << 16), kT, 0, st>>>(O.deep, n_deep, L0, B);
     HIP_OK(hipGetLastError());
     {
       const uint32_t nu = (uint32_t)fb_units.size(), chunks = ceil_div(flen, kT);
       k_fb_isa_all<<<kNumXcd * ceil_div(nu, kNumXcd) * chunks, kT, 0, st>>>(ulist, nu, chunks, units, B);
     }
     HIP_OK(hipGetLastError());
-    k_fb_group_isa<<<n_deep, kT, 0, st>>>(L0, B);
+    k_fb_group_isa<<<std::min<uint32_t>(n_deep, 1u << 16), kT, 0, st>>>(L0, n_deep, B);
     HIP_OK(hipGetLastError());
     if (debug) {
       std::vector<Grp> hd(n_deep);
@@ -1882,7 +1913,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
               (unsigned long long)hist[4], fb_units.size(), h0);
     }
     doubling_sort(ws, B, L0, n_deep, h0, &dbl_iters, &dbl_elems, st);
-    k_deep_out<<<n_deep, kT, 0, st>>>(L0, units, B.sa, r.blk, bwt);
+    k_deep_out<<<std::min<uint32_t>(n_deep, 1u << 16), kT, 0, st>>>(L0, n_deep, units, B.sa, r.blk, bwt);
     HIP_OK(hipGetLastError());
     k_rank0_isa<<<grid(fb_units.size()), kT, 0, st>>>(ulist, (uint32_t)fb_units.size(), units, B.isa, rank0);
     HIP_OK(hipGetLastError());

@@ -189,6 +189,27 @@ def test_bwt_long_repeats_fallback():
         assert orig[b] == o, b
 
 
+def test_many_deep_groups_repeats():
+    """Enwik-like long repeats at scale: 400 MB of text with a quarter overwritten by copies of
+    earlier passages (2-200 kB) gives tens of millions of groups still tied after the string
+    passes (more than one launch of one workgroup per group could hold): the doubling fallback
+    must order every one of them (the whole stream against the reference)."""
+    torch = pytest.importorskip("torch")
+    import bench
+
+    n = 400_000_000
+    d = torch.frombuffer(bytearray(datagen.text(n, 0x5EED0007)), dtype=torch.uint8).to("cuda")
+    bench.add_repeats(d, 0.25)
+    data = d.cpu().numpy().tobytes()
+    cap = B.bound(n)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    nb, _, _ = B.compress_device(d.data_ptr(), n, 9, out.data_ptr(), cap)
+    torch.cuda.synchronize()
+    got = out[:nb].cpu().numpy().tobytes()
+    del d, out
+    assert got == expected(data, 9)
+
+
 def test_long_repeats_streams():
     blocks, _ = _long_repeat_blocks()
     for level in (1, 9):
