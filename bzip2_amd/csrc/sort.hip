@@ -1913,7 +1913,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
               (unsigned long long)hist[4], fb_units.size(), h0);
     }
     doubling_sort(ws, B, L0, n_deep, h0, &dbl_iters, &dbl_elems, st);
-    k_deep_out<<<std::min<uint32_t>(n_deep, 1u << 16), kT, 0, st>>>(L0, n_deep, units, B.sa, r.blk, bwt);
+    if (getenv("BZG_FULL_UNIT_OUT")) {
+      k_unit_out<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B.sa, r.blk, bwt);
+    } else {
+      k_deep_out<<<std::min<uint32_t>(n_deep, 1u << 16), kT, 0, st>>>(L0, n_deep, units, B.sa, r.blk, bwt);
+    }
     HIP_OK(hipGetLastError());
     k_rank0_isa<<<grid(fb_units.size()), kT, 0, st>>>(ulist, (uint32_t)fb_units.size(), units, B.isa, rank0);
     HIP_OK(hipGetLastError());
