@@ -122,7 +122,8 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
   return xcd < rem ? xcd * (per + 1) + j : rem * (per + 1) + (xcd - rem) * per + j;
 }
 
-// Lanes of the wave whose 8-bit value equals this lane's (among active lanes).
+// Lanes of the wave whose 8-bit value equals this lane's, among `active`.  Every lane of
+// `active` must execute the call (lanes outside the ballots would match a value of zero).
 __device__ __forceinline__ uint64_t match_byte(uint32_t d, uint64_t active) {
   uint64_t m = active;
 #pragma unroll

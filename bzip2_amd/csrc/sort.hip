@@ -1000,8 +1000,11 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
     const uint64_t live = __ballot(!done);
     if (live == 0) break;
     if (d >= B.dwave) {  // still tied after B.dwave characters: leave to the doubling fallback
+      // buckets of one wave reach the depth limit at different steps: only the lanes in this
+      // branch take part in match_byte's ballots, so restrict its candidates to them
+      const uint64_t here = __ballot(true);
       if (!done) {
-        const uint64_t mates = match_byte(cls, live);
+        const uint64_t mates = match_byte(cls, live & here);
         const uint32_t r = (uint32_t)__popcll(mates & lanemask_lt());
         B.sa[s0 + pos + r] = v;
         if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, (uint32_t)__popcll(mates), unit, grp_flags(0u, d, 1u)};
