@@ -712,6 +712,7 @@ struct S1pLds {
   uint32_t sstart[2][kPSeg], ssize[2][kPSeg], sdepth[2][kPSeg], scache[2][kPSeg], sdelta[2][kPSeg], sunit[2][kPSeg];
   uint32_t stoff[2][kPSeg], slen[2][kPSeg];  // text offset / length of the segment's unit
   uint32_t segb[kPSeg];             // scan value at each segment's first bin
+  uint32_t ccls[8];                 // S2 groups of the tile per size class; [7] = records
   uint32_t nbig[2];
   uint32_t sh[kPT / 64];
 };
@@ -727,14 +728,24 @@ __device__ __forceinline__ void cls_append(const ClsLists& C, uint32_t* __restri
 }
 
 __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
-                                            const uint32_t* __restrict__ last, SortBufs B, SortOut O, ClsLists C,
-                                            uint32_t* __restrict__ app) {
+                                            const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
+                                            SortBufs B, SortOut O, uint32_t* __restrict__ rec,
+                                            uint32_t* __restrict__ nrec, uint32_t* __restrict__ ccnt, uint32_t nTot,
+                                            uint32_t ibase, uint32_t nT) {
   __shared__ S1pLds S;
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const uint32_t i0 = first[t];
-  if (i0 == 0xffffffffu) return;
-  const uint32_t ni = min(last[t], i0 + kSGrp) - i0;
   const uint32_t tid = threadIdx.x;
+  if (i0 == 0xffffffffu) {
+    if (tid < 6) ccnt[(size_t)tid * nTot + ibase + t] = 0;
+    if (tid == 0) nrec[t] = 0;
+    return;
+  }
+  const uint32_t ni = min(last[t], i0 + kSGrp) - i0;
+  if (tid < 8) S.ccls[tid] = 0;
+  // S2 groups leave as 2-word records (slot; unit:16 | depth:7 | size:9) in the tile's own part
+  // of `rec` (a tile of n rotations has at most n / 2 groups), for k_s1p_emit
+  uint32_t* trec = rec + P[i0];
   // ---- load the tile's groups: segment tables 0 and every element's rotation and key
   if (tid < ni) {
     const Grp g = SG[i0 + tid];
@@ -904,27 +915,27 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
         B.sa[slot] = vv[i];
       }
     }
-    // one group record per bin of 2.. rotations (S2 class list, or deep)
-    for (uint32_t b0 = 0; b0 < nb * 256; b0 += kPT) {
-      const uint32_t b = b0 + tid;
-      const bool in = b < nb * 256;
-      const uint32_t c = in ? S.cnt[b] : 0u;
-      const bool grp = in && c >= 2 && S.nseg[b] == 0xfe;
+    // one group record per bin of 2.. rotations (S2 record, or deep)
+    for (uint32_t b = tid; b < nb * 256; b += kPT) {
+      const uint32_t c = S.cnt[b];
+      if (c < 2 || S.nseg[b] != 0xfe) continue;
       const uint32_t j = b >> 8;
-      Grp g{0, 0, 0, 0};
-      uint32_t cl = 0xffu;
-      if (grp) {
-        const uint32_t d = S.sdepth[cur_t][j] + 1;
-        g = Grp{S.cur[b] + S.sdelta[cur_t][j], c, S.sunit[cur_t][j], grp_flags(0u, d, 0u)};
-        cl = c <= kBig ? size_cls(c) : kClsDeep;
+      const uint32_t d = S.sdepth[cur_t][j] + 1, slot = S.cur[b] + S.sdelta[cur_t][j];
+      if (c <= kBig) {
+        atomicAdd(&S.ccls[size_cls(c)], 1u);
+        const uint32_t x = atomicAdd(&S.ccls[7], 1u);
+        trec[2 * x] = slot;
+        trec[2 * x + 1] = (S.sunit[cur_t][j] << 16) | (d << 9) | c;
+      } else {  // still big at kDLds characters (rare): to the doubling fallback
+        O.deep[atomicAdd(O.n_deep, 1u)] = Grp{slot, c, S.sunit[cur_t][j], grp_flags(0u, d, 0u)};
       }
-      cls_append(C, app, grp && cl < 6u, cl, g);
-      const uint32_t dp = wave_append(O.n_deep, grp && cl == kClsDeep);
-      if (grp && cl == kClsDeep) O.deep[dp] = g;
     }
     __syncthreads();
     cur_t = nxt;
   }
+  __syncthreads();
+  if (tid < 6) ccnt[(size_t)tid * nTot + ibase + t] = S.ccls[tid];
+  if (tid == 0) nrec[t] = S.ccls[7];
   if (O.dbg && tid == 0) {
     atomicAdd(&O.dbg[0], 1ull);
     atomicAdd(&O.dbg[1], (unsigned long long)npass);
@@ -933,10 +944,31 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
   }
 }
 
-// app[c] = first free index of S2 class list c after this pass's tiled emissions
-__global__ void k_app_init(const uint32_t* __restrict__ bounds, ClsLists C, uint32_t* __restrict__ app) {
-  const uint32_t c = threadIdx.x;
-  if (c < 6) app[c] = C.base[c] + (bounds[c + 1] - bounds[c]);
+// The records of k_s1p into the S2 class lists (class-major offsets from cscan); one wave per
+// tile (the order inside a tile is immaterial).
+__global__ void __launch_bounds__(kT) k_s1p_emit(const uint32_t* __restrict__ first, const uint32_t* __restrict__ P,
+                                                 uint32_t nT, const uint32_t* __restrict__ rec,
+                                                 const uint32_t* __restrict__ nrec, const uint32_t* __restrict__ cscan,
+                                                 uint32_t nTot, uint32_t ibase, ClsLists C) {
+  __shared__ uint32_t Wcc[kT / 64][8];
+  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
+  const uint32_t t = blockIdx.x * (kT / 64) + wv;
+  if (t >= nT) return;
+  const uint32_t i0 = first[t];
+  if (i0 == 0xffffffffu) return;
+  uint32_t* cc = Wcc[wv];
+  if (lane < 8) cc[lane] = 0;
+  wave_sync();
+  const uint32_t* trec = rec + P[i0];
+  const uint32_t m = nrec[t];
+  for (uint32_t x = lane; x < m; x += 64) {
+    const uint32_t slot = trec[2 * x], w = trec[2 * x + 1];
+    const uint32_t size = w & 511u, depth = (w >> 9) & 127u, unit = w >> 16;
+    const uint32_t cl = size_cls(size);
+    const uint32_t q = atomicAdd(&cc[cl], 1u);
+    C.l[cl][C.base[cl] + cscan[(size_t)cl * nTot + ibase + t] - cscan[(size_t)cl * nTot] + q] =
+        Grp{slot, size, unit, grp_flags(0u, depth, 0u)};
+  }
 }
 
 // out[c] = start of class c in the class-major scan (c < kNCls), out[kNCls] = total.
@@ -1675,7 +1707,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* first = ws.u32("sort_first", max_ptiles);
   uint32_t* last = ws.u32("sort_last", max_ptiles);
   uint32_t* nrec = ws.u32("sort_nrec", max_ptiles);
-  uint32_t* srec = ws.u32("sort_rec", S / 2 + 64);  // packed-pass bucket records
+  uint32_t* srec = ws.u32("sort_rec", S + 64);  // packed-pass group records (k_s1p: 2 words per group)
   uint32_t* scratch =
       ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[6])) + 64);
   uint32_t hc[48];
@@ -1717,8 +1749,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     read_counters();
     const uint32_t ntl = n7 ? hc[17] : 0;
     const uint32_t nT = n6 ? ceil_div(hc[18], kSG) : 0;
-    // class-major scan over the tiled groups (and, on the k_s1s path, the packed tiles)
-    const uint32_t nTot = use_s1p ? n7 : n7 + nT;
+    // class-major scan over the tiled groups and the packed tiles (tile t at index n7 + t)
+    const uint32_t nTot = n7 + nT;
     if (debug) {
       fprintf(stderr, "[bzg sort S1] pass %d: tiled groups=%u tiles=%u | packed groups=%u elems=%u tiles=%u\n", passes,
               n7, ntl, n6, n6 ? hc[18] : 0, nT);
@@ -1728,10 +1760,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipMemsetAsync(first, 0xff, (size_t)nT * 4, st));
       k_tile_first<<<grid(n6), kT, 0, st>>>(P, n6, first, last);
       HIP_OK(hipGetLastError());
-      if (!use_s1p) {
+      if (use_s1p)
+        k_s1p<<<nT, kPT, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7, nT);
+      else
         k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
-        HIP_OK(hipGetLastError());
-      }
+      HIP_OK(hipGetLastError());
     }
     if (n7) {
       k_s1_hist<<<ntl, kT, 0, st>>>(cur7, n7, TP, B, hist);
@@ -1739,12 +1772,9 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_s1_off<<<n7, kT, 0, st>>>(cur7, nTot, TP, hist, tot, ccnt, O.deep, O.n_deep);
       HIP_OK(hipGetLastError());
     }
-    HIP_OK(hipMemsetAsync(cnt + 8, 0, 9 * 4, st));
-    if (nTot) {
-      scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * nTot, cnt + 16, scratch, st);
-      k_cls_bounds<<<1, 64, 0, st>>>(ccnt, nTot, cnt + 16, cnt + 8);
-      HIP_OK(hipGetLastError());
-    }
+    scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * nTot, cnt + 16, scratch, st);
+    k_cls_bounds<<<1, 64, 0, st>>>(ccnt, nTot, cnt + 16, cnt + 8);
+    HIP_OK(hipGetLastError());
     ClsLists Cp = C;
     for (int c = 0; c < 6; c++) Cp.base[c] = ncls[c];
     Cp.l[6] = nxt6;
@@ -1756,19 +1786,15 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_s1_single<<<n7, kT, 0, st>>>(cur7, B, tot);
       HIP_OK(hipGetLastError());
     }
-    if (nT && !use_s1p) {
-      k_s1s_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(cur6, first, last, P, nT, O, srec, nrec, ccnt, nTot, n7, Cp);
-      HIP_OK(hipGetLastError());
-    }
-    // S2 lists after the tiled emissions; the packed tiles append behind them
-    k_app_init<<<1, 64, 0, st>>>(cnt + 8, Cp, cnt + 32);
-    HIP_OK(hipGetLastError());
-    if (nT && use_s1p) {
-      k_s1p<<<nT, kPT, 0, st>>>(cur6, first, last, B, O, Cp, cnt + 32);
+    if (nT) {
+      if (use_s1p)
+        k_s1p_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(first, P, nT, srec, nrec, ccnt, nTot, n7, Cp);
+      else
+        k_s1s_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(cur6, first, last, P, nT, O, srec, nrec, ccnt, nTot, n7, Cp);
       HIP_OK(hipGetLastError());
     }
     read_counters();
-    for (int c = 0; c < 6; c++) ncls[c] = hc[32 + c];
+    for (int c = 0; c < 6; c++) ncls[c] += hc[8 + c + 1] - hc[8 + c];
     n6 = hc[8 + 7] - hc[8 + 6];
     n7 = hc[8 + 8] - hc[8 + 7];
     std::swap(cur6, nxt6);
