@@ -737,7 +737,7 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
   const uint32_t i0 = first[t];
   const uint32_t tid = threadIdx.x;
   if (i0 == 0xffffffffu) {
-    if (tid < 6) ccnt[(size_t)tid * nTot + ibase + t] = 0;
+    if (tid < (uint32_t)kNCls) ccnt[(size_t)tid * nTot + ibase + t] = 0;
     if (tid == 0) nrec[t] = 0;
     return;
   }
@@ -934,7 +934,8 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
     cur_t = nxt;
   }
   __syncthreads();
-  if (tid < 6) ccnt[(size_t)tid * nTot + ibase + t] = S.ccls[tid];
+  // every class of the scan (6 and 7 stay empty: packed groups end in S2 or the deep list)
+  if (tid < (uint32_t)kNCls) ccnt[(size_t)tid * nTot + ibase + t] = tid < 6 ? S.ccls[tid] : 0u;
   if (tid == 0) nrec[t] = S.ccls[7];
   if (O.dbg && tid == 0) {
     atomicAdd(&O.dbg[0], 1ull);
