@@ -14,7 +14,7 @@
 #include <thread>
 
 #include "../../include/bzg.h"
-#include "resolver.h"
+#include "tieorder.h"
 #include "stages.h"
 
 #define BZ_OK 0
