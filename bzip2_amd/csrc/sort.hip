@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, uint3
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[kk[i] >> 24], 1u);
+    (void)lds_count_rank<8>(h, kk[i] >> 24, lo + i * kT + threadIdx.x < hi);
   __syncthreads();
   hist[(size_t)t * 256 + threadIdx.x] = h[threadIdx.x];
 }
@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, ui
   uint32_t rk[kPerT];
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    if (lo + i * kT + threadIdx.x < hi) rk[i] = atomicAdd(&cnt[kk[i] >> 24], 1u);
+    rk[i] = lds_count_rank<8>(cnt, kk[i] >> 24, lo + i * kT + threadIdx.x < hi);
   __syncthreads();
   {
     const uint32_t c = cnt[d];
@@ -567,7 +567,7 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
   s1s_load<true, false>(S, B, ni, n, vv, kk, jj);
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++)
-    if (i * kTS + threadIdx.x < n) jj[i] = atomicAdd(&S.cnt[jj[i] * 256 + (kk[i] >> 24)], 1u) | (jj[i] << 16);
+    jj[i] = lds_count_rank<12>(S.cnt, jj[i] * 256 + (kk[i] >> 24), i * kTS + threadIdx.x < n) | (jj[i] << 16);
   __syncthreads();
   // tile-relative bucket bases: exclusive scan over the (group, digit) bins
   {
@@ -831,7 +831,10 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
         const uint32_t len = S.slen[cur_t][sg[i]];
         kk[i] = q[i] + 4 <= len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.stoff[cur_t][sg[i]], len, q[i]);
       }
-      if (sg[i] != 0xff) rk[i] = atomicAdd(&S.cnt[sg[i] * 256u + (kk[i] >> 24)], 1u);
+    }
+#pragma unroll
+    for (int i = 0; i < (int)kPPer; i++) {
+      rk[i] = lds_count_rank<13>(S.cnt, (sg[i] == 0xff ? 0u : sg[i]) * 256u + (kk[i] >> 24), sg[i] != 0xff);
     }
     __syncthreads();
     // ---- bins -> tile positions: one exclusive scan over all bins (segments are contiguous in

@@ -111,7 +111,8 @@ def test_decoder_streaming_small_chunks(lib):
 
 
 def test_periodic_resolver_matches_reference(lib):
-    """A5: origPtr of exactly periodic blocks replays the reference's divsufsort tie order."""
+    """A5: origPtr of exactly periodic blocks (bzip2_amd/csrc/tieorder.cpp) against the
+    reference build: the SURVEY.md 8a KATs and random periodic blocks."""
     from tests import oracles as O
     if not O.has_ref():
         pytest.skip("oracle/_ref not built")
@@ -126,6 +127,33 @@ def test_periodic_resolver_matches_reference(lib):
         cases.append(w * rng.randint(2, 300))
     for blk in cases:
         assert B.periodic_origptr(blk) == O.ref_blocksort(blk)[1], (blk[:12], len(blk))
+
+
+def test_periodic_origptr_fuzz(lib):
+    """5,000 random periodic blocks across the regimes of the tie model: short and long roots,
+    2..60,000 copies, one-B*-per-period single-byte-run roots up to full 900 kB blocks (merge
+    buffer in the text, in a 256-entry scratch, or the unsorted bucket rest)."""
+    from tests import oracles as O
+    if not O.has_ref():
+        pytest.skip("oracle/_ref not built")
+    import random
+    rng = random.Random(20260)
+    for _ in range(5000):
+        mode = rng.random()
+        if mode < 0.4:
+            w = bytes(rng.randrange(rng.choice([2, 3, 4, 256])) for _ in range(rng.randint(1, 12)))
+            k = rng.randint(2, 3000)
+        elif mode < 0.7:
+            w = bytes(rng.randrange(rng.choice([2, 4, 26, 256])) for _ in range(rng.randint(1, 60)))
+            k = rng.randint(2, 200)
+        elif mode < 0.9:
+            w = bytes(rng.randrange(rng.choice([2, 4])) for _ in range(rng.randint(2, 6)))
+            k = rng.randint(1000, 60000)
+        else:
+            w = bytes([rng.randrange(256)] * 4 + [rng.randrange(256)])
+            k = rng.randint(2, 180000)
+        blk = w * min(k, 900000 // len(w))
+        assert B.periodic_origptr(blk) == O.ref_blocksort(blk)[1], (w, len(blk) // len(w))
 
 
 def _libc():

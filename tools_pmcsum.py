@@ -1,5 +1,5 @@
-"""Per-kernel sums of PMC counters from tools_r02_pmc.sh output (KB counters converted to
-bytes), with the L2 hit rate when TCC_HIT/TCC_MISS were collected:
+"""Per-kernel sums of PMC counters from tools_r02_pmc.sh output: L2 hit rate, HBM-side bytes
+(FETCH_SIZE / WRITE_SIZE, KB counters -> GB) and SQ instruction / wait counters per kernel.
 python tools_pmcsum.py <dir> [top]"""
 import collections
 import csv
@@ -7,24 +7,26 @@ import glob
 import re
 import sys
 
-
-def short(name):
-    m = re.search(r"::(k_\w+)", name)
-    n = m.group(1) if m else name.split("(")[0][:30]
-    return n
-
-
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(sys.argv[1] + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        k = short(r["Kernel_Name"])
+        m = re.search(r"::(k_\w+)", r["Kernel_Name"])
+        k = m.group(1) if m else r["Kernel_Name"].split("(")[0][:26]
+        if k == "k_bsort":
+            k += "<%s>" % r["Grid_Size"]
         v = float(r["Counter_Value"])
         if r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
             v *= 1024.0
         agg[k][r["Counter_Name"]] += v
-top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-print(f'{"kernel":22s} {"FETCH GB":>9s} {"WRITE GB":>9s} {"L2 hit":>7s} {"HIT+MISS G":>10s}')
-for k, v in sorted(agg.items(), key=lambda kv: -(kv[1].get("FETCH_SIZE", 0) + kv[1].get("WRITE_SIZE", 0)))[:top]:
-    h, m = v.get("TCC_HIT_sum", 0), v.get("TCC_MISS_sum", 0)
-    hr = f"{h / (h + m):7.3f}" if h + m else "      -"
-    print(f"{k:22s} {v.get('FETCH_SIZE', 0) / 1e9:9.2f} {v.get('WRITE_SIZE', 0) / 1e9:9.2f} {hr} {(h + m) / 1e9:10.3f}")
+top = int(sys.argv[2]) if len(sys.argv) > 2 else 24
+cols = ["FETCH", "WRITE", "L2hit", "VALU_M", "LDS_M", "VMEM_M", "waveGcyc", "wait%", "ldsconf", "waitLDS%"]
+print(f'{"kernel":26s} ' + " ".join(f"{c:>8s}" for c in cols))
+key = "SQ_WAVE_CYCLES" if any("SQ_WAVE_CYCLES" in v for v in agg.values()) else "FETCH_SIZE"
+for k, v in sorted(agg.items(), key=lambda kv: -kv[1].get(key, 0))[:top]:
+    h, mi = v.get("TCC_HIT_sum", 0), v.get("TCC_MISS_sum", 0)
+    wc = v.get("SQ_WAVE_CYCLES", 0) or 1
+    vals = [v.get("FETCH_SIZE", 0) / 1e9, v.get("WRITE_SIZE", 0) / 1e9, h / (h + mi) if h + mi else 0,
+            v.get("SQ_INSTS_VALU", 0) / 1e6, v.get("SQ_INSTS_LDS", 0) / 1e6, v.get("SQ_INSTS_VMEM", 0) / 1e6,
+            v.get("SQ_WAVE_CYCLES", 0) / 1e9, v.get("SQ_WAIT_INST_ANY", 0) / wc, v.get("SQ_LDS_BANK_CONFLICT", 0) / 1e6,
+            v.get("SQ_WAIT_INST_LDS", 0) / wc]
+    print(f"{k:26s} " + " ".join(f"{x:8.3f}" for x in vals))
