@@ -18,6 +18,8 @@ namespace {
 constexpr int kT = 256;
 constexpr uint32_t kChunk = 1024;
 
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
 __device__ __forceinline__ uint32_t nsym(uint32_t z) { return z ? 31u - (uint32_t)__builtin_clz(z + 1) : 0u; }
 
 // Visits bytes [lo, hi) of p with aligned 16-byte loads (buffers carry >= 16 B of padding),
@@ -170,18 +172,22 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
                                                 uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
                                                 uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
   __shared__ uint32_t lst[64 - kRegW][kT];
+  // rank words of the wave's 64 chunks for one 64-symbol window, [chunk][word] (17: no bank
+  // conflicts on the per-lane writes); flushed as 16-byte stores, 4 lanes per chunk
+  __shared__ uint32_t stg[kT / 64][64 * 17];
   const ChunkRef r = chunk_ref(boff, cbase);
-  if (!r.valid) return;
-  const uint32_t t = threadIdx.x;
-  const uint32_t* src = init + (size_t)r.gidx * 64;
+  const uint32_t t = threadIdx.x, lane = __lane_id();
+  uint32_t* sw = stg[t >> 6];
+  const uint32_t len = r.valid ? r.hi - r.lo : 0u;
+  const uint32_t* src = init + (size_t)(r.valid ? r.gidx : 0u) * 64;
   uint32_t W[kRegW];
 #pragma unroll
   for (int w = 0; w < kRegW; w++) W[w] = src[w];
   for (int w = kRegW; w < 64; w++) lst[w - kRegW][t] = src[w];
-  uint32_t racc = 0;  // 4 ranks packed, stored as one word when aligned
+  uint32_t racc = 0;  // 4 ranks packed
   uint32_t ld = 0, z = 0, cnt = 0;
   bool seen = false;
-  for_bytes<true>(L, r.lo, r.hi, [&](uint32_t i, uint32_t c) {
+  auto step = [&](uint32_t j, uint32_t c) {
     const uint32_t pat = c * 0x01010101u;
     uint32_t fw = kRegW, fz = 0;
 #pragma unroll
@@ -223,13 +229,9 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
       }
       pos = w * 4 + ((uint32_t)__builtin_ctz(x) >> 3);
     }
-    racc |= pos << (8 * (i & 3));
-    if ((i & 3) == 3 || i + 1 == r.hi) {
-      if ((i & 3) == 3 && i >= r.lo + 3) {
-        *reinterpret_cast<uint32_t*>(ranks + i - 3) = racc;
-      } else {
-        for (uint32_t q = (i & ~3u) > r.lo ? (i & ~3u) : r.lo; q <= i; q++) ranks[q] = (uint8_t)(racc >> (8 * (q & 3)));
-      }
+    racc |= pos << (8 * (j & 3));
+    if ((j & 3) == 3 || j + 1 == len) {
+      sw[lane * 17 + ((j >> 2) & 15)] = racc;
       racc = 0;
     }
     // zero-run summary (RUNA/RUNB symbols of inner runs are counted here)
@@ -284,7 +286,34 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
       const uint32_t lowmask = (tb == 3) ? 0xffffffffu : ((1u << (8 * (tb + 1))) - 1u);
       lst[tw - kRegW][t] = (v & ~lowmask) | (((v << 8) | carry) & lowmask);
     }
-  });
+  };
+  // chunk g's ranks go to ranks[g * kChunk, g * kChunk + len): chunk-aligned, so the wave's
+  // lanes complete rank words together and every window goes out as full 64-byte segments
+  const uint32_t g0 = (uint32_t)__shfl((int)r.gidx, 0, 64);
+  for (uint32_t w0 = 0; w0 < kChunk; w0 += 64) {
+    if (__ballot(len > w0) == 0) break;
+    for (uint32_t jj = 0; jj < 64; jj += 16) {
+      const uint32_t j0 = w0 + jj;
+      uint4 q = make_uint4(0, 0, 0, 0);
+      if (j0 < len) __builtin_memcpy(&q, L + r.lo + j0, 16);  // unaligned; the column is padded
+      const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int e = 0; e < 16; e++)
+        if (j0 + e < len) step(j0 + e, (wd[e >> 2] >> (8 * (e & 3))) & 0xffu);
+    }
+    wave_sync();
+#pragma unroll
+    for (uint32_t s4 = 0; s4 < 4; s4++) {
+      const uint32_t cc = (lane >> 2) + 16 * s4, qw = (lane & 3) * 4;
+      const uint32_t lc = (uint32_t)__shfl((int)len, (int)cc, 64);
+      if (lc > w0 + qw * 4) {
+        const uint32_t* rw = sw + cc * 17 + qw;
+        *reinterpret_cast<uint4*>(ranks + (size_t)(g0 + cc) * kChunk + w0 + qw * 4) = make_uint4(rw[0], rw[1], rw[2], rw[3]);
+      }
+    }
+    wave_sync();
+  }
+  if (!r.valid) return;
   lead[r.gidx] = seen ? ld : 0xffffffffu;  // all-zero chunk marker
   trail[r.gidx] = z;
   inner[r.gidx] = cnt;
@@ -378,11 +407,15 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
     const uint32_t base = lo + lane * 16;
     uint32_t rk[16];
     uint32_t nzmask = 0;
+    {  // chunk-aligned ranks (k_mtf_run): one 16-byte load per lane
+      const uint4 q = *reinterpret_cast<const uint4*>(ranks + (size_t)g * kChunk + lane * 16);
+      const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      rk[k] = base + k < hi ? ranks[base + k] : 0u;
-      if (base + k < hi && rk[k]) nzmask |= 1u << k;
+      for (int k = 0; k < 16; k++) rk[k] = base + k < hi ? (wd[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
     }
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (base + k < hi && rk[k]) nzmask |= 1u << k;
     const uint32_t cnt = base < hi ? min(16u, hi - base) : 0u;
     const bool has = nzmask != 0;
     const uint32_t lz = has ? (uint32_t)__builtin_ctz(nzmask) : cnt;
@@ -509,7 +542,7 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
   uint8_t* sig = ws.u8("mtf_sig", (size_t)nchunks * 256);
   uint32_t* siglen = ws.u32("mtf_siglen", nchunks);
   uint32_t* init = ws.u32("mtf_init", (size_t)nchunks * 64);
-  uint8_t* ranks = ws.u8("mtf_ranks", hboff[nb] + 16);
+  uint8_t* ranks = ws.u8("mtf_ranks", (size_t)nchunks * kChunk + 64);  // chunk-aligned
   uint32_t* lead = ws.u32("mtf_lead", nchunks);
   uint32_t* trail = ws.u32("mtf_trail", nchunks);
   uint32_t* inner = ws.u32("mtf_inner", nchunks);
