@@ -134,34 +134,6 @@ __device__ __forceinline__ uint64_t match_byte(uint32_t d, uint64_t active) {
   return m;
 }
 
-// Lanes of the wave (among `active`) whose low kBits bits of v equal this lane's.  Every lane
-// of `active` must execute the call.
-template <int kBits>
-__device__ __forceinline__ uint64_t match_bits(uint32_t v, uint64_t active) {
-  uint64_t m = active;
-#pragma unroll
-  for (int b = 0; b < kBits; b++) {
-    const uint64_t bal = __ballot((v >> b) & 1u);
-    m &= ((v >> b) & 1u) ? bal : ~bal;
-  }
-  return m;
-}
-
-// LDS counter bins with one atomic per distinct bin in the wave instead of one per lane (a
-// skewed digit distribution would otherwise serialise a wave's lanes on one address).  The
-// whole wave must call; lanes with `act` add 1 to ctr[bin] (bin < 2^kBits) and get their
-// rank among the additions (the old value plus the lanes of the same bin below them).
-template <int kBits>
-__device__ __forceinline__ uint32_t lds_count_rank(uint32_t* ctr, uint32_t bin, bool act) {
-  const uint64_t peers = match_bits<kBits>(bin, __ballot(act));
-  const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
-  uint32_t old = 0;
-  if (act && below == 0) old = atomicAdd(&ctr[bin], (uint32_t)__popcll(peers));
-  const int leader = peers ? __ffsll((unsigned long long)peers) - 1 : (int)__lane_id();
-  old = (uint32_t)__shfl((int)old, leader, 64);
-  return old + below;
-}
-
 // List append with one atomic per wave: every lane of the wave must call it; lanes with
 // `pred` get consecutive slots.  Returns the slot (undefined when !pred).
 __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {

@@ -342,7 +342,7 @@ class EnginePool {
         } catch (...) {
           g.lock();
           count_[dev]--;
-          cv_.notify_one();
+          cv_.notify_all();
           throw;
         }
       }
@@ -350,12 +350,58 @@ class EnginePool {
     }
   }
 
+  // Engines for every entry of devs (repeats allowed), taken together under one lock so that
+  // concurrent multi-engine calls cannot deadlock holding part of their sets.
+  std::vector<Engine*> acquire_set(const std::vector<int>& devs) {
+    for (int d : devs)
+      if (d < 0 || d >= devices()) throw HipFailure(hipErrorInvalidDevice);
+    std::vector<int> want(kMaxDev, 0);
+    for (int d : devs) want[d]++;
+    for (int d = 0; d < kMaxDev; d++)
+      if (want[d] > cap_) throw HipFailure(hipErrorInvalidValue);
+    std::unique_lock<std::mutex> g(mu_);
+    cv_.wait(g, [&] {
+      for (int d = 0; d < kMaxDev; d++)
+        if (want[d] && (int)idle_[d].size() + (cap_ - count_[d]) < want[d]) return false;
+      return true;
+    });
+    std::vector<Engine*> out;
+    std::vector<int> fresh;
+    for (int d : devs) {
+      if (!idle_[d].empty()) {
+        out.push_back(idle_[d].back());
+        idle_[d].pop_back();
+      } else {
+        count_[d]++;
+        out.push_back(nullptr);
+        fresh.push_back((int)out.size() - 1);
+      }
+    }
+    g.unlock();
+    try {
+      for (int i : fresh) {
+        DeviceScope ds(devs[i]);
+        out[i] = new Engine(devs[i]);
+      }
+    } catch (...) {
+      g.lock();
+      for (size_t i = 0; i < out.size(); i++) {
+        if (out[i]) idle_[out[i]->device].push_back(out[i]);
+      }
+      for (int i : fresh)
+        if (!out[i]) count_[devs[i]]--;
+      cv_.notify_all();
+      throw;
+    }
+    return out;
+  }
+
   void release(Engine* e) {
     {
       std::lock_guard<std::mutex> g(mu_);
       idle_[e->device].push_back(e);
     }
-    cv_.notify_one();
+    cv_.notify_all();
   }
 
   // Frees the device memory of every idle engine (engines in use keep theirs).
@@ -440,6 +486,317 @@ struct SegState {
 static SegState& seg_state() {
   static SegState* s = new SegState();
   return *s;
+}
+
+// ---------------------------------------------------------------- several devices, one stream
+// One .bz2 stream over several devices inside one process (bzg_compress_host with BZG_NGPUS
+// > 1): the drop-in's callers (the CLI, BZ2_bzBuffToBuffCompress users) live in one process,
+// so the node's GPUs are driven from here rather than from one process per GPU.  The steps
+// are those of bzip2_amd/shard.py, in C++:
+//  1. every device maps the RLE1 chunks of its shard of the input (in parallel);
+//  2. the block cuts are walked shard after shard (bzlib.c:211-315: a block ends once it
+//     holds >= nblockMAX RLE1 bytes; the pending run opens the next block; the stream's last
+//     byte never opens one), the run crossing a shard start settled by arithmetic;
+//  3. a block belongs to the device whose shard holds its first byte; every device compresses
+//     its range of blocks (in parallel) as a flushed segment without trailer, the first range
+//     with the stream header;
+//  4. each device shifts its bits to the range's bit offset mod 8 and they are copied behind
+//     each other into the caller's buffer (the shared boundary bytes OR-ed), then the combined
+//     CRC (combined = rotl(combined, blocks_d) ^ crc_d, compress.c:826-828) and the trailer.
+// The output is byte-identical to the single-device stream (the cuts do not depend on the
+// sharding).  BZG_DEVICES="0,0,0" runs the same path with several engines on one device.
+namespace {
+
+__global__ void k_shift_bits(const uint8_t* __restrict__ in, uint64_t nbits, uint32_t sh, uint8_t* __restrict__ out) {
+  // out = the first nbits bits of `in` moved sh bits later (0 <= sh < 8), trailing bits zero
+  const uint64_t nbytes = (nbits + sh + 7) / 8, nin = (nbits + 7) / 8;
+  const uint32_t tail = (uint32_t)(nbits & 7);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += (uint64_t)gridDim.x * blockDim.x) {
+    auto byte_at = [&](uint64_t j) -> uint32_t {
+      if (j >= nin) return 0u;
+      uint32_t v = in[j];
+      if (j + 1 == nin && tail) v &= (0xffu << (8 - tail)) & 0xffu;
+      return v;
+    };
+    const uint32_t cur = byte_at(i), prev = i ? byte_at(i - 1) : 0u;
+    out[i] = (uint8_t)(((cur >> sh) | (prev << (8 - sh))) & 0xffu);
+  }
+}
+
+struct Shard {
+  int dev;
+  uint64_t s, e;         // input shard [s, e)
+  uint64_t p;            // first run start inside the shard (relative)
+  Engine* eng = nullptr;
+  uint8_t* d_shard = nullptr;
+  std::vector<uint64_t> cuts;  // global block starts inside the shard
+  uint64_t lo = 0, hi = 0;     // owned range
+  uint64_t nbits = 0;
+  uint32_t nblocks = 0, crc = 0;
+  uint8_t* d_bits = nullptr;   // shifted bits
+  uint64_t nshift = 0;
+  bzg_stats stats{};
+};
+
+inline uint32_t chunk_size(uint64_t len) { return len < 4 ? (uint32_t)len : 5u; }
+
+// first j >= 1 with x[j] != x[j - 1] (or len)
+uint64_t first_run_start(const uint8_t* x, uint64_t len) {
+  uint64_t j = 1;
+  while (j < len && x[j] == x[j - 1]) j++;
+  return j;
+}
+
+// the chunks of a run piece [t, x) of equal bytes whose first chunk starts at t (chunks every
+// 255 bytes, 5 RLE1 bytes each): cuts where the block fills (never at the stream's last byte)
+void extend_run(uint64_t& t, uint32_t& fill, uint64_t x, uint32_t mx, std::vector<uint64_t>& cuts, uint64_t last_pos) {
+  uint64_t q = (x - t - 1) / 255;
+  while (q > 0) {
+    const uint64_t need = fill >= mx ? 1 : std::max<uint64_t>(1, (mx - fill + 4) / 5);
+    if (need <= q) {
+      t += 255 * need;
+      q -= need;
+      if (t != last_pos) {
+        cuts.push_back(t);
+        fill = 0;
+      } else {
+        fill += (uint32_t)(5 * need);
+      }
+    } else {
+      t += 255 * q;
+      fill += (uint32_t)(5 * q);
+      q = 0;
+    }
+  }
+}
+
+struct ChainMsg {
+  bool valid = false;
+  uint64_t t = 0;      // start of the open chunk
+  uint32_t fill = 0;   // block fill before it
+  uint8_t byte = 0;
+  uint64_t covered = 0;
+};
+
+}  // namespace
+
+static int compress_host_multi(const uint8_t* src, uint64_t n, int level, uint8_t* dst, uint64_t dst_cap,
+                               uint64_t* dst_len, const std::vector<int>& devs) {
+  const uint32_t mx = 100000u * (uint32_t)level - 19u;
+  const size_t N = devs.size();
+  std::vector<Shard> sh(N);
+  for (size_t d = 0; d < N; d++) {
+    sh[d].dev = devs[d];
+    sh[d].s = n * d / N;
+    sh[d].e = n * (d + 1) / N;
+  }
+  // engines for the whole call (every engine keeps its chunk map between the steps), taken as
+  // one set and returned to the pool on every exit path
+  struct SetLease {
+    std::vector<Engine*> e;
+    ~SetLease() {
+      for (Engine* x : e) pool().release(x);
+    }
+  } lease{pool().acquire_set(devs)};
+  for (size_t d = 0; d < N; d++) sh[d].eng = lease.e[d];
+  auto parallel = [&](auto&& fn) {
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(N);
+    for (size_t d = 0; d < N; d++)
+      th.emplace_back([&, d] {
+        try {
+          DeviceScope ds(sh[d].dev);
+          fn(sh[d]);
+        } catch (...) {
+          err[d] = std::current_exception();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  };
+  // 1. shards in device memory and their chunk maps
+  parallel([&](Shard& S) {
+    const uint64_t len = S.e - S.s;
+    S.p = first_run_start(src + S.s, len);
+    S.d_shard = S.eng->ws.u8("mg_shard", len + 64);
+    HIP_OK(hipMemcpyAsync(S.d_shard, src + S.s, len, hipMemcpyHostToDevice, S.eng->stream));
+    if (S.p < len) seg_map_stage(S.eng->ws, S.d_shard + S.p, len - S.p, S.eng->stream);
+    HIP_OK(hipStreamSynchronize(S.eng->stream));
+  });
+  // 2. the cut chain, shard after shard
+  const uint64_t last_pos = n - 1;
+  ChainMsg msg;
+  for (size_t d = 0; d < N; d++) {
+    Shard& S = sh[d];
+    DeviceScope ds(S.dev);
+    const uint64_t len = S.e - S.s;
+    const bool final = d + 1 == N;
+    const uint8_t d0 = src[S.s], dlast = src[S.e - 1];
+    uint64_t t;
+    uint32_t fill;
+    if (!msg.valid) {
+      t = S.s;
+      fill = 0;
+    } else {
+      t = msg.t;
+      fill = msg.fill;
+      if (msg.byte != d0 || msg.covered >= 255) {  // the open chunk ends at the shard start
+        fill += chunk_size(msg.covered);
+        t = S.s;
+        if (fill >= mx && S.s != last_pos) {
+          S.cuts.push_back(S.s);
+          fill = 0;
+        }
+      }
+    }
+    const uint64_t x = S.s + S.p;  // [t, x) is one run piece of byte d0
+    extend_run(t, fill, x, mx, S.cuts, last_pos);
+    msg = ChainMsg{};
+    if (S.p == len) {  // the whole shard is one run piece
+      if (!final) msg = ChainMsg{true, t, fill, d0, S.e - t};
+      continue;
+    }
+    fill += chunk_size(x - t);  // the run ends at x, a run start
+    if (x == last_pos) continue;  // the stream's last byte joins the open block
+    if (fill >= mx) {
+      S.cuts.push_back(x);
+      fill = 0;
+    }
+    std::vector<uint64_t> rc;
+    uint64_t lc = 0;
+    uint32_t lf = fill;
+    seg_walk_stage(S.eng->ws, S.d_shard + S.p, len - S.p, level, fill, final, rc, lc, lf, S.eng->stream);
+    for (uint64_t c : rc) S.cuts.push_back(x + c);
+    if (!final) msg = ChainMsg{true, x + lc, lf, dlast, S.e - (x + lc)};
+  }
+  // 3. owned ranges: from the first block start in the shard to the next owner's
+  {
+    std::vector<uint64_t> first(N, UINT64_MAX);
+    for (size_t d = 0; d < N; d++) {
+      if (d == 0) first[d] = 0;
+      else if (!sh[d].cuts.empty()) first[d] = sh[d].cuts.front();
+    }
+    // a cut made by shard d's walk lies inside shard d, except the arithmetic ones of a run
+    // crossing into later shards: assign every cut to the shard holding it
+    std::vector<uint64_t> all;
+    for (auto& S : sh) all.insert(all.end(), S.cuts.begin(), S.cuts.end());
+    std::sort(all.begin(), all.end());
+    for (size_t d = 1; d < N; d++) {
+      auto it = std::lower_bound(all.begin(), all.end(), sh[d].s);
+      first[d] = (it != all.end() && *it < sh[d].e) ? *it : UINT64_MAX;
+    }
+    for (size_t d = 0; d < N; d++) {
+      if (first[d] == UINT64_MAX) continue;
+      uint64_t nx = n;
+      for (size_t j = d + 1; j < N; j++)
+        if (first[j] != UINT64_MAX) {
+          nx = first[j];
+          break;
+        }
+      sh[d].lo = first[d];
+      sh[d].hi = nx;
+    }
+  }
+  // 4. compress the ranges, shift the bits to their byte offsets on the device
+  parallel([&](Shard& S) {
+    if (S.hi <= S.lo) return;
+    Engine& E = *S.eng;
+    const uint64_t len = S.hi - S.lo;
+    uint8_t* din = E.ws.u8("mg_in", len + 64);
+    HIP_OK(hipMemcpyAsync(din, src + S.lo, len, hipMemcpyHostToDevice, E.stream));
+    const uint64_t cap = bzg_bound(len) + 64;
+    uint8_t* dout = E.ws.u8("mg_out", cap);
+    bzg_stream_state st;
+    bzg_stream_init(&st, level);
+    st.header_done = S.lo == 0 ? 0 : 1;
+    const unsigned flags = BZG_FLAG_END_SEGMENT | (S.hi == n ? BZG_FLAG_TAIL_MERGE : 0u);
+    uint64_t ob = 0, cons = 0;
+    E.compress(din, len, flags, &st, dout, cap, &ob, &cons, E.stream, S.stats);
+    S.nbits = 8 * ob + st.carry_bits;
+    if (st.carry_bits) {  // the unfinished last byte (not part of the ob whole bytes)
+      HIP_OK(hipMemcpyAsync(dout + ob, &st.carry_byte, 1, hipMemcpyHostToDevice, E.stream));
+      HIP_OK(hipStreamSynchronize(E.stream));
+    }
+    S.nblocks = st.blocks_done;
+    S.crc = st.combined_crc;
+  });
+  uint64_t total_bits = 0;
+  std::vector<uint64_t> off(N);
+  for (size_t d = 0; d < N; d++) {
+    off[d] = total_bits;
+    total_bits += sh[d].nbits;
+  }
+  const uint64_t out_len = (total_bits + 80 + 7) / 8;
+  if (out_len > dst_cap) return BZ_OUTBUFF_FULL;
+  std::memset(dst, 0, out_len);
+  std::vector<uint8_t> head(N, 0);
+  parallel([&](Shard& S) {
+    const size_t d = &S - sh.data();
+    if (S.nbits == 0) return;
+    Engine& E = *S.eng;
+    const uint32_t s8 = (uint32_t)(off[d] & 7);
+    const uint64_t nb = (S.nbits + s8 + 7) / 8;
+    uint8_t* dout = E.ws.u8("mg_out", 1);  // same buffer (already large enough)
+    uint8_t* dsh = E.ws.u8("mg_shift", nb + 64);
+    k_shift_bits<<<(unsigned)std::min<uint64_t>(ceil_div64(nb, 256), 65536), 256, 0, E.stream>>>(dout, S.nbits, s8,
+                                                                                               dsh);
+    HIP_OK(hipGetLastError());
+    // byte 0 is shared with the previous range's last byte: OR-ed on the host below
+    HIP_OK(hipMemcpyAsync(&head[d], dsh, 1, hipMemcpyDeviceToHost, E.stream));
+    if (nb > 1) HIP_OK(hipMemcpyAsync(dst + off[d] / 8 + 1, dsh + 1, nb - 1, hipMemcpyDeviceToHost, E.stream));
+    HIP_OK(hipStreamSynchronize(E.stream));
+  });
+  uint32_t comb = 0;
+  bzg_stats acc{};
+  for (size_t d = 0; d < N; d++) {
+    if (sh[d].nbits) dst[off[d] / 8] |= head[d];
+    const uint32_t k = sh[d].nblocks % 32;
+    if (k) comb = (comb << k) | (comb >> (32 - k));
+    comb ^= sh[d].crc;
+    acc.total_ms = std::max(acc.total_ms, sh[d].stats.total_ms);
+    acc.nblocks += sh[d].stats.nblocks;
+    acc.rle_bytes += sh[d].stats.rle_bytes;
+    acc.mtf_symbols += sh[d].stats.mtf_symbols;
+  }
+  publish_stats(acc);
+  // trailer: 0x177245385090 and the combined CRC at bit total_bits, zero padded
+  {
+    const uint64_t tr_hi = 0x177245385090ull;
+    uint64_t bit = total_bits;
+    auto put = [&](uint64_t v, int nbits) {
+      for (int i = nbits - 1; i >= 0; i--, bit++)
+        if ((v >> i) & 1u) dst[bit >> 3] |= (uint8_t)(0x80u >> (bit & 7));
+    };
+    put(tr_hi, 48);
+    put(comb, 32);
+  }
+  *dst_len = out_len;
+  return BZ_OK;
+}
+
+// Devices of the multi-device path: BZG_DEVICES (a list, repeats allowed) or the first
+// BZG_NGPUS devices; empty when the single-device path applies.
+static std::vector<int> multi_devices(uint64_t n) {
+  std::vector<int> devs;
+  const char* list = getenv("BZG_DEVICES");
+  const char* ng = getenv("BZG_NGPUS");
+  const int ndev = pool().devices();
+  if (list && *list) {
+    for (const char* p = list; *p;) {
+      char* end = nullptr;
+      const long v = strtol(p, &end, 10);
+      if (end == p) break;
+      if (v >= 0 && v < ndev) devs.push_back((int)v);
+      p = *end ? end + 1 : end;
+    }
+  } else if (ng) {
+    const int k = std::min(atoi(ng), ndev);
+    for (int d = 0; d < k; d++) devs.push_back(d);
+  }
+  // worth it only for inputs of several blocks per device; shards within one batch
+  if (devs.size() < 2 || n < (uint64_t)devs.size() * 4000000ull || n / devs.size() + 1 > kMaxBatch) devs.clear();
+  return devs;
 }
 
 }  // namespace bzg
@@ -564,6 +921,13 @@ static int host_call(const void* src, uint64_t n, unsigned flags, bzg_stream_sta
 
 int bzg_compress_host(const void* src, uint64_t n, int level, void* dst, uint64_t dst_cap, uint64_t* dst_len) {
   if (level < 1 || level > 9 || (n && !src) || !dst || !dst_len) return BZ_PARAM_ERROR;
+  if (pool().devices() > 0) {
+    const std::vector<int> devs = multi_devices(n);
+    if (!devs.empty())
+      return guarded([&] {
+        return compress_host_multi((const uint8_t*)src, n, level, (uint8_t*)dst, dst_cap, dst_len, devs);
+      });
+  }
   bzg_stream_state st;
   bzg_stream_init(&st, level);
   const unsigned flags = BZG_FLAG_END_SEGMENT | BZG_FLAG_TRAILER | (n ? BZG_FLAG_TAIL_MERGE : 0u);

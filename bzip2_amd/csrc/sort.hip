@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, uint3
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    (void)lds_count_rank<8>(h, kk[i] >> 24, lo + i * kT + threadIdx.x < hi);
+    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[kk[i] >> 24], 1u);
   __syncthreads();
   hist[(size_t)t * 256 + threadIdx.x] = h[threadIdx.x];
 }
@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, ui
   uint32_t rk[kPerT];
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    rk[i] = lds_count_rank<8>(cnt, kk[i] >> 24, lo + i * kT + threadIdx.x < hi);
+    if (lo + i * kT + threadIdx.x < hi) rk[i] = atomicAdd(&cnt[kk[i] >> 24], 1u);
   __syncthreads();
   {
     const uint32_t c = cnt[d];
@@ -567,7 +567,7 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
   s1s_load<true, false>(S, B, ni, n, vv, kk, jj);
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++)
-    jj[i] = lds_count_rank<12>(S.cnt, jj[i] * 256 + (kk[i] >> 24), i * kTS + threadIdx.x < n) | (jj[i] << 16);
+    if (i * kTS + threadIdx.x < n) jj[i] = atomicAdd(&S.cnt[jj[i] * 256 + (kk[i] >> 24)], 1u) | (jj[i] << 16);
   __syncthreads();
   // tile-relative bucket bases: exclusive scan over the (group, digit) bins
   {
@@ -831,10 +831,7 @@ __global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const u
         const uint32_t len = S.slen[cur_t][sg[i]];
         kk[i] = q[i] + 4 <= len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.stoff[cur_t][sg[i]], len, q[i]);
       }
-    }
-#pragma unroll
-    for (int i = 0; i < (int)kPPer; i++) {
-      rk[i] = lds_count_rank<13>(S.cnt, (sg[i] == 0xff ? 0u : sg[i]) * 256u + (kk[i] >> 24), sg[i] != 0xff);
+      if (sg[i] != 0xff) rk[i] = atomicAdd(&S.cnt[sg[i] * 256u + (kk[i] >> 24)], 1u);
     }
     __syncthreads();
     // ---- bins -> tile positions: one exclusive scan over all bins (segments are contiguous in
@@ -1721,9 +1718,9 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   };
   auto grid = [](uint64_t n) { return (unsigned)std::max<uint64_t>(1, ceil_div64(n, kT)); };
   static const bool debug = getenv("BZG_DEBUG") != nullptr;
-  static const bool use_s1p = [] {  // packed groups finished in LDS (k_s1p); 0: one pass per kernel (k_s1s)
+  static const bool use_s1p = [] {  // 1: packed groups finished in LDS (k_s1p); default: one pass per kernel (k_s1s)
     const char* e = getenv("BZG_S1P");
-    return !e || atoi(e) != 0;
+    return e && atoi(e) != 0;
   }();
 
   HIP_OK(hipMemsetAsync(cnt, 0, 64 * 4, st));

@@ -411,6 +411,32 @@ def test_file_api_write_matches_reference(tmp_path):
     assert q.read_bytes() == O.ref_stream_compress(pieces, 9)
 
 
+@pytest.mark.parametrize("level", [1, 9])
+def test_multi_device_host_path(monkeypatch, level):
+    """BZ2_bzBuffToBuffCompress over several engines in one process (BZG_DEVICES=0,0,0: three
+    engines on this box's GPU; the 8-GPU node uses BZG_NGPUS=8): chunk maps per shard, the cut
+    chain, owned block ranges, bit-shifted copies behind each other, combined CRC and trailer
+    give the reference's stream."""
+    rnd = random.Random(level)
+    txt = datagen.text(14_000_000, 0x5EED0011)
+    cases = {
+        "text": txt,
+        "text_run_text": txt[:5_000_000] + b"q" * 9_000_000 + txt[5_000_000:9_000_000],
+        "one_byte": b"z" * 30_000_000,  # one run over every shard boundary
+        "runs_of_4": b"aaaabbbb" * 1_600_000,
+        "random": datagen.random_bytes(13_000_000, 5),
+        "mixed_runs": bytes(np.repeat(np.frombuffer(datagen.random_bytes(200_000, 9), np.uint8) % 3,
+                                      np.random.default_rng(3).integers(1, 300, 200_000)).tobytes()[:13_000_000]),
+    }
+    monkeypatch.setenv("BZG_DEVICES", "0,0,0")
+    for name, data in cases.items():
+        got = B.buff_to_buff_compress(data, level)
+        assert got == expected(data, level), name
+    monkeypatch.setenv("BZG_DEVICES", "0,0,0,0")  # a stream whose last byte opens no block
+    data = b"a" * (255 * 19996 * 3 + 4) + b"b"
+    assert B.buff_to_buff_compress(data, 1) == expected(data, 1)
+
+
 def test_round_trip_large_properties():
     """At bench-like sizes: decode(encode(x)) == x with the system bzip2 decoder, and the
     stream equals the reference's on a 4 MB slice."""
