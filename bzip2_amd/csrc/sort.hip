@@ -441,12 +441,19 @@ __global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, uint32_t* _
   if (g < n) sizes[g] = L[g].size;
 }
 
-// packed kernels: 512 threads x 8 elements (a tile holds < 2 kSG rotations)
-constexpr uint32_t kTS = 512, kPerTS = 2 * kSG / kTS;
+// packed kernels: 512 threads x 8 elements (a tile holds < 2 kSG rotations; kSG on average,
+// so the element loops stop at the tile's last 512-element round)
+#ifndef BZG_TS
+#define BZG_TS 512
+#endif
+constexpr uint32_t kTS = BZG_TS, kPerTS = 2 * kSG / kTS;
 struct S1sLds {
-  uint32_t cnt[kSGrp * 256];   // bucket counts
-  uint32_t cur[kSGrp * 256];   // bucket cursors (tile-relative)
-  uint32_t gstart[kSGrp], goff[kSGrp + 1], gfl[kSGrp], gunit[kSGrp], gtoff[kSGrp], glen[kSGrp];
+  // (group, digit) bins: counts, then (in place) exclusive tile-relative bases; entry
+  // ni * 256 = tile size, so a bin's total is the difference of neighbouring entries
+  uint32_t cur[kSGrp * 256 + 1];
+  // per group: first slot, tile offset, flags, unit, and the unit's text offset, length,
+  // first slot and copies
+  uint32_t gstart[kSGrp], goff[kSGrp + 1], gfl[kSGrp], gunit[kSGrp], gtoff[kSGrp], glen[kSGrp], gsb[kSGrp], gk[kSGrp];
   uint32_t sh[kTS / 64];
   uint32_t cc[kNCls + 1];
 };
@@ -466,8 +473,10 @@ __device__ __forceinline__ uint32_t s1s_setup(S1sLds& S, const Grp* __restrict__
     S.gunit[threadIdx.x] = g.unit;
     S.gtoff[threadIdx.x] = U.toff;
     S.glen[threadIdx.x] = U.len;
+    S.gsb[threadIdx.x] = U.sbase;
+    S.gk[threadIdx.x] = U.k;
   }
-  for (uint32_t i = threadIdx.x; i < ni * 256; i += kTS) S.cnt[i] = 0;
+  for (uint32_t i = threadIdx.x; i < ni * 256; i += kTS) S.cur[i] = 0;
   if (threadIdx.x <= (uint32_t)kNCls) S.cc[threadIdx.x] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -478,70 +487,33 @@ __device__ __forceinline__ uint32_t s1s_setup(S1sLds& S, const Grp* __restrict__
   return ni;
 }
 
-// Group boundaries of the tile in registers (goff[q], or ~0 past the last group): the owner
-// of a tile element is then a few compares.
+// Group boundaries of the tile in scalar registers (goff[q], or ~0 past the last group): the
+// owner of a tile element is a compare per group boundary of the tile (scalar loop bound).
 struct S1sOwner {
   uint32_t go[kSGrp - 1];
-  __device__ __forceinline__ S1sOwner(const S1sLds& S, uint32_t ni) {
+  uint32_t nb;  // boundaries in use (ni - 1)
+  __device__ __forceinline__ S1sOwner(const S1sLds& S, uint32_t ni) : nb(ni - 1) {
 #pragma unroll
     for (uint32_t q = 1; q < kSGrp; q++) go[q - 1] = __builtin_amdgcn_readfirstlane(q < ni ? S.goff[q] : 0xffffffffu);
   }
   __device__ __forceinline__ uint32_t operator()(uint32_t e) const {
     uint32_t j = 0;
 #pragma unroll
-    for (uint32_t q = 0; q + 1 < kSGrp; q++) j += e >= go[q];
+    for (uint32_t q = 0; q + 1 < kSGrp; q++) {
+      if (q >= nb) break;  // uniform
+      j += e >= go[q];
+    }
     return j;
   }
 };
-
-// Packed path: rotations vv, keys kk and groups jj of the tile's elements (lanes past n get
-// element n - 1's).  kCounting: empty caches are refilled from the text (kWriteBack: and
-// stored back to the source slots).
-template <bool kCounting, bool kWriteBack = kCounting>
-__device__ __forceinline__ void s1s_load(const S1sLds& S, const SortBufs& B, uint32_t ni, uint32_t n,
-                                         uint32_t (&vv)[kPerTS], uint32_t (&kk)[kPerTS], uint32_t (&jj)[kPerTS]) {
-  const S1sOwner own(S, ni);
-  uint32_t sl[kPerTS];  // slot
-#pragma unroll
-  for (int i = 0; i < (int)kPerTS; i++) {
-    const uint32_t e = min(i * kTS + threadIdx.x, n - 1);
-    const uint32_t j = own(e), o = e - S.goff[j], fl = S.gfl[j];
-    jj[i] = j;
-    sl[i] = S.gstart[j] + o;
-    vv[i] = (fl & kGrpIdent) ? o : ((fl & kGrpAlt) ? B.sa2 : B.sa)[sl[i]];
-  }
-#pragma unroll
-  for (int i = 0; i < (int)kPerTS; i++) {
-    const uint32_t j = jj[i], fl = S.gfl[j];
-    const bool fresh = (fl & kGrpIdent) || (kCounting && grp_cache(Grp{0, 0, 0, fl}) == 0);
-    const uint8_t* p = fresh ? B.text + S.gtoff[j] + cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j])
-                             : reinterpret_cast<const uint8_t*>(((fl & kGrpAlt) ? B.sk2 : B.sk) + sl[i]);
-    kk[i] = ld_u32(p);
-  }
-#pragma unroll
-  for (int i = 0; i < (int)kPerTS; i++) {
-    const uint32_t j = jj[i], fl = S.gfl[j];
-    const bool fresh = (fl & kGrpIdent) || (kCounting && grp_cache(Grp{0, 0, 0, fl}) == 0);
-    if (fresh) {
-      const uint32_t q = cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j]);
-      kk[i] = q + 4 <= S.glen[j] ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.gtoff[j], S.glen[j], q);
-    }
-  }
-  if (kWriteBack) {
-#pragma unroll
-    for (int i = 0; i < (int)kPerTS; i++) {
-      const uint32_t fl = S.gfl[jj[i]];
-      if (i * kTS + threadIdx.x < n && !(fl & kGrpIdent) && grp_cache(Grp{0, 0, 0, fl}) == 0)
-        ((fl & kGrpAlt) ? B.sk2 : B.sk)[sl[i]] = kk[i];
-    }
-  }
-}
 
 // One packed pass in one kernel: counts, LDS reorder, stores of the slots and caches, and
 // the tile's buckets of two or more rotations as records (group:4 | start:14 | size:14,
 // tile-relative) in the tile's own part of `rec` (it starts at half the tile's first element
 // offset: a tile of n rotations has at most n / 2 such buckets), with the per-class counts for
 // the class-major scan.  k_s1s_emit turns the records into class-list entries.
+// Element rounds past the tile's size are skipped (uniform branches); loads are issued for
+// all rounds before their values are used, from addresses selected without branches.
 __device__ __forceinline__ uint32_t rec_pack(uint32_t j, uint32_t start, uint32_t size) {
   return (j << 28) | (start << 14) | size;
 }
@@ -552,7 +524,7 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
                                                  uint32_t* __restrict__ nrec, uint32_t* __restrict__ ccnt, uint32_t nTot,
                                                  uint32_t ibase) {
   __shared__ S1sLds S;
-  __shared__ uint32_t Lv[2 * kSG], Lk[2 * kSG];  // the tile in bucket order
+  __shared__ uint32_t Lv[2 * kSG];  // the tile's rotations in bucket order
   __shared__ uint32_t nr;
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const uint32_t ni = s1s_setup(S, SG, first, last, t, B);
@@ -563,20 +535,56 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
   }
   if (threadIdx.x == 0) nr = 0;
   const uint32_t n = S.goff[ni];
-  uint32_t vv[kPerTS], kk[kPerTS], jj[kPerTS];
-  s1s_load<true, false>(S, B, ni, n, vv, kk, jj);
+  const uint32_t rounds = ceil_div(n, kTS);  // uniform
+  const S1sOwner own(S, ni);
+  const uint32_t lane = __lane_id();
+  uint32_t vv[kPerTS], kk[kPerTS], jj[kPerTS], qq[kPerTS];
+  // rotations (identity groups: the offset; slots of identity groups hold stale values,
+  // loaded anyway so that no load sits behind a branch)
 #pragma unroll
-  for (int i = 0; i < (int)kPerTS; i++)
-    if (i * kTS + threadIdx.x < n) jj[i] = atomicAdd(&S.cnt[jj[i] * 256 + (kk[i] >> 24)], 1u) | (jj[i] << 16);
+  for (int i = 0; i < (int)kPerTS; i++) {
+    if ((uint32_t)i >= rounds) break;
+    const uint32_t e = min(i * kTS + threadIdx.x, n - 1);
+    const uint32_t j = own(e), fl = S.gfl[j];
+    jj[i] = j;
+    qq[i] = e - S.goff[j];
+    vv[i] = ((fl & kGrpAlt) ? B.sa2 : B.sa)[S.gstart[j] + qq[i]];
+  }
+  // keys: the cache, or 4 characters of the text when the cache is empty
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    if ((uint32_t)i >= rounds) break;
+    const uint32_t j = jj[i], fl = S.gfl[j], o = qq[i];
+    if (fl & kGrpIdent) vv[i] = o;
+    const bool fresh = (fl & kGrpIdent) || grp_cache(Grp{0, 0, 0, fl}) == 0;
+    const uint32_t q = cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j]);
+    qq[i] = fresh ? q : 0xffffffffu;  // text position, or none
+    kk[i] = ld_u32(fresh ? B.text + S.gtoff[j] + q
+                         : reinterpret_cast<const uint8_t*>(((fl & kGrpAlt) ? B.sk2 : B.sk) + S.gstart[j] + o));
+  }
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    if ((uint32_t)i >= rounds) break;
+    if (qq[i] != 0xffffffffu) {
+      const uint32_t j = jj[i];
+      kk[i] = qq[i] + 4 <= S.glen[j] ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.gtoff[j], S.glen[j], qq[i]);
+    }
+  }
+  // counts; qq = rank of the element in its bin
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    if ((uint32_t)i >= rounds) break;
+    if (i * kTS + threadIdx.x < n) qq[i] = atomicAdd(&S.cur[jj[i] * 256 + (kk[i] >> 24)], 1u);
+  }
   __syncthreads();
-  // tile-relative bucket bases: exclusive scan over the (group, digit) bins
+  // tile-relative bin bases: exclusive scan over the (group, digit) bins, in place
   {
     constexpr uint32_t kB = (kSGrp * 256 + kTS - 1) / kTS;
     uint32_t c[kB], sum = 0;
 #pragma unroll
     for (int q = 0; q < (int)kB; q++) {
       const uint32_t b = threadIdx.x * kB + q;
-      c[q] = b < ni * 256 ? S.cnt[b] : 0u;
+      c[q] = b < ni * 256 ? S.cur[b] : 0u;
       sum += c[q];
     }
     uint32_t run = block_incl_sum(sum, S.sh, (uint32_t*)nullptr) - sum;
@@ -586,52 +594,61 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
       if (b < ni * 256) S.cur[b] = run;
       run += c[q];
     }
+    if (threadIdx.x == 0) S.cur[ni * 256] = n;
   }
   __syncthreads();
-  // bucket records and class counts
+  // bucket records (one LDS atomic per wave) and class counts
   uint32_t* trec = rec + P[first[t]] / 2;
-  for (uint32_t b = threadIdx.x; b < ni * 256; b += kTS) {
-    const uint32_t j = b >> 8, total = S.cnt[b];
-    const uint32_t cl = bucket_cls(total, grp_depth(Grp{0, 0, 0, S.gfl[j]}) + 1);
-    if (cl == 0xffu) continue;
-    if (cl < (uint32_t)kNCls) atomicAdd(&S.cc[cl], 1u);
-    trec[atomicAdd(&nr, 1u)] = rec_pack(j, S.cur[b], total);
+  for (uint32_t b0 = 0; b0 < ni * 256; b0 += kTS) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint32_t j = b >> 8, total = b < ni * 256 ? S.cur[b + 1] - S.cur[b] : 0u;
+    const uint32_t cl = total < 2 ? 0xffu : bucket_cls(total, grp_depth(Grp{0, 0, 0, S.gfl[j]}) + 1);
+    const uint64_t m = __ballot(cl != 0xffu);
+    if (m == 0) continue;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&nr, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, 0, 64);
+    if (cl != 0xffu) {
+      trec[base + (uint32_t)__popcll(m & lanemask_lt())] = rec_pack(j, S.cur[b], total);
+      if (cl < (uint32_t)kNCls) atomicAdd(&S.cc[cl], 1u);
+    }
   }
-  // reorder the tile by bucket in LDS (jj = rank in bin | group << 16)
+  // every element at its place: the rotation into the LDS tile (stored coalesced below), the
+  // key cache of a bucket that stays in S1, and a bucket of one is final (the group lies in
+  // this tile, so its primary SA slots are free)
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {
+    if ((uint32_t)i >= rounds) break;
     if (i * kTS + threadIdx.x < n) {
-      const uint32_t lp = S.cur[(jj[i] >> 16) * 256 + (kk[i] >> 24)] + (jj[i] & 0xffffu);
-      Lv[lp] = vv[i];
-      Lk[lp] = kk[i];
+      const uint32_t j = jj[i], fl = S.gfl[j];
+      const uint32_t bin = j * 256 + (kk[i] >> 24);
+      const uint32_t x = S.cur[bin] + qq[i], total = S.cur[bin + 1] - S.cur[bin];
+      const uint32_t v = vv[i];
+      Lv[x] = v;
+      const uint32_t slot = S.gstart[j] + x - S.goff[j];
+      const bool dst_alt = !(fl & kGrpIdent) && !(fl & kGrpAlt);
+      // key caches only for buckets that stay in S1 (S2 and S3 read the text)
+      if (bucket_cls(total, grp_depth(Grp{0, 0, 0, fl}) + 1) == 6u) (dst_alt ? B.sk2 : B.sk)[slot] = kk[i] << 8;
+      if (total == 1) {
+        if (dst_alt) B.sa[slot] = v;
+        const uint32_t r = slot - S.gsb[j];
+        const uint32_t len = S.glen[j];
+        if (S.gk[j] == 1) O.bwt[S.gtoff[j] + r] = B.text[S.gtoff[j] + (v == 0 ? len - 1 : v - 1)];
+        if (v == 0) O.rank0[S.gunit[j]] = r;
+      }
     }
   }
   __syncthreads();
   if (threadIdx.x < (uint32_t)kNCls) ccnt[(size_t)threadIdx.x * nTot + ibase + t] = S.cc[threadIdx.x];
   if (threadIdx.x == 0) nrec[t] = nr;
-  const S1sOwner own(S, ni);
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {
+    if ((uint32_t)i >= rounds) break;
     const uint32_t x = i * kTS + threadIdx.x;
     if (x < n) {
       const uint32_t j = own(x), fl = S.gfl[j];
-      vv[i] = Lv[x];
-      kk[i] = Lk[x];
-      jj[i] = S.gstart[j] + x - S.goff[j];  // slot
       const bool dst_alt = !(fl & kGrpIdent) && !(fl & kGrpAlt);
-      (dst_alt ? B.sa2 : B.sa)[jj[i]] = vv[i];
-      // key caches only for buckets that stay in S1 (S2 and S3 read the text)
-      if (bucket_cls(S.cnt[j * 256 + (kk[i] >> 24)], grp_depth(Grp{0, 0, 0, fl}) + 1) == 6u)
-        (dst_alt ? B.sk2 : B.sk)[jj[i]] = kk[i] << 8;
-    }
-  }
-  // a bucket of one: ordered (the group lies in this tile, so the primary SA is free)
-#pragma unroll
-  for (int i = 0; i < (int)kPerTS; i++) {
-    const uint32_t x = i * kTS + threadIdx.x;
-    if (x < n) {
-      const uint32_t j = own(x);
-      if (S.cnt[j * 256 + (kk[i] >> 24)] == 1) emit_final(B, O, B.units[S.gunit[j]], S.gunit[j], jj[i], vv[i], true);
+      (dst_alt ? B.sa2 : B.sa)[S.gstart[j] + x - S.goff[j]] = Lv[x];
     }
   }
 }
@@ -1032,17 +1049,25 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
   for (;;) {
     const uint64_t live = __ballot(!done);
     if (live == 0) break;
-    if (d >= B.dwave) {  // still tied after B.dwave characters: leave to the doubling fallback
-      // buckets of one wave reach the depth limit at different steps: only the lanes in this
-      // branch take part in match_byte's ballots, so restrict its candidates to them
-      const uint64_t here = __ballot(true);
-      if (!done) {
-        const uint64_t mates = match_byte(cls, live & here);
-        const uint32_t r = (uint32_t)__popcll(mates & lanemask_lt());
-        B.sa[s0 + pos + r] = v;
-        if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, (uint32_t)__popcll(mates), unit, grp_flags(0u, d, 1u)};
+    // still tied after B.dwave characters: leave to the doubling fallback.  The members of a
+    // class and their ranks come from the bucket's 8 lanes (all lanes of the wave still run
+    // here, so every shuffle source is active)
+    const bool deep_now = d >= B.dwave;
+    if (__ballot(deep_now)) {
+      uint32_t cnt = 0, r = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t cj = (uint32_t)__shfl((int)cls, base + j, 64);
+        if (cj == cls) {
+          cnt++;
+          r += (uint32_t)(base + j) < lane;
+        }
       }
-      break;
+      if (deep_now && !done) {
+        B.sa[s0 + pos + r] = v;
+        if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
+      }
+      if (deep_now) break;
     }
     uint32_t k[4] = {0u, 0u, 0u, 0u};
     if (!done) text_key16(t, U.len, cyc_pos(v, d, U.len), k);
@@ -1144,7 +1169,8 @@ __device__ __forceinline__ void bitonic_j(BsortKey (&K)[kPer], int k, uint32_t s
           if (r2 > r) {
             const uint32_t p = sl * kPer + r;
             const bool asc = (p & k) == 0;
-            const bool sw = asc ? key_less(K[r2], K[r]) : key_less(K[r], K[r2]);
+            // keys are distinct but for pads (equal; swapping them is harmless): one compare
+            const bool sw = key_less(K[r2], K[r]) == asc;
             const BsortKey x = K[r], y = K[r2];
             K[r] = sw ? y : x;
             K[r2] = sw ? x : y;
@@ -1295,11 +1321,15 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
                                               S2Emit E = S2Emit{}) {
   constexpr int kBPW = 64 / kSeg;
   constexpr int kE = 64 * kPer;  // elements per wave
+  // the rank-counting tail (TK, TC, Lk) only exists without emission: the emitting classes
+  // hand runs still tied at B.dwave to the doubling fallback directly, so they need little LDS
+  // and run at full occupancy
+  constexpr int kTE = kEmit ? 1 : kE;
   __shared__ uint32_t Lv[kT / 64][kE];
   __shared__ uint8_t Lc[kT / 64][kE];
-  __shared__ uint32_t Lk[kT / 64][kE];
-  __shared__ uint4 TK[kT / 64][kE];
-  __shared__ uint32_t TC[kT / 64][kE];
+  __shared__ uint32_t Lk[kT / 64][kEmit ? 8 : kE];
+  __shared__ uint4 TK[kT / 64][kTE];
+  __shared__ uint32_t TC[kT / 64][kTE];
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   const uint32_t sl = lane % kSeg;
   const uint32_t bi = (blockIdx.x * (kT / 64) + w) * kBPW + lane / kSeg;
@@ -1362,7 +1392,11 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
 #pragma unroll
   for (int r = 0; r < kPer; r++) done[r] = false;
   int round = 0;
+  // BZG_DEBUG: waves entering each round, per class (dbg[8 + 8 * class + round]; round 7:
+  // the rank-counting tail)
+  constexpr int kDbgCls = kSeg * kPer == 16 ? 1 : kSeg * kPer == 32 ? 2 : kSeg * kPer == 64 ? 3 : kSeg * kPer == 128 ? 4 : 5;
   for (;;) {
+    if (O.dbg && lane == 0) atomicAdd(&O.dbg[8 + 8 * kDbgCls + min(round, 6)], 1ull);
     bitonic<kSeg, kPer>(K);
     // ties with the previous / next position of the segment (same run start and key)
     bool tp[kPer], tn[kPer];
@@ -1430,7 +1464,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     if (++round >= kRounds || depth >= B.dwave) {
       if constexpr (kEmit) {
         static_assert(kSeg == 64, "one group per wave");
-        if (depth < B.dwave) {
+        {
           uint32_t* cc = Lk[w];  // per-class counters, then the record cursor
           if (lane < 8) cc[lane] = 0;
           wave_sync();
@@ -1441,16 +1475,22 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
             B.sa[g.start + p] = Lv[w][key_idx(K[r])];
             if (!tn[r]) {  // last member of its run
               const uint32_t size = p - rsn[r] + 1;
-              atomicAdd(&cc[size_cls(size)], 1u);
-              E.rec[g.start / 2 + atomicAdd(&cc[7], 1u)] = (depth << 17) | (rsn[r] << 9) | size;
+              if (depth >= B.dwave) {  // still tied after B.dwave characters: doubling fallback
+                O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + rsn[r], size, g.unit, grp_flags(0u, depth, 2u)};
+              } else {
+                atomicAdd(&cc[size_cls(size)], 1u);
+                E.rec[g.start / 2 + atomicAdd(&cc[7], 1u)] = (depth << 17) | (rsn[r] << 9) | size;
+              }
             }
           }
           wave_sync();
           if (lane < 6) E.ccnt[(size_t)lane * E.total + E.gbase + bi] = cc[lane];
           break;
         }
+      } else {
+        if (O.dbg && lane == 0) atomicAdd(&O.dbg[8 + 8 * kDbgCls + 7], 1ull);
+        bsort_tail<kSeg, kPer, kBatch>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       }
-      bsort_tail<kSeg, kPer, kBatch>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       break;
     }
     // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
@@ -1629,6 +1669,31 @@ __global__ void __launch_bounds__(kT) k_unit_out(const uint32_t* __restrict__ ul
   bwt[U.toff + x] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
 }
 
+// BZG_CHECK diagnostics: every member of group g must equal member 0 on min(depth, 64)
+// characters.  res[0] counts violating groups, res[1..4] the first one (start, size, unit, flags).
+__global__ void k_check_groups(const Grp* __restrict__ L, uint32_t n, SortBufs B, uint32_t* __restrict__ res) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const Grp gr = L[g];
+  if (gr.size < 2) return;
+  const Unit U = B.units[gr.unit];
+  const uint32_t* src = (gr.flags & kGrpAlt) ? B.sa2 : B.sa;
+  auto rot = [&](uint32_t e) { return (gr.flags & kGrpIdent) ? e : src[gr.start + e]; };
+  const uint32_t d = min(grp_depth(gr), 64u);
+  const uint8_t* t = B.text + U.toff;
+  const uint32_t v0 = rot(0);
+  bool bad = false;
+  for (uint32_t e = 1; e < min(gr.size, 64u) && !bad; e++) {
+    const uint32_t v = rot(e);
+    if (v >= U.len) { bad = true; break; }
+    for (uint32_t c = 0; c < d; c++)
+      if (t[(v0 + c) % U.len] != t[(v + c) % U.len]) { bad = true; break; }
+  }
+  if (bad && atomicAdd(&res[0], 1u) == 0) {
+    res[1] = gr.start; res[2] = gr.size; res[3] = gr.unit; res[4] = gr.flags;
+  }
+}
+
 __global__ void k_rank0_isa(const uint32_t* __restrict__ ulist, uint32_t n, const Unit* __restrict__ units,
                             const uint32_t* __restrict__ isa, uint32_t* __restrict__ rank0) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1690,8 +1755,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   O.deep = ws.typed<Grp>("sort_deep", S / 2 + nb + 16);
   O.dbg = nullptr;
   if (getenv("BZG_DEBUG")) {
-    O.dbg = reinterpret_cast<unsigned long long*>(ws.u32("sort_dbg", 16));
-    HIP_OK(hipMemsetAsync(O.dbg, 0, 64, st));
+    O.dbg = reinterpret_cast<unsigned long long*>(ws.u32("sort_dbg", 128));
+    HIP_OK(hipMemsetAsync(O.dbg, 0, 512, st));
   }
   // counters: 0..7 class counts (init), 8..16 class bounds + total, 17 tiles, 18 packed total,
   // 19 n_deep, 20 min depth
@@ -1718,6 +1783,19 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   };
   auto grid = [](uint64_t n) { return (unsigned)std::max<uint64_t>(1, ceil_div64(n, kT)); };
   static const bool debug = getenv("BZG_DEBUG") != nullptr;
+  static const bool check = getenv("BZG_CHECK") != nullptr;
+  uint32_t* chk = check ? ws.u32("sort_chk", 8) : nullptr;
+  auto check_list = [&](const Grp* L, uint32_t n, const char* what, int it, int cls) {
+    if (!check || n == 0) return;
+    HIP_OK(hipMemsetAsync(chk, 0, 32, st));
+    k_check_groups<<<grid(n), kT, 0, st>>>(L, n, B, chk);
+    uint32_t h[5];
+    HIP_OK(hipMemcpyAsync(h, chk, 20, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (h[0])
+      fprintf(stderr, "[bzg check] %s iter %d class %d: %u bad groups of %u; first start %u size %u unit %u depth %u flags %u\n",
+              what, it, cls, h[0], n, h[1], h[2], h[3], h[4] >> kGrpDepthShift, h[4] & 31u);
+  };
   static const bool use_s1p = [] {  // 1: packed groups finished in LDS (k_s1p); default: one pass per kernel (k_s1s)
     const char* e = getenv("BZG_S1P");
     return e && atoi(e) != 0;
@@ -1737,6 +1815,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   // ---- S1: byte passes over the buckets larger than kBig (tiled groups > kSG, packed ones <= kSG)
   while (n6 + n7 > 0) {
     ++passes;
+    check_list(cur6, n6, "S1 packed", passes, 6);
+    check_list(cur7, n7, "S1 tiled", passes, 7);
     if (n7) {
       k_group_tiles<<<grid(n7), kT, 0, st>>>(cur7, n7, TP);
       HIP_OK(hipGetLastError());
@@ -1848,6 +1928,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       if (debug)
         fprintf(stderr, "[bzg sort S2] iter %d: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", s2_iters,
                 ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5]);
+      for (int c = 0; c < 6; c++) check_list(C.l[c], ncls[c], "S2", s2_iters, c);
       if (ncls[0]) k_tiny<<<ceil_div(ncls[0], 8 * (kT / 64)), kT, 0, st>>>(C.l[0], ncls[0], B, O);
       if (ncls[1]) k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
       if (ncls[2]) k_bsort<32, 1, 2, false><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O);
@@ -1874,6 +1955,15 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       }
     }
     if (stats) stats->s2_iters = s2_iters;
+    if (debug && O.dbg) {
+      unsigned long long d[64];
+      HIP_OK(hipMemcpyAsync(d, O.dbg, sizeof(d), hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      for (int c = 1; c < 6; c++)
+        fprintf(stderr, "[bzg sort S2] class %d waves by round: %llu %llu %llu %llu %llu %llu %llu+ tail %llu\n", c,
+                d[8 + 8 * c], d[9 + 8 * c], d[10 + 8 * c], d[11 + 8 * c], d[12 + 8 * c], d[13 + 8 * c], d[14 + 8 * c],
+                d[15 + 8 * c]);
+    }
   }
   HIP_OK(hipGetLastError());
   read_counters();
@@ -1889,6 +1979,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     uint32_t* uflag = ws.u32("sort_uflag", nb + 16);
     HIP_OK(hipMemsetAsync(uflag, 0, 4 * (size_t)nb, st));
     HIP_OK(hipMemsetAsync(cnt + 20, 0xff, 4, st));
+    check_list(O.deep, n_deep, "S3 deep", 0, 8);
     k_fb_flag<<<grid(n_deep), kT, 0, st>>>(O.deep, n_deep, uflag, cnt + 20);
     HIP_OK(hipGetLastError());
     std::vector<uint32_t> hf(nb);
