@@ -44,7 +44,7 @@ ENGINE_EXPORTS = [
     "bzg_stream_init", "bzg_compress_device", "bzg_compress_host", "bzg_compress_host_stream",
     "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_stage_code_lengths", "bzg_last_stats",
     "bzg_release", "bzg_device_ok", "bzg_periodic_origptr", "bzg_seg_map", "bzg_seg_walk",
-    "bzg_find_magics",
+    "bzg_find_magics", "bzg_decompress_device", "bzg_decompress_host", "bzg_last_decode_stats",
 ]
 
 
@@ -85,6 +85,13 @@ class bzg_stats(ctypes.Structure):
     ]
 
 
+class bzg_decode_stats(ctypes.Structure):
+    _fields_ = [
+        ("total_ms", ctypes.c_float), ("blocks", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
+        ("out_bytes", ctypes.c_uint64),
+    ]
+
+
 _lib = None
 
 
@@ -121,6 +128,9 @@ def lib() -> ctypes.CDLL:
         L.bzg_find_magics.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64), vp]
         L.bzg_seg_walk.argtypes = [u32, ci, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.bzg_periodic_origptr.restype = ctypes.c_int32
+        L.bzg_decompress_device.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64), vp]
+        L.bzg_decompress_host.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64)]
+        L.bzg_last_decode_stats.argtypes = [ctypes.POINTER(bzg_decode_stats)]
         _lib = L
     return _lib
 
@@ -149,13 +159,37 @@ def buff_to_buff_compress(data: bytes, level: int = 9) -> bytes:
     return dst.raw[: dl.value]
 
 
-def buff_to_buff_decompress(data: bytes, out_cap: int) -> bytes:
+def buff_to_buff_decompress(data: bytes, out_cap: int, small: int = 0) -> bytes:
+    """BZ2_bzBuffToBuffDecompress (reference bzlib.c:1361-1410): the GPU decoder for small=0
+    when a device is present, the library's bit-serial decoder otherwise."""
     dst = ctypes.create_string_buffer(max(out_cap, 1))
     dl = ctypes.c_uint(out_cap)
-    rc = lib().BZ2_bzBuffToBuffDecompress(dst, ctypes.byref(dl), bytes(data), len(data), 0, 0)
+    rc = lib().BZ2_bzBuffToBuffDecompress(dst, ctypes.byref(dl), bytes(data), len(data), small, 0)
     if rc != BZ_OK:
         raise BzError(rc, "BZ2_bzBuffToBuffDecompress")
     return dst.raw[: dl.value]
+
+
+def decompress_device(d_in_ptr: int, n: int, d_out_ptr: int, out_cap: int, stream_ptr: int = 0):
+    """bzg_decompress_device on device-resident buffers: (return code, bytes written)."""
+    got = ctypes.c_uint64(0)
+    rc = lib().bzg_decompress_device(ctypes.c_void_p(d_in_ptr), n, ctypes.c_void_p(d_out_ptr), out_cap,
+                                     ctypes.byref(got), ctypes.c_void_p(stream_ptr or None))
+    return rc, got.value
+
+
+def decompress_host(data: bytes, out_cap: int):
+    """bzg_decompress_host: (return code, output bytes)."""
+    dst = ctypes.create_string_buffer(max(out_cap, 1))
+    got = ctypes.c_uint64(0)
+    rc = lib().bzg_decompress_host(bytes(data), len(data), dst, out_cap, ctypes.byref(got))
+    return rc, dst.raw[: got.value]
+
+
+def last_decode_stats() -> dict:
+    s = bzg_decode_stats()
+    lib().bzg_last_decode_stats(ctypes.byref(s))
+    return {k: getattr(s, k) for k, _ in bzg_decode_stats._fields_}
 
 
 def stream_compress(chunks, level: int = 9, finish_with_last: bool = False, out_chunk: int = 1 << 16,

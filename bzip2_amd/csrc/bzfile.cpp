@@ -8,14 +8,15 @@
 //     BZ_SEQUENCE_ERROR, a stdio failure is BZ_IO_ERROR, a compressed file that ends early
 //     is BZ_UNEXPECTED_EOF;
 //   * close on a null handle is a no-op with BZ_OK.
-// Compression goes through BZ2_bzCompress (the GPU engine), decompression through the
-// library's CPU decoder; both are driven through a BZ_MAX_UNUSED-byte staging buffer as the
+// Compression goes through BZ2_bzCompress (the GPU engine), stream decompression through the
+// library's CPU decoder (BZ2_bzBuffToBuffDecompress uses the GPU decoder); both are driven through a BZ_MAX_UNUSED-byte staging buffer as the
 // reference does, so the bytes written to the FILE are exactly those of the stream calls.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 
+#include "../../include/bzg.h"
 #include "../../include/bzlib.h"
 
 namespace {
@@ -341,6 +342,15 @@ int BZ2_bzBuffToBuffDecompress(char* dest, unsigned int* destLen, char* source, 
                                int verbosity) {
   if (!dest || !destLen || !source || (small != 0 && small != 1) || verbosity < 0 || verbosity > 4)
     return BZ_PARAM_ERROR;
+  // Whole in-memory streams decode on the GPU (decomp.hip, all blocks in parallel); the
+  // small-memory mode (small = 1) and GPU-less hosts use the library's bit-serial decoder.
+  static const bool force_cpu = std::getenv("BZG_CPU_DECODE") != nullptr;
+  if (!small && !force_cpu && bzg_device_ok()) {
+    uint64_t got = 0;
+    const int g = bzg_decompress_host(source, sourceLen, dest, *destLen, &got);
+    if (g == BZ_OK) *destLen = (unsigned)got;
+    return g;
+  }
   bz_stream z;
   std::memset(&z, 0, sizeof(z));
   int rc = BZ2_bzDecompressInit(&z, verbosity, small);

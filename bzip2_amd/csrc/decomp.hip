@@ -1,0 +1,873 @@
+// decomp.hip -- block-parallel .bz2 decompression on the GPU.
+//
+// The reference decodes a stream bit-serially, one block after another (decompress.c:232-…,
+// the decode tables of huffman.c:180-236, the inverse BWT and un-RLE1 of bzlib.c:531-677).
+// Here every block is decoded at once:
+//   0. block boundaries: every block-header / end-of-stream magic of the stream, at any bit
+//      offset (magic.hip).  A magic can also occur by chance inside coded data, so each
+//      candidate is decoded speculatively and the real blocks are the chain that starts at
+//      bit 32 and continues at each block's end bit.
+//   1. k_dec_huff, one wave per candidate: header, selectors (unary + MTF), delta-coded code
+//      lengths, canonical decode tables (9-bit lookup table + per-length limits in LDS), then
+//      the symbol loop -- Huffman decode, RUNA/RUNB run lengths, inverse MTF -- writing the
+//      block's BWT last column L.  All decoder state is wave-uniform; the 64 lanes hold the
+//      bit window (64 words + 64 prefetched) and the MTF list (4 entries per lane, a move to
+//      front is one lane shift), and stage output bytes in LDS for 256-byte stores.
+//   2. k_dec_tt, a workgroup per block: stable counting sort of L (per-wave byte histograms
+//      from 8-ballot byte matching), giving for every row j of the sorted rotations the
+//      packed successor Q[j] = (i << 8) | L[i] with LF(i) = j.
+//   3. k_dec_walk, a workgroup per block: the text is the walk j <- Q[j] >> 8 from origPtr,
+//      emitting Q[j] & 0xff (bzlib_private.h BZ_GET_FAST).  The walk is split at every 256th
+//      row (a ruling set): each thread walks its splitters' segments to the next splitter,
+//      one thread chains the segments (LDS) into output offsets, and the segments are walked
+//      again writing bytes.  A walk that closes its cycle before n steps (periodic blocks)
+//      repeats with the cycle's period, as the reference's n-step walk does.
+//   4. un-RLE1 as a 5-state machine (state = length of the current run since the last count
+//      byte, 4 = the next byte is a count).  k_dec_rle_scan composes each chunk's transition
+//      function for all 5 start states and chains the chunks; k_dec_rle_emit replays each
+//      chunk from its start state into the output with its CRC piece, and the block CRC is
+//      the GF(2) fold of the pieces.
+// The host checks the block CRCs and the combined CRC (bzlib.c BZ2_bzDecompress) and maps the
+// outcome to the return codes BZ2_bzBuffToBuffDecompress gives (bzlib.c:1361-1410): an error
+// in block k is reported after blocks < k are output; output that does not fit is
+// BZ_OUTBUFF_FULL; a stream that ends early is BZ_UNEXPECTED_EOF.
+#include <algorithm>
+#include <vector>
+
+#include "stages.h"
+
+#define BZ_OK 0
+#define BZ_DATA_ERROR (-4)
+#define BZ_DATA_ERROR_MAGIC (-5)
+#define BZ_UNEXPECTED_EOF (-7)
+#define BZ_OUTBUFF_FULL (-8)
+
+namespace bzg {
+namespace {
+
+constexpr int kLutBits = 9;
+constexpr int kMaxDecLen = 20;          // BZ_MAX_DECODE_LEN (bzlib_private.h:141)
+constexpr uint32_t kSelCap = 18002;     // BZ_MAX_SELECTORS: more is a data error (decompress.c:380)
+constexpr uint32_t kSplit = 256;        // ruling-set spacing of the inverse-BWT walk
+constexpr uint32_t kMaxSplit = 900000 / kSplit + 2;
+constexpr uint32_t kRleChunks = 256;    // un-RLE1 chunks (threads) per block
+constexpr uint32_t kBatch = 1024;       // block candidates decoded per pass
+
+struct DecRes {
+  int32_t status;   // 0, BZ_DATA_ERROR or BZ_UNEXPECTED_EOF
+  uint32_t nblock;  // bytes of L
+  uint64_t end_bit; // first bit after the block
+  uint32_t origptr;
+  uint32_t crc;     // stored block CRC
+  uint32_t rand;    // randomised-block bit
+  uint32_t pad;
+};
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Big-endian 32-bit word w of the stream (bytes past the end read as zero).
+__device__ __forceinline__ uint32_t stream_word(const uint8_t* __restrict__ in, uint64_t nbytes, uint64_t w) {
+  const uint64_t b = 4 * w;
+  if (b + 4 <= nbytes) return ((uint32_t)in[b] << 24) | ((uint32_t)in[b + 1] << 16) | ((uint32_t)in[b + 2] << 8) | in[b + 3];
+  uint32_t v = 0;
+  for (int k = 0; k < 4; k++) v = (v << 8) | (b + k < nbytes ? (uint32_t)in[b + k] : 0u);
+  return v;
+}
+
+// Wave-wide bit window: lane l holds word wbase + l in `cur` and wbase + 64 + l in `nxt`.
+// Positions only move forward; peek32 returns the 32 bits starting at absolute bit p.
+struct BitWindow {
+  const uint8_t* in;
+  uint64_t nbytes;
+  uint64_t wbase;
+  uint32_t cur, nxt;
+  __device__ void init(const uint8_t* i, uint64_t nb, uint64_t p) {
+    in = i;
+    nbytes = nb;
+    wbase = p >> 5;
+    cur = stream_word(in, nbytes, wbase + __lane_id());
+    nxt = stream_word(in, nbytes, wbase + 64 + __lane_id());
+  }
+  __device__ __forceinline__ uint32_t peek32(uint64_t p) {
+    uint64_t off = p - 32 * wbase;
+    while (off >= 2048) {
+      cur = nxt;
+      wbase += 64;
+      nxt = stream_word(in, nbytes, wbase + 64 + __lane_id());
+      off -= 2048;
+    }
+    const uint32_t wi = (uint32_t)(off >> 5), sh = (uint32_t)(off & 31);
+    const uint32_t hi = rdlane(cur, wi);
+    const uint32_t lo = wi < 63 ? rdlane(cur, wi + 1) : rdlane(nxt, 0);
+    return sh ? (hi << sh) | (lo >> (32 - sh)) : hi;
+  }
+  __device__ __forceinline__ uint32_t get(uint64_t& p, uint32_t k) {  // 1 <= k <= 32
+    const uint32_t v = peek32(p);
+    p += k;
+    return k == 32 ? v : v >> (32 - k);
+  }
+};
+
+// Move-to-front of entry r (>= 1) of the list held 4 entries per lane (lane l: entries
+// 4l..4l+3, entry 4l+k in byte k).  Returns the entry.
+__device__ __forceinline__ uint32_t mtf_take(uint32_t& word, uint32_t r) {
+  const uint32_t v = (rdlane(word, r >> 2) >> (8 * (r & 3))) & 0xffu;
+  const int lane = __lane_id();
+  uint32_t carry = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(word >> 24), 0x138, 0xf, 0xf, false);  // wave_shr:1
+  if (lane == 0) carry = v;
+  const uint32_t up = (word << 8) | carry;
+  const int d = (int)r - 4 * lane;  // bytes 0..d of this lane take their predecessor
+  const uint32_t m = d >= 3 ? 0xffffffffu : (d < 0 ? 0u : ((1u << (8 * (d + 1))) - 1u));
+  word = (up & m) | (word & ~m);
+  return v;
+}
+
+__global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in, uint64_t nbytes,
+                                                 const uint64_t* __restrict__ cbit, uint32_t nc, uint32_t nbmax,
+                                                 uint8_t* __restrict__ lbuf, uint8_t* __restrict__ selbuf,
+                                                 DecRes* __restrict__ res) {
+  __shared__ uint16_t lut[kNGroups][1 << kLutBits];  // (sym << 4) | len for codes <= 9 bits, 0 = longer
+  __shared__ uint16_t perm[kNGroups][kMaxAlpha];     // symbols in canonical order
+  __shared__ int32_t limit[kNGroups][kMaxDecLen + 1];
+  __shared__ int32_t cbase[kNGroups][kMaxDecLen + 1];
+  __shared__ uint8_t lens[kNGroups][kMaxAlpha];
+  __shared__ uint32_t cnt[kMaxDecLen + 1];
+  __shared__ uint32_t stage[64];                     // 256 output bytes
+  __shared__ uint8_t seq[256];
+  const uint32_t c = blockIdx.x;
+  if (c >= nc) return;
+  const uint32_t lane = __lane_id();
+  const uint64_t nbits = 8 * nbytes;
+  uint64_t p = cbit[c];
+  int status = 0;
+  uint32_t nblk = 0, origptr = 0, bcrc = 0, rnd = 0;
+  uint8_t* out = lbuf + (size_t)c * nbmax;
+  uint8_t* stage8 = reinterpret_cast<uint8_t*>(stage);
+  BitWindow W;
+  W.init(in, nbytes, p);
+  uint32_t ninuse = 0, g = 0, nsel = 0, alpha = 0;
+
+  // ---- block header (decompress.c:306-352): magic (found by the scan), CRC, rand bit, origPtr
+  if (p + 48 + 32 + 1 + 24 + 16 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
+  p += 48;
+  bcrc = W.get(p, 32);
+  rnd = W.get(p, 1);
+  origptr = W.get(p, 24);
+  if (origptr > nbmax) { status = BZ_DATA_ERROR; goto done; }
+  // ---- symbol map (decompress.c:354-370)
+  {
+    const uint32_t used16 = W.get(p, 16);
+    for (uint32_t j = 0; j < 16; j++) {
+      if (!((used16 >> (15 - j)) & 1u)) continue;
+      if (p + 16 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
+      const uint32_t w = W.get(p, 16);
+      for (uint32_t i = 0; i < 16; i++)
+        if ((w >> (15 - i)) & 1u) {
+          if (lane == 0) seq[ninuse] = (uint8_t)(16 * j + i);
+          ninuse++;
+        }
+    }
+  }
+  if (ninuse == 0) { status = BZ_DATA_ERROR; goto done; }
+  alpha = ninuse + 2;
+  // ---- selectors (decompress.c:375-410): unary MTF indices, then their inverse MTF
+  if (p + 18 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
+  g = W.get(p, 3);
+  nsel = W.get(p, 15);
+  if (g < 2 || g > 6 || nsel < 1 || nsel > kSelCap) { status = BZ_DATA_ERROR; goto done; }
+  {
+    uint32_t pos = 0x543210u;  // MTF list of table numbers, 4 bits per entry
+    uint32_t sreg = 0;
+    uint8_t* sdst = selbuf + (size_t)c * kSelCap;
+    for (uint32_t i = 0; i < nsel; i++) {
+      const uint32_t v = W.peek32(p);
+      const uint32_t o = (~v == 0u) ? 32u : (uint32_t)__builtin_clz(~v);  // leading 1 bits
+      const uint32_t need = o >= g ? g : o + 1;  // the g-th 1 bit is the error
+      if (p + need > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
+      if (o >= g) { status = BZ_DATA_ERROR; goto done; }
+      p += o + 1;
+      const uint32_t t = (pos >> (4 * o)) & 0xfu;
+      if (o) {
+        const uint32_t low = pos & ((1u << (4 * o)) - 1u);
+        pos = (pos & ~((1u << (4 * (o + 1))) - 1u)) | (low << 4) | t;
+      }
+      if (lane == (i & 63)) sreg = t;
+      if ((i & 63) == 63 || i + 1 == nsel) {
+        const uint32_t b0 = i & ~63u;
+        if (b0 + lane <= i) sdst[b0 + lane] = (uint8_t)sreg;
+      }
+    }
+  }
+  // ---- code lengths (decompress.c:412-425): 5-bit start, then per symbol 0 | 1(0:+1, 1:-1)
+  for (uint32_t t = 0; t < g; t++) {
+    if (p + 5 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
+    uint32_t curr = W.get(p, 5);
+    for (uint32_t s = 0; s < alpha; s++) {
+      for (;;) {
+        if (curr < 1 || curr > (uint32_t)kMaxDecLen) { status = BZ_DATA_ERROR; goto done; }
+        if (p + 2 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
+        const uint32_t two = W.peek32(p) >> 30;
+        if (!(two & 2u)) {
+          p += 1;
+          break;
+        }
+        p += 2;
+        curr = (two & 1u) ? curr - 1 : curr + 1;
+      }
+      if (lane == 0) lens[t][s] = (uint8_t)curr;
+    }
+  }
+  __syncthreads();
+  // ---- decode tables (huffman.c:180-236 accepts exactly the complete codes: Kraft sum 1)
+  for (uint32_t t = 0; t < g; t++) {
+    if (lane <= (uint32_t)kMaxDecLen) cnt[lane] = 0;
+    __syncthreads();
+    for (uint32_t s = lane; s < alpha; s += 64) atomicAdd(&cnt[lens[t][s]], 1u);
+    __syncthreads();
+    uint32_t kraft = 0;
+    for (int l = 1; l <= kMaxDecLen; l++) kraft += cnt[l] << (kMaxDecLen - l);
+    kraft = uni(kraft);
+    if (kraft != (1u << kMaxDecLen)) { status = BZ_DATA_ERROR; goto done; }
+    if (lane == 0) {
+      int32_t code = 0, off = 0;
+      for (int l = 1; l <= kMaxDecLen; l++) {
+        const int32_t k = (int32_t)cnt[l];
+        limit[t][l] = code + k - 1;
+        cbase[t][l] = off - code;
+        cnt[l] = (uint32_t)off;  // becomes the running slot of length l
+        off += k;
+        code = (code + k) << 1;
+      }
+      for (uint32_t s = 0; s < alpha; s++) perm[t][cnt[lens[t][s]]++] = (uint16_t)s;
+    }
+    __syncthreads();
+    for (uint32_t x = lane; x < (1u << kLutBits); x += 64) {
+      uint16_t e = 0;
+      for (int l = 1; l <= kLutBits; l++) {
+        const int32_t v = (int32_t)(x >> (kLutBits - l));
+        if (v <= limit[t][l]) {
+          e = (uint16_t)((perm[t][cbase[t][l] + v] << 4) | l);
+          break;
+        }
+      }
+      lut[t][x] = e;
+    }
+    __syncthreads();
+  }
+  // ---- symbols (decompress.c:444-664): Huffman, RUNA/RUNB, inverse MTF, block fill limits
+  {
+    uint32_t word = reinterpret_cast<const uint32_t*>(seq)[lane];  // MTF list: in-use bytes ascending
+    const uint32_t eob = ninuse + 1;
+    const uint8_t* ssrc = selbuf + (size_t)c * kSelCap;
+    uint32_t sreg = 0, gi = 0, gleft = 0, t = 0;
+    uint32_t run = 0, rdig = 0;
+    bool inrun = false;
+    for (;;) {
+      if (gleft == 0) {
+        if (gi >= nsel) { status = BZ_DATA_ERROR; goto done; }
+        if ((gi & 63) == 0) sreg = gi + lane < nsel ? ssrc[gi + lane] : 0u;
+        t = rdlane(sreg, gi & 63);
+        gi++;
+        gleft = kGroupSize;
+      }
+      gleft--;
+      const uint32_t v32 = W.peek32(p);
+      uint32_t e = uni(lut[t][v32 >> (32 - kLutBits)]);
+      uint32_t len, sym;
+      if (e) {
+        len = e & 15u;
+        sym = e >> 4;
+      } else {
+        len = kLutBits + 1;
+        for (;; len++) {
+          const int32_t v = (int32_t)(v32 >> (32 - len));
+          if (v <= limit[t][len]) break;
+        }
+        sym = uni(perm[t][cbase[t][len] + (int32_t)(v32 >> (32 - len))]);
+      }
+      if (p + len > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
+      p += len;
+      if (sym <= 1) {  // RUNA / RUNB: bijective base-2 digits of a run of the front byte
+        if (inrun && run > (1u << 20)) { status = BZ_DATA_ERROR; goto done; }
+        run += (sym + 1) << rdig;
+        rdig++;
+        inrun = true;
+        continue;
+      }
+      if (inrun) {
+        if (nblk + run > nbmax) { status = BZ_DATA_ERROR; goto done; }
+        const uint32_t u = rdlane(word, 0) & 0xffu;
+        while (run) {
+          const uint32_t fill = nblk & 255u, take = min(run, 256u - fill);
+          for (uint32_t i = lane; i < take; i += 64) stage8[fill + i] = (uint8_t)u;
+          nblk += take;
+          run -= take;
+          if ((nblk & 255u) == 0) {
+            __syncthreads();
+            reinterpret_cast<uint32_t*>(out + nblk - 256)[lane] = stage[lane];
+            __syncthreads();
+          }
+        }
+        rdig = 0;
+        inrun = false;
+      }
+      if (sym == eob) break;
+      if (nblk == nbmax) { status = BZ_DATA_ERROR; goto done; }
+      const uint32_t v = mtf_take(word, sym - 1);
+      if (lane == 0) stage8[nblk & 255u] = (uint8_t)v;
+      nblk++;
+      if ((nblk & 255u) == 0) {
+        __syncthreads();
+        reinterpret_cast<uint32_t*>(out + nblk - 256)[lane] = stage[lane];
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+    const uint32_t rem = nblk & 255u;
+    for (uint32_t i = lane; i < rem; i += 64) out[(nblk & ~255u) + i] = stage8[i];
+    if (origptr >= nblk) status = BZ_DATA_ERROR;
+  }
+done:
+  if (lane == 0) {
+    DecRes r;
+    r.status = status;
+    r.nblock = nblk;
+    r.end_bit = p;
+    r.origptr = origptr;
+    r.crc = bcrc;
+    r.rand = rnd;
+    r.pad = 0;
+    res[c] = r;
+  }
+}
+
+// ---- stage 2: Q[j] = (i << 8) | L[i] for LF(i) = j (the reference's tt, decompress.c:786-791)
+__global__ void __launch_bounds__(1024) k_dec_tt(const uint8_t* __restrict__ lbuf, const uint32_t* __restrict__ slot,
+                                                 const DecRes* __restrict__ res, uint32_t nbmax,
+                                                 uint32_t* __restrict__ qbuf) {
+  __shared__ uint32_t hist[16][256];
+  __shared__ uint32_t sh[16];
+  const uint32_t b = blockIdx.x, c = slot[b];
+  const uint32_t n = res[c].nblock;
+  const uint8_t* L = lbuf + (size_t)c * nbmax;
+  uint32_t* Q = qbuf + (size_t)b * nbmax;
+  const uint32_t tid = threadIdx.x, w = tid >> 6, lane = __lane_id();
+  for (uint32_t i = tid; i < 16 * 256; i += 1024) (&hist[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t seg = ceil_div(ceil_div(n, 16), 64) * 64;
+  const uint32_t lo = min(n, w * seg), hi = min(n, lo + seg);
+  for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const bool in = i < hi;
+    const uint32_t d = in ? L[i] : 0u;
+    const uint64_t m = match_byte(d, __ballot(in));
+    if (in && (m & lanemask_lt()) == 0) hist[w][d] += (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  uint32_t tot = 0;
+  if (tid < 256) {
+    for (int k = 0; k < 16; k++) {
+      const uint32_t x = hist[k][tid];
+      hist[k][tid] = tot;
+      tot += x;
+    }
+  }
+  const uint32_t incl = block_incl_sum(tot, sh, (uint32_t*)nullptr);
+  if (tid < 256) {
+    const uint32_t C = incl - tot;
+    for (int k = 0; k < 16; k++) hist[k][tid] += C;
+  }
+  __syncthreads();
+  for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const bool in = i < hi;
+    const uint32_t d = in ? L[i] : 0u;
+    const uint64_t m = match_byte(d, __ballot(in));
+    if (in) {
+      const uint32_t pos = hist[w][d] + (uint32_t)__popcll(m & lanemask_lt());
+      Q[pos] = (i << 8) | d;
+    }
+    if (in && (m & lanemask_lt()) == 0) hist[w][d] += (uint32_t)__popcll(m);
+  }
+}
+
+// Byte writer for a thread-sequential output run: whole aligned words as 4-byte stores, the
+// partial words at either end (shared with other threads) as byte stores.
+struct ByteSink {
+  uint8_t* base;
+  uintptr_t lo;  // address of the first byte this sink writes
+  uintptr_t a;   // address of the next byte
+  uint32_t acc;
+  __device__ void init(uint8_t* p) {
+    base = p;
+    lo = a = reinterpret_cast<uintptr_t>(p);
+    acc = 0;
+  }
+  __device__ __forceinline__ void put(uint32_t b) {
+    acc |= b << (8 * (a & 3));
+    if ((a & 3) == 3) {
+      const uintptr_t w = a - 3;
+      if (w >= lo) {
+        *reinterpret_cast<uint32_t*>(w) = acc;
+      } else {
+        for (uintptr_t q = lo; q <= a; q++) *reinterpret_cast<uint8_t*>(q) = (uint8_t)(acc >> (8 * (q & 3)));
+      }
+      acc = 0;
+    }
+    a++;
+  }
+  __device__ void finish() {
+    const uintptr_t w = a & ~(uintptr_t)3;
+    for (uintptr_t q = max(w, lo); q < a; q++) *reinterpret_cast<uint8_t*>(q) = (uint8_t)(acc >> (8 * (q & 3)));
+  }
+};
+
+__device__ __forceinline__ uint32_t rand_flip(const uint32_t* __restrict__ rbits, uint32_t period, uint32_t t) {
+  const uint32_t k = t % period;
+  return (rbits[k >> 5] >> (k & 31)) & 1u;
+}
+
+// ---- stage 3: the walk from origPtr (BZ_GET_FAST), split at a ruling set of rows
+__global__ void __launch_bounds__(1024) k_dec_walk(const uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ slot,
+                                                   const DecRes* __restrict__ res, uint32_t nbmax,
+                                                   const uint32_t* __restrict__ rbits, uint32_t rperiod,
+                                                   uint8_t* __restrict__ ybuf, uint32_t* __restrict__ cycle_out) {
+  __shared__ uint16_t nx[kMaxSplit];
+  __shared__ uint32_t ln[kMaxSplit];
+  __shared__ uint32_t of[kMaxSplit];
+  __shared__ uint32_t cyc_sh;
+  const uint32_t b = blockIdx.x, c = slot[b];
+  const uint32_t n = res[c].nblock, o = res[c].origptr;
+  const bool rnd = res[c].rand != 0;
+  const uint32_t* Q = qbuf + (size_t)b * nbmax;
+  uint8_t* Y = ybuf + (size_t)c * nbmax;
+  const uint32_t ns = ceil_div(n, kSplit) + 1, start = ns - 1;
+  auto slot_of = [&](uint32_t s) { return s == start ? o : s * kSplit; };
+  auto is_split = [&](uint32_t j) { return j == o || (j % kSplit) == 0; };
+  auto id_of = [&](uint32_t j) { return j == o ? start : j / kSplit; };
+  for (uint32_t s = threadIdx.x; s < ns; s += blockDim.x) {
+    uint32_t j = slot_of(s), len = 0;
+    if (s != start && j >= n) {  // past the rows (n a multiple of the spacing): unused
+      nx[s] = (uint16_t)start;
+      ln[s] = 0;
+      of[s] = ~0u;
+      continue;
+    }
+    do {
+      j = Q[j] >> 8;
+      len++;
+    } while (!is_split(j));
+    nx[s] = (uint16_t)id_of(j);
+    ln[s] = len;
+    of[s] = ~0u;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = start, off = 0;
+    for (;;) {
+      of[s] = off;
+      off += ln[s];
+      if (off >= n) break;
+      s = nx[s];
+      if (s == start) break;
+    }
+    cyc_sh = min(off, n);
+  }
+  __syncthreads();
+  const uint32_t cyc = cyc_sh;
+  for (uint32_t s = threadIdx.x; s < ns; s += blockDim.x) {
+    const uint32_t t0 = of[s];
+    if (t0 == ~0u) continue;
+    const uint32_t len = min(ln[s], cyc - t0);
+    uint32_t j = slot_of(s), t = t0;
+    ByteSink sink;
+    sink.init(Y + t0);
+    for (uint32_t k = 0; k < len; k++, t++) {
+      const uint32_t e = Q[j];
+      j = e >> 8;
+      uint32_t y = e & 0xffu;
+      if (rnd) y ^= rand_flip(rbits, rperiod, t);
+      sink.put(y);
+    }
+    sink.finish();
+  }
+  if (cyc < n) {  // the walk repeats its cycle (periodic blocks): y[t] = raw[t mod cyc]
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t t = cyc + threadIdx.x; t < n; t += blockDim.x) {
+      const uint32_t s = t % cyc;
+      uint32_t y = Y[s];
+      if (rnd) y ^= rand_flip(rbits, rperiod, s) ^ rand_flip(rbits, rperiod, t);
+      Y[t] = (uint8_t)y;
+    }
+  }
+  if (threadIdx.x == 0) cycle_out[b] = cyc;
+}
+
+// ---- stage 4: un-RLE1 (bzlib.c:531-677) as a 5-state machine
+// state s: 0 = after a count byte (or at the block start), 1..3 = current run length, 4 = the
+// next byte is a count.  A block that ends in state 4 is corrupt (bzlib.c:627-633).
+__device__ __forceinline__ void rle_step(uint32_t& s, uint32_t& cnt, uint32_t x, uint32_t prev) {
+  if (s == 4) {
+    cnt += x;
+    s = 0;
+  } else {
+    cnt += 1;
+    s = (s == 0 || x != prev) ? 1u : s + 1;
+  }
+}
+
+__device__ __forceinline__ void rle_chunk(uint32_t n, uint32_t tid, uint32_t& lo, uint32_t& hi) {
+  const uint32_t cs = ceil_div(ceil_div(n, kRleChunks), 16) * 16;
+  lo = min(n, tid * cs);
+  hi = min(n, lo + cs);
+}
+
+__global__ void __launch_bounds__(kRleChunks) k_dec_rle_scan(const uint8_t* __restrict__ ybuf,
+                                                              const uint32_t* __restrict__ slot,
+                                                              const DecRes* __restrict__ res, uint32_t nbmax,
+                                                              uint32_t* __restrict__ info, uint32_t* __restrict__ btot) {
+  __shared__ uint32_t fn[kRleChunks][5];  // (count << 3) | end state, per start state
+  const uint32_t b = blockIdx.x, c = slot[b];
+  const uint32_t n = res[c].nblock;
+  const uint8_t* Y = ybuf + (size_t)c * nbmax;
+  uint32_t lo, hi;
+  rle_chunk(n, threadIdx.x, lo, hi);
+  uint32_t st[5] = {0, 1, 2, 3, 4}, ct[5] = {0, 0, 0, 0, 0};
+  uint32_t prev = lo ? Y[lo - 1] : 0u;
+  uint32_t i = lo;
+  for (; i + 16 <= hi; i += 16) {
+    const uint4 q = *reinterpret_cast<const uint4*>(Y + i);
+    const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t x = (wv[k >> 2] >> (8 * (k & 3))) & 0xffu;
+#pragma unroll
+      for (int s = 0; s < 5; s++) rle_step(st[s], ct[s], x, prev);
+      prev = x;
+    }
+  }
+  for (; i < hi; i++) {
+    const uint32_t x = Y[i];
+#pragma unroll
+    for (int s = 0; s < 5; s++) rle_step(st[s], ct[s], x, prev);
+    prev = x;
+  }
+#pragma unroll
+  for (int s = 0; s < 5; s++) fn[threadIdx.x][s] = (ct[s] << 3) | st[s];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0, acc = 0;
+    for (uint32_t k = 0; k < kRleChunks; k++) {
+      info[(size_t)b * kRleChunks + k] = (acc << 3) | s;
+      const uint32_t f = fn[k][s];
+      acc += f >> 3;
+      s = f & 7u;
+    }
+    btot[2 * b] = acc;
+    btot[2 * b + 1] = s;
+  }
+}
+
+__device__ __forceinline__ uint32_t gf_mul_d(uint32_t a, uint32_t b) {  // a*b mod P (MSB-first CRC-32)
+  uint32_t r = 0;
+  for (int i = 31; i >= 0; i--) {
+    r = (r & 0x80000000u) ? (r << 1) ^ 0x04C11DB7u : (r << 1);
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t shift8(uint32_t a, const uint32_t* __restrict__ xp2, uint64_t len) {
+  // a * x^(8 len) mod P; xp2[k] = x^(8 * 2^k)
+  for (int k = 0; len; k++, len >>= 1)
+    if (len & 1) a = gf_mul_d(a, xp2[k]);
+  return a;
+}
+
+__global__ void __launch_bounds__(kRleChunks) k_dec_rle_emit(const uint8_t* __restrict__ ybuf,
+                                                              const uint32_t* __restrict__ slot,
+                                                              const DecRes* __restrict__ res, uint32_t nbmax,
+                                                              const uint32_t* __restrict__ info,
+                                                              const uint32_t* __restrict__ btot,
+                                                              const uint64_t* __restrict__ boff,
+                                                              const uint32_t* __restrict__ crc_table,
+                                                              const uint32_t* __restrict__ xp2_g, uint8_t* __restrict__ out,
+                                                              uint32_t* __restrict__ bcrc) {
+  __shared__ uint32_t tab[256];
+  __shared__ uint32_t xp2[48];
+  __shared__ uint32_t red[kRleChunks / 64];
+  const uint32_t b = blockIdx.x, c = slot[b];
+  const uint32_t n = res[c].nblock;
+  const uint8_t* Y = ybuf + (size_t)c * nbmax;
+  tab[threadIdx.x] = crc_table[threadIdx.x];
+  if (threadIdx.x < 48) xp2[threadIdx.x] = xp2_g[threadIdx.x];
+  __syncthreads();
+  uint32_t lo, hi;
+  rle_chunk(n, threadIdx.x, lo, hi);
+  const uint32_t inf = info[(size_t)b * kRleChunks + threadIdx.x];
+  const uint32_t off = inf >> 3, total = btot[2 * b];
+  uint32_t s = inf & 7u;
+  uint32_t prev = lo ? Y[lo - 1] : 0u;
+  uint32_t crc = 0, emitted = 0;
+  ByteSink sink;
+  sink.init(out + boff[b] + off);
+  auto emit = [&](uint32_t x) {
+    crc = (crc << 8) ^ tab[(crc >> 24) ^ x];
+    sink.put(x);
+  };
+  for (uint32_t i = lo; i < hi; i++) {
+    const uint32_t x = Y[i];
+    if (s == 4) {
+      for (uint32_t k = 0; k < x; k++) emit(prev);
+      emitted += x;
+      s = 0;
+    } else {
+      emit(x);
+      emitted++;
+      s = (s == 0 || x != prev) ? 1u : s + 1;
+    }
+    prev = x;
+  }
+  sink.finish();
+  uint32_t part = emitted ? shift8(crc, xp2, (uint64_t)(total - off - emitted)) : 0u;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) part ^= (uint32_t)__shfl_xor((int)part, o, 64);
+  if (__lane_id() == 0) red[threadIdx.x >> 6] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t x = shift8(0xffffffffu, xp2, total);
+    for (uint32_t k = 0; k < kRleChunks / 64; k++) x ^= red[k];
+    bcrc[b] = ~x;
+  }
+}
+
+// Positions t (mod the period) whose byte the randomised-block mask flips: t = A_{k+1} - 2 with
+// A the running sum of the reference's random-number table (bzlib_private.h:167-179
+// BZ_RAND_*, applied to every byte the walk fetches, count bytes included).
+const uint16_t kRNums[512] = {
+#include "rnums.inc"
+};
+
+}  // namespace
+
+struct DecodeWork {
+  uint32_t* rbits = nullptr;
+  uint32_t rperiod = 0;
+};
+
+static void rand_table(Workspace& ws, uint32_t*& bits, uint32_t& period) {
+  uint32_t sum = 0;
+  for (int k = 0; k < 512; k++) sum += kRNums[k];
+  period = sum;
+  const uint32_t words = (sum + 31) / 32;
+  std::vector<uint32_t> h(words, 0u);
+  uint32_t a = 0;
+  for (int k = 0; k < 512; k++) {
+    a += kRNums[k];
+    const uint32_t t = a - 2;
+    h[t >> 5] |= 1u << (t & 31);
+  }
+  bits = ws.u32("dec_rbits", words);
+  HIP_OK(hipMemcpy(bits, h.data(), 4 * words, hipMemcpyHostToDevice));
+}
+
+// Decodes the .bz2 stream d_in[0, n) into d_out (capacity out_cap).  Returns BZ_OK when the
+// stream ends correctly, else the code BZ2_bzBuffToBuffDecompress returns for it.
+int decode_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t out_cap,
+                 uint64_t* out_len, DecodeStats* stats, hipStream_t st) {
+  *out_len = 0;
+  uint64_t produced = 0;
+  auto eof_code = [&] { return produced == out_cap ? BZ_OUTBUFF_FULL : BZ_UNEXPECTED_EOF; };
+  // header "BZh1".."BZh9" (decompress.c:281-292), checked byte by byte as the input arrives
+  uint8_t h[16] = {0};
+  const uint64_t hn = std::min<uint64_t>(n, 4);
+  if (hn) HIP_OK(hipMemcpyAsync(h, d_in, hn, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  const uint8_t want[3] = {'B', 'Z', 'h'};
+  for (uint64_t i = 0; i < hn; i++) {
+    if (i < 3 && h[i] != want[i]) return BZ_DATA_ERROR_MAGIC;
+    if (i == 3 && (h[3] < '1' || h[3] > '9')) return BZ_DATA_ERROR_MAGIC;
+  }
+  if (n < 4) return eof_code();
+  const uint32_t nbmax = 100000u * (uint32_t)(h[3] - '0');
+  const uint64_t nbits = 8 * n;
+
+  std::vector<uint64_t> found;
+  find_magics_stage(d_in, n, found, st);
+  // reads `len` bytes at byte offset `at` (bounded by the stream)
+  auto read_bytes = [&](uint64_t at, uint32_t len, uint8_t* dst) {
+    std::fill(dst, dst + len, 0);
+    if (at < n) {
+      HIP_OK(hipMemcpyAsync(dst, d_in + at, std::min<uint64_t>(len, n - at), hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+    }
+  };
+  auto bits_at = [&](uint64_t bit, uint32_t k) -> uint64_t {  // k <= 48 bits at `bit`
+    uint8_t b[8];
+    read_bytes(bit >> 3, 8, b);
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v = (v << 8) | b[i];
+    return (v << (bit & 7)) >> (64 - k);
+  };
+  // no magic where the previous block ended: the reference compares the header bytes one by
+  // one (decompress.c:308-322, 650-660), so the outcome is EOF or a data error
+  auto bad_header = [&](uint64_t pos) -> int {
+    const uint8_t blk[6] = {0x31, 0x41, 0x59, 0x26, 0x53, 0x59}, eos[6] = {0x17, 0x72, 0x45, 0x38, 0x50, 0x90};
+    if (pos + 8 > nbits) return eof_code();
+    const uint32_t first = (uint32_t)bits_at(pos, 8);
+    const uint8_t* m = first == 0x31 ? blk : first == 0x17 ? eos : nullptr;
+    if (!m) return BZ_DATA_ERROR;
+    for (int k = 1; k < 6; k++) {
+      if (pos + 8 * (k + 1) > nbits) return eof_code();
+      if ((uint32_t)bits_at(pos + 8 * k, 8) != m[k]) return BZ_DATA_ERROR;
+    }
+    return BZ_DATA_ERROR;  // not reached: the scan finds every complete magic
+  };
+
+  DecodeWork dw;
+  rand_table(ws, dw.rbits, dw.rperiod);
+  uint32_t combined = 0;
+  uint64_t pos = 32;
+  DecodeStats ds{};
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  struct EvGuard {
+    hipEvent_t a, b;
+    ~EvGuard() {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+    }
+  } evg{e0, e1};
+  HIP_OK(hipEventRecord(e0, st));
+  int rc = BZ_OK;
+  for (;;) {
+    auto it = std::lower_bound(found.begin(), found.end(), 2 * pos);
+    if (it == found.end() || (*it >> 1) != pos) {
+      rc = bad_header(pos);
+      break;
+    }
+    if (*it & 1) {  // end of stream: stored combined CRC (decompress.c:662-680)
+      if (pos + 48 + 32 > nbits) {
+        rc = eof_code();
+        break;
+      }
+      const uint32_t stored = (uint32_t)bits_at(pos + 48, 32);
+      rc = stored == combined ? BZ_OK : BZ_DATA_ERROR;
+      break;
+    }
+    // candidates of this pass: block-kind magics from pos on
+    std::vector<uint64_t> cand;
+    for (auto q = it; q != found.end() && cand.size() < kBatch; ++q)
+      if (!(*q & 1)) cand.push_back(*q >> 1);
+    const uint32_t nc = (uint32_t)cand.size();
+    uint64_t* d_cbit = ws.typed<uint64_t>("dec_cbit", nc);
+    uint8_t* lbuf = ws.u8("dec_l", (size_t)nc * nbmax + 64);
+    uint8_t* selbuf = ws.u8("dec_sel", (size_t)nc * kSelCap + 64);
+    DecRes* d_res = ws.typed<DecRes>("dec_res", nc);
+    HIP_OK(hipMemcpyAsync(d_cbit, cand.data(), 8 * nc, hipMemcpyHostToDevice, st));
+    k_dec_huff<<<nc, 64, 0, st>>>(d_in, n, d_cbit, nc, nbmax, lbuf, selbuf, d_res);
+    HIP_OK(hipGetLastError());
+    std::vector<DecRes> hres(nc);
+    HIP_OK(hipMemcpyAsync(hres.data(), d_res, sizeof(DecRes) * nc, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    ds.candidates += nc;
+    // the chain of real blocks through this pass's candidates
+    std::vector<uint32_t> chain;
+    int pending = BZ_OK;
+    bool at_end = false;  // the chain left this pass's window at a non-candidate / EOS
+    for (;;) {
+      auto ci = std::lower_bound(cand.begin(), cand.end(), pos);
+      if (ci == cand.end() || *ci != pos) {
+        at_end = true;
+        break;
+      }
+      const uint32_t k = (uint32_t)(ci - cand.begin());
+      if (hres[k].status != 0) {
+        pending = hres[k].status == BZ_UNEXPECTED_EOF ? 1 : BZ_DATA_ERROR;  // 1: EOF marker
+        break;
+      }
+      chain.push_back(k);
+      pos = hres[k].end_bit;
+    }
+    (void)at_end;
+    const uint32_t R = (uint32_t)chain.size();
+    int stop = BZ_OK;  // a reason to stop inside this pass's blocks
+    if (R) {
+      uint32_t* d_slot = ws.u32("dec_slot", R);
+      HIP_OK(hipMemcpyAsync(d_slot, chain.data(), 4 * R, hipMemcpyHostToDevice, st));
+      uint32_t* qbuf = ws.u32("dec_q", (size_t)R * nbmax + 16);
+      uint32_t* cyc = ws.u32("dec_cyc", R);
+      uint32_t* info = ws.u32("dec_info", (size_t)R * kRleChunks);
+      uint32_t* btot = ws.u32("dec_btot", 2 * R);
+      k_dec_tt<<<R, 1024, 0, st>>>(lbuf, d_slot, d_res, nbmax, qbuf);
+      HIP_OK(hipGetLastError());
+      // Y overwrites L in place: the walk reads only Q
+      k_dec_walk<<<R, 1024, 0, st>>>(qbuf, d_slot, d_res, nbmax, dw.rbits, dw.rperiod, lbuf, cyc);
+      HIP_OK(hipGetLastError());
+      k_dec_rle_scan<<<R, kRleChunks, 0, st>>>(lbuf, d_slot, d_res, nbmax, info, btot);
+      HIP_OK(hipGetLastError());
+      std::vector<uint32_t> htot(2 * R);
+      HIP_OK(hipMemcpyAsync(htot.data(), btot, 8 * R, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      // output order: block r is written only if every earlier block was; a block that ends
+      // in a pending count byte is corrupt (data error once its output fits)
+      std::vector<uint64_t> hoff(R);
+      uint32_t emit = 0;
+      uint64_t acc = produced;
+      for (uint32_t r = 0; r < R; r++) {
+        if (acc + htot[2 * r] > out_cap) {
+          stop = BZ_OUTBUFF_FULL;
+          break;
+        }
+        if (htot[2 * r + 1] == 4) {
+          stop = BZ_DATA_ERROR;
+          break;
+        }
+        hoff[r] = acc;
+        acc += htot[2 * r];
+        emit++;
+      }
+      if (emit) {
+        uint64_t* d_boff = ws.typed<uint64_t>("dec_boff", emit);
+        uint32_t* d_bcrc = ws.u32("dec_bcrc", emit);
+        HIP_OK(hipMemcpyAsync(d_boff, hoff.data(), 8 * emit, hipMemcpyHostToDevice, st));
+        k_dec_rle_emit<<<emit, kRleChunks, 0, st>>>(lbuf, d_slot, d_res, nbmax, info, btot, d_boff,
+                                                     ws.crc_table(), ws.xpow2_table(), d_out, d_bcrc);
+        HIP_OK(hipGetLastError());
+        std::vector<uint32_t> hcrc(emit);
+        HIP_OK(hipMemcpyAsync(hcrc.data(), d_bcrc, 4 * emit, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        for (uint32_t r = 0; r < emit; r++) {
+          produced += htot[2 * r];
+          if (hcrc[r] != hres[chain[r]].crc) {  // bzlib.c: block CRC check after its output
+            stop = BZ_DATA_ERROR;
+            break;
+          }
+          combined = ((combined << 1) | (combined >> 31)) ^ hcrc[r];
+          ds.blocks++;
+        }
+      }
+    }
+    if (stop != BZ_OK) {
+      rc = stop;
+      break;
+    }
+    if (pending != BZ_OK) {
+      rc = pending == 1 ? eof_code() : BZ_DATA_ERROR;
+      break;
+    }
+  }
+  HIP_OK(hipEventRecord(e1, st));
+  HIP_OK(hipEventSynchronize(e1));
+  (void)hipEventElapsedTime(&ds.total_ms, e0, e1);
+  ds.out_bytes = produced;
+  if (stats) *stats = ds;
+  *out_len = produced;
+  return rc;
+}
+
+}  // namespace bzg

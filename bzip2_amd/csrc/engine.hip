@@ -944,6 +944,55 @@ int bzg_compress_host_stream(const void* src, uint64_t n, unsigned flags, bzg_st
   return rc;
 }
 
+// ---------------------------------------------------------------- decompression
+static std::mutex g_dstats_mu;
+static bzg_decode_stats g_dlast{};
+
+static void publish_decode_stats(const DecodeStats& d) {
+  std::lock_guard<std::mutex> g(g_dstats_mu);
+  g_dlast.total_ms = d.total_ms;
+  g_dlast.blocks = d.blocks;
+  g_dlast.candidates = d.candidates;
+  g_dlast.out_bytes = d.out_bytes;
+}
+
+int bzg_decompress_device(const void* d_in, uint64_t n, void* d_out, uint64_t out_cap, uint64_t* out_len, void* stream) {
+  if ((n && !d_in) || (out_cap && !d_out) || !out_len) return BZ_PARAM_ERROR;
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  return guarded([&] {
+    Lease L(current_device());
+    hipStream_t s = stream ? (hipStream_t)stream : L->stream;
+    DecodeStats ds;
+    const int rc = decode_stage(L->ws, (const uint8_t*)d_in, n, (uint8_t*)d_out, out_cap, out_len, &ds, s);
+    publish_decode_stats(ds);
+    return rc;
+  });
+}
+
+int bzg_decompress_host(const void* src, uint64_t n, void* dst, uint64_t dst_cap, uint64_t* dst_len) {
+  if ((n && !src) || (dst_cap && !dst) || !dst_len) return BZ_PARAM_ERROR;
+  if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
+  return guarded([&] {
+    Lease L(current_device());
+    uint8_t* din = L->ws.u8("dhost_in", n + 16);
+    uint8_t* dout = L->ws.u8("dhost_out", dst_cap + 16);
+    if (n) HIP_OK(hipMemcpyAsync(din, src, n, hipMemcpyHostToDevice, L->stream));
+    DecodeStats ds;
+    uint64_t got = 0;
+    const int rc = decode_stage(L->ws, din, n, dout, dst_cap, &got, &ds, L->stream);
+    if (got) HIP_OK(hipMemcpyAsync(dst, dout, got, hipMemcpyDeviceToHost, L->stream));
+    HIP_OK(hipStreamSynchronize(L->stream));
+    *dst_len = got;
+    publish_decode_stats(ds);
+    return rc;
+  });
+}
+
+void bzg_last_decode_stats(bzg_decode_stats* out) {
+  std::lock_guard<std::mutex> g(g_dstats_mu);
+  if (out) *out = g_dlast;
+}
+
 void bzg_last_stats(bzg_stats* out) {
   std::lock_guard<std::mutex> g(g_stats_mu);
   if (out) *out = g_last;

@@ -110,4 +110,17 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
                     uint32_t nblocks, int level, bool final_batch, StreamCarry& carry, uint8_t* out,
                     uint64_t out_cap, hipStream_t st);
 
+// ---- decompression (decomp.hip) --------------------------------------
+struct DecodeStats {
+  uint64_t candidates = 0;  // block magics decoded (real blocks + chance matches)
+  uint64_t blocks = 0;
+  uint64_t out_bytes = 0;
+  float total_ms = 0;
+};
+// Decodes the .bz2 stream d_in[0, n) into d_out[0, out_cap).  Returns BZ_OK for a complete,
+// correct stream, else the code BZ2_bzBuffToBuffDecompress returns (bzlib.c:1361-1410);
+// *out_len = bytes written.
+int decode_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t out_cap,
+                 uint64_t* out_len, DecodeStats* stats, hipStream_t st);
+
 }  // namespace bzg

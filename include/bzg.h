@@ -109,6 +109,25 @@ int bzg_seg_walk(uint32_t fill_in, int final_region, uint64_t *cuts, uint32_t ma
  * scan reports them.  *count = the number found; BZ_OUTBUFF_FULL when it exceeds cap (out holds
  * the first cap).  Replaces the bit-serial scan of bzip2recover.c:360-395. */
 int bzg_find_magics(const void *d_in, uint64_t n, uint64_t *out, uint64_t cap, uint64_t *count, void *stream);
+/* GPU decompression: decode the .bz2 stream d_in[0, n) (device memory)
+ * into d_out[0, out_cap) (device memory); *out_len = bytes written.  Blocks are found by the
+ * magic scan and decoded in parallel (Huffman + inverse MTF, inverse BWT, un-RLE1, CRCs).
+ * Returns BZ_OK for a complete stream with correct CRCs, else the code the reference's
+ * BZ2_bzBuffToBuffDecompress returns for the same input (bzlib.c:1361-1410): BZ_DATA_ERROR,
+ * BZ_DATA_ERROR_MAGIC, BZ_UNEXPECTED_EOF, BZ_OUTBUFF_FULL; BZ_MEM_ERROR / BZ_CONFIG_ERROR for
+ * device failures.  Replaces: BZ2_bzDecompress's decode loop (decompress.c:232-…,
+ * huffman.c:180-236, bzlib.c:531-677) for a whole in-memory stream. */
+int bzg_decompress_device(const void *d_in, uint64_t n, void *d_out, uint64_t out_cap, uint64_t *out_len,
+                          void *stream);
+/* The same with host buffers (one H2D and one D2H copy); used by BZ2_bzBuffToBuffDecompress. */
+int bzg_decompress_host(const void *src, uint64_t n, void *dst, uint64_t dst_cap, uint64_t *dst_len);
+typedef struct {
+  float total_ms;       /* device time of the last decompression */
+  uint64_t blocks;      /* blocks decoded */
+  uint64_t candidates;  /* block magics decoded speculatively (blocks + chance matches) */
+  uint64_t out_bytes;
+} bzg_decode_stats;
+void bzg_last_decode_stats(bzg_decode_stats *out);
 void bzg_last_stats(bzg_stats *out);
 
 /* Release the engine's device memory (it is re-acquired on the next call). */

@@ -123,6 +123,17 @@ def ref_compress(data: bytes, level: int) -> bytes:
     return dst.raw[: dl.value]
 
 
+def ref_decompress(data: bytes, cap: int, small: int = 0):
+    """The reference's BZ2_bzBuffToBuffDecompress: (return code, output bytes)."""
+    L = ref()
+    dst = ctypes.create_string_buffer(max(cap, 1))
+    dl = ctypes.c_uint(cap)
+    L.BZ2_bzBuffToBuffDecompress.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint), ctypes.c_void_p,
+                                             ctypes.c_uint, ctypes.c_int, ctypes.c_int]
+    rc = L.BZ2_bzBuffToBuffDecompress(dst, ctypes.byref(dl), data, len(data), small, 0)
+    return rc, dst.raw[: dl.value] if rc == 0 else b""
+
+
 class _Strm(ctypes.Structure):
     _fields_ = [
         ("next_in", ctypes.c_void_p), ("avail_in", ctypes.c_uint),
