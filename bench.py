@@ -193,7 +193,7 @@ def main():
         if not a.no_cpu:
             result.update(cpu_and_parity(data, a, d_in))
         if not a.no_extra and mode == "independent":
-            result["secondary"] = extra_configs(a, d_in, d_out, cap, no_cpu=a.no_cpu)
+            result["secondary"] = extra_configs(a, d_in, d_out, cap, no_cpu=a.no_cpu, nb_text=out_bytes)
         print(json.dumps(result), flush=True)
     if dist:
         torch.distributed.barrier()
@@ -293,11 +293,54 @@ def add_repeats(d, frac: float, seed: int = 0x5EED0009) -> None:
         covered += ln
 
 
-def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False):
-    """Secondary lines (never `value`): BASELINE configs 4 and 5 at full size (4 GiB, device
-    resident; bzg_compress_device cuts them into 1.5e9-byte batches), and enwik-like text with
-    long duplicated passages (the sorter's deep-group path)."""
+def decode_line(a, d_text, d_stream, nb, no_cpu):
+    """GPU decompression of the main workload's stream, device resident:
+    output-side MB/s, the output compared with the input, the reference decoder timed on a
+    bounded sample in a pinned child.  Decode bytes model: read c + 18 rho + write 1 per output
+    byte (L written 1, read twice 2, Q written 4 and read by two walks 8, Y written 1 and read
+    twice 2)."""
+    n = d_text.numel()
+    d_dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    sp = torch.cuda.current_stream().cuda_stream
+    rc, got = B.decompress_device(d_stream.data_ptr(), nb, d_dec.data_ptr(), n + 64, stream_ptr=sp)
+    torch.cuda.synchronize()
+    ok = rc == 0 and got == n and bool(torch.equal(d_dec[:n], d_text))
+    steps = 3
+    t = time.perf_counter()
+    for _ in range(steps):
+        B.decompress_device(d_stream.data_ptr(), nb, d_dec.data_ptr(), n + 64, stream_ptr=sp)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) * 1e3 / steps
+    st = B.last_decode_stats()
+    c = nb / n
+    b_alg = c + 18.0 + 1.0
+    line = {"workload": f"decompression of the main workload's -{a.level} stream ({nb} B -> {n} B), device resident",
+            "bytes_out": n, "value": round(n / ms / 1e3, 2), "unit": "MB/s (output side)", "ms_per_step": round(ms, 3),
+            "blocks": st["blocks"], "candidates": st["candidates"], "output_equals_input": ok,
+            "roofline": {"bound": "hbm", "b_alg_per_byte": round(b_alg, 3),
+                         "achieved": round(n * b_alg / (ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(n * b_alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 5)}}
+    del d_dec
+    from tests import oracles as O
+
+    if not no_cpu and O.has_ref():
+        m = 100_000_000
+        sample = O.ref_compress(d_text[:m].cpu().numpy().tobytes(), a.level)
+        secs, _ = run_cpu_child(sample, a.level, sorted(os.sched_getaffinity(0))[:1], op="d", cap=m)
+        line["cpu_baseline"] = {"value": round(m / secs / 1e6, 3), "unit": "MB/s (output side)", "cores": 1,
+                                "kind": "reference",
+                                "sample": f"BZ2_bzBuffToBuffDecompress of the -{a.level} stream of the first {m} B, "
+                                          f"pinned child"}
+    return line
+
+
+def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False, nb_text=0):
+    """Secondary lines (never `value`): GPU decompression of the main stream, BASELINE configs 4
+    and 5 at full size (4 GiB, device resident; bzg_compress_device cuts them into 1.5e9-byte
+    batches), and enwik-like text with long duplicated passages (the sorter's deep-group path)."""
     res = {}
+    if nb_text:
+        res["decompress_text"] = decode_line(a, d_text, d_out_text, nb_text, no_cpu)
     n4 = 1 << 32
     level = 9
     d = torch.full((n4,), 0x61, dtype=torch.uint8, device="cuda")
@@ -384,7 +427,7 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_child(path: str, level: int, cpus: str) -> None:
+def cpu_child(path: str, level: int, cpus: str, op: str = "c", cap: int = 0) -> None:
     """`bench.py --cpu-child`: the reference CPU path (oracle/_ref, the reference's own
     blocksort.c/compress.c build) timed in a child process pinned to `cpus` (no GPU touched).
     One cpu: one BZ2_bzBuffToBuffCompress of the whole sample, output kept beside it for the
@@ -398,7 +441,12 @@ def cpu_child(path: str, level: int, cpus: str) -> None:
     os.sched_setaffinity(0, cs)
     data = open(path, "rb").read()
     nt = len(cs)
-    if nt == 1:
+    if op == "d":  # the reference decoder on one .bz2 stream
+        t = time.perf_counter()
+        rc, out = O.ref_decompress(data, cap)
+        dt = time.perf_counter() - t
+        assert rc == 0 and len(out) == cap, rc
+    elif nt == 1:
         t = time.perf_counter()
         out = O.ref_compress(data, level)
         dt = time.perf_counter() - t
@@ -413,7 +461,7 @@ def cpu_child(path: str, level: int, cpus: str) -> None:
     print(json.dumps({"seconds": dt, "bytes": len(data), "threads": nt}), flush=True)
 
 
-def run_cpu_child(sample: bytes, level: int, cpus) -> tuple:
+def run_cpu_child(sample: bytes, level: int, cpus, op: str = "c", cap: int = 0) -> tuple:
     """Times the reference on `sample` in a pinned child (taskset when present); returns
     (seconds, reference output or None)."""
     import shutil
@@ -424,7 +472,7 @@ def run_cpu_child(sample: bytes, level: int, cpus) -> tuple:
         path = os.path.join(td, "sample.bin")
         open(path, "wb").write(sample)
         cl = ",".join(str(c) for c in cpus)
-        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", path, str(level), cl]
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child", path, str(level), cl, op, str(cap)]
         if shutil.which("taskset"):
             cmd = ["taskset", "-c", cl] + cmd
         r = subprocess.run(cmd, capture_output=True, text=True, check=True, timeout=600)
@@ -476,7 +524,7 @@ def cpu_and_parity(data, a, d_in):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) == 5 and sys.argv[1] == "--cpu-child":
-        cpu_child(sys.argv[2], int(sys.argv[3]), sys.argv[4])
+    if len(sys.argv) == 7 and sys.argv[1] == "--cpu-child":
+        cpu_child(sys.argv[2], int(sys.argv[3]), sys.argv[4], sys.argv[5], int(sys.argv[6]))
     else:
         main()

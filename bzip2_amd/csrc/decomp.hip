@@ -128,7 +128,10 @@ __device__ __forceinline__ uint32_t mtf_take(uint32_t& word, uint32_t r) {
 __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in, uint64_t nbytes,
                                                  const uint64_t* __restrict__ cbit, uint32_t nc, uint32_t nbmax,
                                                  uint8_t* __restrict__ lbuf, uint8_t* __restrict__ selbuf,
-                                                 DecRes* __restrict__ res) {
+                                                 DecRes* __restrict__ res, uint64_t* __restrict__ dbg) {
+  const uint64_t t_start = clock64();
+  uint64_t t_sym = 0;
+  uint32_t nsym = 0;
   __shared__ uint16_t lut[kNGroups][1 << kLutBits];  // (sym << 4) | len for codes <= 9 bits, 0 = longer
   __shared__ uint16_t perm[kNGroups][kMaxAlpha];     // symbols in canonical order
   __shared__ int32_t limit[kNGroups][kMaxDecLen + 1];
@@ -265,7 +268,9 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
     uint32_t sreg = 0, gi = 0, gleft = 0, t = 0;
     uint32_t run = 0, rdig = 0;
     bool inrun = false;
+    t_sym = clock64();
     for (;;) {
+      nsym++;
       if (gleft == 0) {
         if (gi >= nsel) { status = BZ_DATA_ERROR; goto done; }
         if ((gi & 63) == 0) sreg = gi + lane < nsel ? ssrc[gi + lane] : 0u;
@@ -331,6 +336,13 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
     if (origptr >= nblk) status = BZ_DATA_ERROR;
   }
 done:
+  if (dbg && lane == 0) {
+    const uint64_t t_end = clock64();
+    dbg[4 * c] = t_sym ? t_sym - t_start : 0;
+    dbg[4 * c + 1] = t_sym ? t_end - t_sym : 0;
+    dbg[4 * c + 2] = nsym;
+    dbg[4 * c + 3] = p - cbit[c];
+  }
   if (lane == 0) {
     DecRes r;
     r.status = status;
@@ -769,8 +781,24 @@ int decode_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, uint8_t* d_out,
     uint8_t* selbuf = ws.u8("dec_sel", (size_t)nc * kSelCap + 64);
     DecRes* d_res = ws.typed<DecRes>("dec_res", nc);
     HIP_OK(hipMemcpyAsync(d_cbit, cand.data(), 8 * nc, hipMemcpyHostToDevice, st));
-    k_dec_huff<<<nc, 64, 0, st>>>(d_in, n, d_cbit, nc, nbmax, lbuf, selbuf, d_res);
+    static const bool dbg_on = getenv("BZG_DEC_DEBUG") != nullptr;
+    uint64_t* d_dbg = dbg_on ? ws.typed<uint64_t>("dec_dbg", 4 * (size_t)nc) : nullptr;
+    k_dec_huff<<<nc, 64, 0, st>>>(d_in, n, d_cbit, nc, nbmax, lbuf, selbuf, d_res, d_dbg);
     HIP_OK(hipGetLastError());
+    if (dbg_on) {
+      std::vector<uint64_t> h(4 * (size_t)nc);
+      HIP_OK(hipMemcpyAsync(h.data(), d_dbg, 8 * h.size(), hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      double hc = 0, sc = 0, ns = 0, nbit = 0;
+      for (uint32_t k = 0; k < nc; k++) {
+        hc += (double)h[4 * k];
+        sc += (double)h[4 * k + 1];
+        ns += (double)h[4 * k + 2];
+        nbit += (double)h[4 * k + 3];
+      }
+      fprintf(stderr, "[bzg decode] %u candidates: header %.0f clk, symbols %.0f clk / %.0f sym = %.1f clk/sym, %.0f bits\n",
+              nc, hc / nc, sc / nc, ns / nc, sc / std::max(ns, 1.0), nbit / nc);
+    }
     std::vector<DecRes> hres(nc);
     HIP_OK(hipMemcpyAsync(hres.data(), d_res, sizeof(DecRes) * nc, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
