@@ -48,6 +48,12 @@ constexpr uint32_t kSG = BZG_SG;      // S1 groups up to this size are packed in
 constexpr int kNCls = 8;
 constexpr uint32_t kClsMax[7] = {8, 16, 32, 64, 128, 256, kSG};
 constexpr uint32_t kClsDeep = 8;
+// S2 workgroups walk the (block-ordered) group lists XCD by XCD: each XCD's L2 then holds the
+// text and slots of its own few blocks instead of every block's
+#ifndef BZG_S2_XCD
+#define BZG_S2_XCD 1
+#endif
+__device__ __forceinline__ uint32_t s2_wg() { return BZG_S2_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; }
 
 __host__ __device__ __forceinline__ uint32_t size_cls(uint32_t n) {
   return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= 256 ? 5u : n <= kSG ? 6u : 7u;
@@ -1022,7 +1028,7 @@ __device__ __forceinline__ void text_key8(const uint8_t* t, uint32_t len, uint32
 // (same class, named by its first lane) and adds the smaller ones to its position.
 __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint32_t n_tiny, SortBufs B, SortOut O) {
   const uint32_t lane = __lane_id();
-  const uint32_t wv = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+  const uint32_t wv = s2_wg() * (kT / 64) + (threadIdx.x >> 6);
   const uint32_t bi = wv * 8 + lane / 8, el = lane % 8;
   bool act = false;
   uint32_t s0 = 0, d = 0, v = 0, unit = 0;
@@ -1332,7 +1338,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
   __shared__ uint32_t TC[kT / 64][kTE];
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   const uint32_t sl = lane % kSeg;
-  const uint32_t bi = (blockIdx.x * (kT / 64) + w) * kBPW + lane / kSeg;
+  const uint32_t bi = (s2_wg() * (kT / 64) + w) * kBPW + lane / kSeg;
   const bool has = bi < nL;
   if (__ballot(has) == 0) return;
   Grp g{0, 0, 0, 0};

@@ -5,7 +5,7 @@ set -e
 N=$1; F=$2; shift 2
 cd /root/repo/bzip2_amd
 mkdir -p ../variants build_var/$N
-for o in scan rle1 sort sortdbl mtf code magic engine tieorder bzlib_api bzfile decode; do cp -f build/$o.o build_var/$N/; done
+for o in scan rle1 sort sortdbl mtf code magic engine tieorder bzlib_api bzfile decode decomp; do cp -f build/$o.o build_var/$N/; done
 for s in ${@:-sort}; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 $F -c csrc/$s.hip -o build_var/$N/$s.o
 done
