@@ -45,22 +45,27 @@
 namespace bzg {
 namespace {
 
-constexpr int kLutBits = 9;
+constexpr int kLutBits = 10;
 constexpr int kMaxDecLen = 20;          // BZ_MAX_DECODE_LEN (bzlib_private.h:141)
 constexpr uint32_t kSelCap = 18002;     // BZ_MAX_SELECTORS: more is a data error (decompress.c:380)
 constexpr uint32_t kSplit = 256;        // ruling-set spacing of the inverse-BWT walk
 constexpr uint32_t kMaxSplit = 900000 / kSplit + 2;
 constexpr uint32_t kRleChunks = 256;    // un-RLE1 chunks (threads) per block
-constexpr uint32_t kBatch = 1024;       // block candidates decoded per pass
+constexpr uint32_t kBatch = 4096;       // block candidates decoded per pass
+
+constexpr uint32_t kMtfChunk = 1024;    // symbols per inverse-MTF chunk
+constexpr int kStatusCap = -100;        // more symbols than a block can hold (a data error)
 
 struct DecRes {
-  int32_t status;   // 0, BZ_DATA_ERROR or BZ_UNEXPECTED_EOF
-  uint32_t nblock;  // bytes of L
+  int32_t status;   // phase 1: 0 (EOB reached), BZ_DATA_ERROR, BZ_UNEXPECTED_EOF or kStatusCap
+  uint32_t nsym;    // symbols before EOB (or before the failure)
   uint64_t end_bit; // first bit after the block
   uint32_t origptr;
   uint32_t crc;     // stored block CRC
   uint32_t rand;    // randomised-block bit
-  uint32_t pad;
+  uint32_t ninuse;
+  uint32_t nblock;  // phase 2: bytes of L
+  uint32_t err2;    // phase 2: index of the first symbol the reference rejects (~0: none)
 };
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
@@ -75,6 +80,13 @@ __device__ __forceinline__ uint32_t stream_word(const uint8_t* __restrict__ in, 
   uint32_t v = 0;
   for (int k = 0; k < 4; k++) v = (v << 8) | (b + k < nbytes ? (uint32_t)in[b + k] : 0u);
   return v;
+}
+
+// The same word as stored (little-endian load of the big-endian stream word; bswap32 at use).
+__device__ __forceinline__ uint32_t stream_word_raw(const uint8_t* __restrict__ in, uint64_t nbytes, uint64_t w) {
+  const uint64_t b = 4 * w;
+  if (b + 4 <= nbytes && ((reinterpret_cast<uintptr_t>(in) & 3) == 0)) return reinterpret_cast<const uint32_t*>(in)[w];
+  return bswap32(stream_word(in, nbytes, w));
 }
 
 // Wave-wide bit window: lane l holds word wbase + l in `cur` and wbase + 64 + l in `nxt`.
@@ -111,34 +123,26 @@ struct BitWindow {
   }
 };
 
-// Move-to-front of entry r (>= 1) of the list held 4 entries per lane (lane l: entries
-// 4l..4l+3, entry 4l+k in byte k).  Returns the entry.
-__device__ __forceinline__ uint32_t mtf_take(uint32_t& word, uint32_t r) {
-  const uint32_t v = (rdlane(word, r >> 2) >> (8 * (r & 3))) & 0xffu;
-  const int lane = __lane_id();
-  uint32_t carry = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(word >> 24), 0x138, 0xf, 0xf, false);  // wave_shr:1
-  if (lane == 0) carry = v;
-  const uint32_t up = (word << 8) | carry;
-  const int d = (int)r - 4 * lane;  // bytes 0..d of this lane take their predecessor
-  const uint32_t m = d >= 3 ? 0xffffffffu : (d < 0 ? 0u : ((1u << (8 * (d + 1))) - 1u));
-  word = (up & m) | (word & ~m);
-  return v;
-}
-
+// Phase 1, one wave per candidate: header, selectors, code lengths, decode tables, then the
+// Huffman symbols of the block (RUNA 0, RUNB 1, MTF value + 1 for 2..nInUse; EOB not stored),
+// 64 per vector store.  The symbol loop keeps its whole state in scalar registers: a 64-bit
+// bit buffer refilled from the lane-held window, one LDS lookup (10-bit table) per symbol.
 __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in, uint64_t nbytes,
                                                  const uint64_t* __restrict__ cbit, uint32_t nc, uint32_t nbmax,
-                                                 uint8_t* __restrict__ lbuf, uint8_t* __restrict__ selbuf,
+                                                 uint32_t symstride, uint16_t* __restrict__ symbuf,
+                                                 uint8_t* __restrict__ seqbuf, uint8_t* __restrict__ selbuf,
                                                  DecRes* __restrict__ res, uint64_t* __restrict__ dbg) {
   const uint64_t t_start = clock64();
   uint64_t t_sym = 0;
-  uint32_t nsym = 0;
-  __shared__ uint16_t lut[kNGroups][1 << kLutBits];  // (sym << 4) | len for codes <= 9 bits, 0 = longer
-  __shared__ uint16_t perm[kNGroups][kMaxAlpha];     // symbols in canonical order
+  // per 10-bit window: total | n << 5 | sym0 << 7 | sym1 << 16 | len0 << 25 -- n = 1 or 2 symbols
+  // decoded from the window (a second one only if both fit and the first is not EOB), n = 0:
+  // the first code is longer than the window
+  __shared__ uint32_t lut[kNGroups * (1u << kLutBits)];
+  __shared__ uint16_t perm[kNGroups][kMaxAlpha];         // symbols in canonical order
   __shared__ int32_t limit[kNGroups][kMaxDecLen + 1];
   __shared__ int32_t cbase[kNGroups][kMaxDecLen + 1];
   __shared__ uint8_t lens[kNGroups][kMaxAlpha];
   __shared__ uint32_t cnt[kMaxDecLen + 1];
-  __shared__ uint32_t stage[64];                     // 256 output bytes
   __shared__ uint8_t seq[256];
   const uint32_t c = blockIdx.x;
   if (c >= nc) return;
@@ -146,9 +150,7 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
   const uint64_t nbits = 8 * nbytes;
   uint64_t p = cbit[c];
   int status = 0;
-  uint32_t nblk = 0, origptr = 0, bcrc = 0, rnd = 0;
-  uint8_t* out = lbuf + (size_t)c * nbmax;
-  uint8_t* stage8 = reinterpret_cast<uint8_t*>(stage);
+  uint32_t origptr = 0, bcrc = 0, rnd = 0, ns = 0;
   BitWindow W;
   W.init(in, nbytes, p);
   uint32_t ninuse = 0, g = 0, nsel = 0, alpha = 0;
@@ -248,111 +250,309 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
     }
     __syncthreads();
     for (uint32_t x = lane; x < (1u << kLutBits); x += 64) {
-      uint16_t e = 0;
+      uint32_t e = 0;
       for (int l = 1; l <= kLutBits; l++) {
         const int32_t v = (int32_t)(x >> (kLutBits - l));
         if (v <= limit[t][l]) {
-          e = (uint16_t)((perm[t][cbase[t][l] + v] << 4) | l);
+          const uint32_t s0 = perm[t][cbase[t][l] + v];
+          e = (uint32_t)l | (1u << 5) | (s0 << 7) | ((uint32_t)l << 25);
+          if (s0 != ninuse + 1) {  // a second code inside the window
+            const uint32_t x2 = (x << l) & ((1u << kLutBits) - 1);
+            for (int l1 = 1; l1 <= kLutBits - l; l1++) {
+              const int32_t v1 = (int32_t)(x2 >> (kLutBits - l1));
+              if (v1 <= limit[t][l1]) {
+                const uint32_t s1 = perm[t][cbase[t][l1] + v1];
+                e = (uint32_t)(l + l1) | (2u << 5) | (s0 << 7) | (s1 << 16) | ((uint32_t)l << 25);
+                break;
+              }
+            }
+          }
           break;
         }
       }
-      lut[t][x] = e;
+      lut[t * (1u << kLutBits) + x] = e;
     }
     __syncthreads();
   }
-  // ---- symbols (decompress.c:444-664): Huffman, RUNA/RUNB, inverse MTF, block fill limits
+  // ---- symbols (decompress.c:444-664, the Huffman half; MTF and runs are phase 2)
   {
-    uint32_t word = reinterpret_cast<const uint32_t*>(seq)[lane];  // MTF list: in-use bytes ascending
     const uint32_t eob = ninuse + 1;
     const uint8_t* ssrc = selbuf + (size_t)c * kSelCap;
-    uint32_t sreg = 0, gi = 0, gleft = 0, t = 0;
-    uint32_t run = 0, rdig = 0;
-    bool inrun = false;
+    uint16_t* sdst = symbuf + (size_t)c * symstride;
+    uint32_t sreg = 0, gi = 0, gleft = 0, lbase = 0, symv = 0;
+    uint64_t wword = p >> 5;  // stream word held by lane 0 of cur
+    // raw (byte-swapped at use) so that the prefetch of nxt is not waited for until needed
+    uint32_t cur = stream_word_raw(in, nbytes, wword + lane);
+    uint32_t nxt = stream_word_raw(in, nbytes, wword + 64 + lane);
+    uint64_t bb = (uint64_t)bswap32(rdlane(cur, 0)) << (32 + (p & 31));  // MSB-aligned bit buffer
+    uint32_t nb = 32 - (uint32_t)(p & 31), wi = 1;
     t_sym = clock64();
+    // every symbol (EOB and run digits included) takes the next slot of its 50-symbol group;
+    // a symbol past the last selector's group is a data error (decompress.c GET_MTF_VAL)
+    const uint64_t p0 = p;
+    const uint32_t left0 = (uint32_t)min<uint64_t>(nbits - p, 0x7fffffffull);
+    uint32_t left = left0;  // bits of the stream after the current position
+    auto emit = [&](uint32_t sym) {
+      symv = lane == (ns & 63) ? sym : symv;
+      ns++;
+      if ((ns & 63) == 0) sdst[ns - 64 + lane] = (uint16_t)symv;
+    };
     for (;;) {
-      nsym++;
       if (gleft == 0) {
-        if (gi >= nsel) { status = BZ_DATA_ERROR; goto done; }
+        if (gi == nsel) { status = BZ_DATA_ERROR; break; }
         if ((gi & 63) == 0) sreg = gi + lane < nsel ? ssrc[gi + lane] : 0u;
-        t = rdlane(sreg, gi & 63);
+        lbase = uni(rdlane(sreg, gi & 63) << kLutBits);
         gi++;
         gleft = kGroupSize;
       }
-      gleft--;
-      const uint32_t v32 = W.peek32(p);
-      uint32_t e = uni(lut[t][v32 >> (32 - kLutBits)]);
-      uint32_t len, sym;
-      if (e) {
-        len = e & 15u;
-        sym = e >> 4;
-      } else {
+      if (nb < 32) {
+        bb |= (uint64_t)bswap32(rdlane(cur, wi)) << (32 - nb);
+        nb += 32;
+        if (++wi == 64) {
+          cur = nxt;
+          wword += 64;
+          nxt = stream_word_raw(in, nbytes, wword + 64 + lane);
+          wi = 0;
+        }
+      }
+      const uint32_t e = uni(lut[lbase + (uint32_t)(bb >> (64 - kLutBits))]);
+      uint32_t len, s0, s1 = 0;
+      bool two = false;
+      if ((e & 0x60u) == 0) {  // a code longer than the window: canonical limits per length
+                               // (the prefix passes limit[l] below the code's length only)
+        const uint32_t t = lbase >> kLutBits;
         len = kLutBits + 1;
-        for (;; len++) {
-          const int32_t v = (int32_t)(v32 >> (32 - len));
-          if (v <= limit[t][len]) break;
-        }
-        sym = uni(perm[t][cbase[t][len] + (int32_t)(v32 >> (32 - len))]);
+#pragma unroll
+        for (int l = kLutBits + 1; l < kMaxDecLen; l++) len += (int32_t)(bb >> (64 - l)) > (int32_t)uni(limit[t][l]) ? 1u : 0u;
+        s0 = uni(perm[t][cbase[t][len] + (int32_t)(bb >> (64 - len))]);
+      } else {
+        s0 = (e >> 7) & 511u;
+        s1 = (e >> 16) & 511u;
+        two = (e & 0x60u) == 0x40u && gleft >= 2 && (e & 31u) <= left;  // both in this group
+        len = two ? (e & 31u) : (e >> 25);
       }
-      if (p + len > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
-      p += len;
-      if (sym <= 1) {  // RUNA / RUNB: bijective base-2 digits of a run of the front byte
-        if (inrun && run > (1u << 20)) { status = BZ_DATA_ERROR; goto done; }
-        run += (sym + 1) << rdig;
-        rdig++;
-        inrun = true;
-        continue;
+      if (len > left) { status = BZ_UNEXPECTED_EOF; break; }
+      left -= len;
+      bb <<= len;
+      nb -= len;
+      gleft = uni(gleft - (two ? 2u : 1u));
+      if (s0 == eob) break;
+      emit(s0);
+      if (two) {
+        if (s1 == eob) break;
+        emit(s1);
       }
-      if (inrun) {
-        if (nblk + run > nbmax) { status = BZ_DATA_ERROR; goto done; }
-        const uint32_t u = rdlane(word, 0) & 0xffu;
-        while (run) {
-          const uint32_t fill = nblk & 255u, take = min(run, 256u - fill);
-          for (uint32_t i = lane; i < take; i += 64) stage8[fill + i] = (uint8_t)u;
-          nblk += take;
-          run -= take;
-          if ((nblk & 255u) == 0) {
-            __syncthreads();
-            reinterpret_cast<uint32_t*>(out + nblk - 256)[lane] = stage[lane];
-            __syncthreads();
-          }
-        }
-        rdig = 0;
-        inrun = false;
-      }
-      if (sym == eob) break;
-      if (nblk == nbmax) { status = BZ_DATA_ERROR; goto done; }
-      const uint32_t v = mtf_take(word, sym - 1);
-      if (lane == 0) stage8[nblk & 255u] = (uint8_t)v;
-      nblk++;
-      if ((nblk & 255u) == 0) {
-        __syncthreads();
-        reinterpret_cast<uint32_t*>(out + nblk - 256)[lane] = stage[lane];
-        __syncthreads();
-      }
+      if ((ns & ~63u) > nbmax) { status = kStatusCap; break; }
     }
-    __syncthreads();
-    const uint32_t rem = nblk & 255u;
-    for (uint32_t i = lane; i < rem; i += 64) out[(nblk & ~255u) + i] = stage8[i];
-    if (origptr >= nblk) status = BZ_DATA_ERROR;
+    p = p0 + (left0 - left);
+    if (lane < (ns & 63)) sdst[(ns & ~63u) + lane] = (uint16_t)symv;
   }
 done:
+  if (lane < 64) reinterpret_cast<uint32_t*>(seqbuf + (size_t)c * 256)[lane] = reinterpret_cast<const uint32_t*>(seq)[lane];
   if (dbg && lane == 0) {
     const uint64_t t_end = clock64();
     dbg[4 * c] = t_sym ? t_sym - t_start : 0;
     dbg[4 * c + 1] = t_sym ? t_end - t_sym : 0;
-    dbg[4 * c + 2] = nsym;
+    dbg[4 * c + 2] = ns;
     dbg[4 * c + 3] = p - cbit[c];
   }
   if (lane == 0) {
     DecRes r;
     r.status = status;
-    r.nblock = nblk;
+    r.nsym = ns;
     r.end_bit = p;
     r.origptr = origptr;
     r.crc = bcrc;
     r.rand = rnd;
-    r.pad = 0;
+    r.ninuse = ninuse;
+    r.nblock = 0;
+    r.err2 = ~0u;
     res[c] = r;
+  }
+}
+
+// Phase 2a, one lane per chunk of kMtfChunk symbols: inverse MTF from a symbolic initial list
+// (position k holds token k, "entry k of the chunk's real initial list").  Writes a token per
+// symbol (a run digit gets the front token) and the chunk's final list of tokens.  The list
+// is 64 words per lane in LDS ([word][lane]: conflict-free); word 0 stays in a register.
+__global__ void __launch_bounds__(64) k_dec_mtf_sym(const uint16_t* __restrict__ symbuf, uint32_t symstride,
+                                                    const uint32_t* __restrict__ chunk_cand,
+                                                    const uint32_t* __restrict__ chunk_j, uint32_t nchunks,
+                                                    const DecRes* __restrict__ res, uint8_t* __restrict__ tokbuf,
+                                                    uint32_t* __restrict__ permbuf) {
+  __shared__ uint32_t Lw[64][64];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t q = blockIdx.x * 64 + lane;
+  if (q >= nchunks) return;
+  const uint32_t c = chunk_cand[q];
+  const uint32_t lo = chunk_j[q] * kMtfChunk, hi = min(res[c].nsym, lo + kMtfChunk);
+  for (uint32_t w = 1; w < 64; w++) Lw[w][lane] = (4 * w) | ((4 * w + 1) << 8) | ((4 * w + 2) << 16) | ((4 * w + 3) << 24);
+  uint32_t w0 = 0x03020100u;
+  const uint16_t* S = symbuf + (size_t)c * symstride;
+  uint8_t* T = tokbuf + (size_t)c * symstride;
+  for (uint32_t i = lo; i < hi; i += 4) {
+    const uint2 q4 = *reinterpret_cast<const uint2*>(S + i);
+    const uint32_t sv[4] = {q4.x & 0xffffu, q4.x >> 16, q4.y & 0xffffu, q4.y >> 16};
+    uint32_t tok4 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (i + k >= hi) break;
+      const uint32_t s = sv[k];
+      uint32_t v;
+      if (s <= 1) {
+        v = w0 & 0xffu;
+      } else {
+        const uint32_t r = s - 1;
+        if (r < 4) {
+          v = (w0 >> (8 * r)) & 0xffu;
+          const uint32_t m = r == 3 ? 0xffffffffu : ((1u << (8 * (r + 1))) - 1u);
+          w0 = (((w0 << 8) | v) & m) | (w0 & ~m);
+        } else {
+          const uint32_t wr = r >> 2, br = r & 3u;
+          const uint32_t x = Lw[wr][lane];
+          v = (x >> (8 * br)) & 0xffu;
+          uint32_t carry = w0 >> 24;
+          w0 = (w0 << 8) | v;
+          for (uint32_t k2 = 1; k2 < wr; k2++) {
+            const uint32_t y = Lw[k2][lane];
+            Lw[k2][lane] = (y << 8) | carry;
+            carry = y >> 24;
+          }
+          const uint32_t m = br == 3 ? 0xffffffffu : ((1u << (8 * (br + 1))) - 1u);
+          Lw[wr][lane] = (((x << 8) | carry) & m) | (x & ~m);
+        }
+      }
+      tok4 |= v << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(T + i) = tok4;
+  }
+  uint32_t* P = permbuf + (size_t)q * 64;
+  P[0] = w0;
+  for (uint32_t w = 1; w < 64; w++) P[w] = Lw[w][lane];
+}
+
+// Phase 2b, a workgroup per block: the real initial list of every chunk,
+// init[j + 1][k] = init[j][perm_j[k]], from the block's in-use bytes ascending.
+__global__ void __launch_bounds__(256) k_dec_mtf_chain(const uint32_t* __restrict__ slot,
+                                                       const uint32_t* __restrict__ chunk_first,
+                                                       const DecRes* __restrict__ res, const uint8_t* __restrict__ seqbuf,
+                                                       const uint32_t* __restrict__ permbuf, uint8_t* __restrict__ initbuf) {
+  __shared__ uint8_t sh[256];
+  const uint32_t b = blockIdx.x, c = slot[b], k = threadIdx.x;
+  const uint32_t q0 = chunk_first[b], nch = chunk_first[b + 1] - q0;
+  uint32_t cur = seqbuf[(size_t)c * 256 + k];
+  const uint8_t* P = reinterpret_cast<const uint8_t*>(permbuf);
+  for (uint32_t j = 0; j < nch; j++) {
+    initbuf[(size_t)(q0 + j) * 256 + k] = (uint8_t)cur;
+    sh[k] = (uint8_t)cur;
+    __syncthreads();
+    const uint32_t pk = P[(size_t)(q0 + j) * 256 + k];
+    cur = sh[pk];
+    __syncthreads();
+  }
+}
+
+// Phase 2c, a workgroup per block: run lengths (RUNA/RUNB digits, bijective base 2), output
+// positions by a block-wide scan, the reference's limits (a run that passes 2^20 before its
+// next digit, more than nblockMAX bytes: decompress.c:486-500, 520-525) as the index of the
+// first failing symbol, and the BWT column L written as 4-byte words.
+__global__ void __launch_bounds__(1024) k_dec_expand(const uint32_t* __restrict__ slot,
+                                                     const uint32_t* __restrict__ chunk_first, uint32_t nbmax,
+                                                     uint32_t symstride, const uint16_t* __restrict__ symbuf,
+                                                     const uint8_t* __restrict__ tokbuf,
+                                                     const uint8_t* __restrict__ initbuf, DecRes* __restrict__ res,
+                                                     uint8_t* __restrict__ lbuf) {
+  __shared__ uint32_t spos[1024];   // output position of each symbol of the tile, relative to the tile
+  __shared__ uint8_t sbyte[1024];
+  __shared__ uint64_t sh64[16];
+  __shared__ int32_t shi[16];
+  __shared__ uint32_t err_sh;
+  __shared__ uint64_t carry_rsp_sh;
+  const uint32_t b = blockIdx.x, c = slot[b], tid = threadIdx.x;
+  const uint32_t ns = res[c].nsym;
+  const bool eob_reached = res[c].status == 0;
+  const uint16_t* S = symbuf + (size_t)c * symstride;
+  const uint8_t* T = tokbuf + (size_t)c * symstride;
+  const uint8_t* I = initbuf + (size_t)chunk_first[b] * 256;
+  uint8_t* L = lbuf + (size_t)c * nbmax;
+  if (tid == 0) {
+    err_sh = ~0u;
+    carry_rsp_sh = 0;
+  }
+  uint64_t carry_pos = 0;
+  int32_t carry_lnd = -1;
+  __syncthreads();
+  for (uint32_t base = 0; base < ns; base += 1024) {
+    const uint32_t i = base + tid;
+    const bool valid = i < ns;
+    const uint32_t s = valid ? S[i] : 2u;
+    const bool dig = valid && s <= 1;
+    // last non-digit index <= i (block_incl_max pads with 0: scan i + 1, 0 for digits)
+    int32_t lnd = (int32_t)block_incl_max(dig ? 0u : i + 1, reinterpret_cast<uint32_t*>(shi)) - 1;
+    lnd = max(lnd, carry_lnd);
+    const uint32_t k = dig ? (uint32_t)((int32_t)i - lnd - 1) : 0u;
+    const uint64_t cntv = valid ? (dig ? ((uint64_t)(s + 1) << min(k, 22u)) : 1ull) : 0ull;
+    uint64_t total;
+    const uint64_t incl = block_incl_sum(cntv, sh64, &total);
+    const uint64_t pos = carry_pos + incl - cntv;
+    spos[tid] = (uint32_t)min<uint64_t>(incl - cntv, 0xffffffffull);
+    uint8_t byte = 0;
+    if (valid) {
+      const uint32_t tok = T[i];
+      byte = I[(size_t)(i / kMtfChunk) * 256 + tok];
+    }
+    sbyte[tid] = byte;
+    const uint64_t crsp = carry_rsp_sh;
+    __syncthreads();
+    if (valid) {
+      if (dig) {
+        const int32_t rs = lnd + 1;  // the run's first digit
+        const uint64_t rsp = rs >= (int32_t)base ? carry_pos + spos[rs - (int32_t)base] : crsp;
+        if (k >= 1 && pos - rsp > (1ull << 20)) atomicMin(&err_sh, i);
+        if (tid == 1023 || i + 1 == ns) carry_rsp_sh = rsp;
+      } else if (pos >= nbmax) {
+        atomicMin(&err_sh, i);
+      }
+    }
+    // L bytes of this tile: [carry_pos, carry_pos + total) clipped to nbmax
+    const uint64_t t0 = carry_pos, t1 = min<uint64_t>(carry_pos + total, nbmax);
+    if (t1 > t0) {
+      const uint32_t nval = min(ns - base, 1024u);
+      for (uint64_t w = (t0 >> 2) + tid; 4 * w < t1; w += 1024) {
+        uint32_t word = 0, have = 0;
+        // symbol covering byte max(4w, t0): last j with spos[j] <= rel
+        const uint64_t a0 = max<uint64_t>(4 * w, t0);
+        uint32_t rel = (uint32_t)(a0 - t0);
+        uint32_t lo2 = 0, hi2 = nval;  // spos[lo2] <= rel < spos[hi2]
+        while (hi2 - lo2 > 1) {
+          const uint32_t mid = (lo2 + hi2) >> 1;
+          if (spos[mid] <= rel) lo2 = mid; else hi2 = mid;
+        }
+        for (uint64_t a = a0; a < 4 * w + 4 && a < t1; a++, rel++) {
+          while (lo2 + 1 < nval && spos[lo2 + 1] <= rel) lo2++;
+          word |= (uint32_t)sbyte[lo2] << (8 * (a & 3));
+          have |= 1u << (a & 3);
+        }
+        if (have == 0xfu) {
+          *reinterpret_cast<uint32_t*>(L + 4 * w) = word;
+        } else {
+          for (uint32_t x = 0; x < 4; x++)
+            if ((have >> x) & 1u) L[4 * w + x] = (uint8_t)(word >> (8 * x));
+        }
+      }
+    }
+    carry_pos += total;
+    __syncthreads();
+    if (tid == 1023) shi[0] = lnd;  // the scan's last entry: the tile's last non-digit
+    __syncthreads();
+    carry_lnd = shi[0];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    uint32_t e = err_sh;
+    if (eob_reached && carry_pos > nbmax) e = min(e, ns);
+    res[c].err2 = e;
+    res[c].nblock = (uint32_t)min<uint64_t>(carry_pos, 0xffffffffull);
   }
 }
 
@@ -517,6 +717,151 @@ __global__ void __launch_bounds__(1024) k_dec_walk(const uint32_t* __restrict__ 
     }
   }
   if (threadIdx.x == 0) cycle_out[b] = cyc;
+}
+
+// ---- stage 3, L2-local form: a block's walk is spread over many workgroups, and the
+// workgroups are dealt XCD by XCD in block order (wgmap), so an XCD works on a few blocks at a
+// time and their Q arrays (<= 3.6 MB each) stay in its L2 / the MALL instead of every block's
+// random 4-byte loads going to HBM.  Splitters every kSplit2 rows; the chain of segments is
+// ranked by pointer jumping in LDS (k_dec_walk_rank).
+constexpr uint32_t kSplit2 = 64;
+constexpr uint32_t kMaxSplit2 = 900000 / kSplit2 + 2;
+constexpr uint32_t kWalkT = 256;
+constexpr uint16_t kNil = 0xffffu;
+
+struct WalkBlock {
+  uint32_t n, o, ns, start;
+  __device__ WalkBlock(const DecRes& r) : n(r.nblock), o(r.origptr) {
+    ns = ceil_div(n, kSplit2) + 1;
+    start = ns - 1;
+  }
+  __device__ uint32_t slot_of(uint32_t s) const { return s == start ? o : s * kSplit2; }
+  __device__ bool is_split(uint32_t j) const { return j == o || (j % kSplit2) == 0; }
+  __device__ uint32_t id_of(uint32_t j) const { return j == o ? start : j / kSplit2; }
+  __device__ bool dead(uint32_t s) const { return s != start && s * kSplit2 == o; }  // start's own row
+};
+
+__global__ void __launch_bounds__(kWalkT) k_dec_walk_seg(const uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ slot,
+                                                         const DecRes* __restrict__ res, uint32_t nbmax,
+                                                         const uint32_t* __restrict__ wgmap, uint32_t* __restrict__ seg_nx,
+                                                         uint32_t* __restrict__ seg_len) {
+  const uint32_t m = wgmap[blockIdx.x];
+  if (m == ~0u) return;
+  const uint32_t b = m >> 8, s = (m & 255u) * kWalkT + threadIdx.x;
+  const WalkBlock W(res[slot[b]]);
+  if (s >= W.ns) return;
+  const uint32_t* Q = qbuf + (size_t)b * nbmax;
+  uint32_t j = W.slot_of(s), len = 0;
+  do {
+    j = Q[j] >> 8;
+    len++;
+  } while (!W.is_split(j));
+  seg_nx[(size_t)b * kMaxSplit2 + s] = W.id_of(j);
+  seg_len[(size_t)b * kMaxSplit2 + s] = len;
+}
+
+__global__ void __launch_bounds__(1024) k_dec_walk_rank(const uint32_t* __restrict__ slot, const DecRes* __restrict__ res,
+                                                        const uint32_t* __restrict__ seg_nx,
+                                                        const uint32_t* __restrict__ seg_len, uint32_t* __restrict__ seg_off,
+                                                        uint32_t* __restrict__ cycle_out) {
+  __shared__ uint16_t nx[kMaxSplit2];
+  __shared__ uint32_t sum[kMaxSplit2];
+  constexpr uint32_t kPer = (kMaxSplit2 + 1023) / 1024;
+  const uint32_t b = blockIdx.x;
+  const WalkBlock W(res[slot[b]]);
+  const uint32_t* gn = seg_nx + (size_t)b * kMaxSplit2;
+  const uint32_t* gl = seg_len + (size_t)b * kMaxSplit2;
+  // the segments of the start's cycle form a list ending at the one that leads back to start
+  for (uint32_t s = threadIdx.x; s < W.ns; s += 1024) {
+    const uint32_t x = gn[s];
+    nx[s] = (x == W.start || W.dead(s)) ? kNil : (uint16_t)x;
+    sum[s] = W.dead(s) ? 0u : gl[s];
+  }
+  __syncthreads();
+  // Wyllie list ranking: sum[s] becomes the length from s to the list end; nodes on other
+  // cycles never reach the end (their sums are not used)
+  for (int round = 0; round < 15; round++) {
+    uint32_t ns_[kPer], nn_[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+      const uint32_t s = threadIdx.x + 1024 * k;
+      ns_[k] = 0;
+      nn_[k] = kNil;
+      if (s < W.ns) {
+        const uint32_t a = nx[s];
+        ns_[k] = sum[s];
+        if (a != kNil) {
+          ns_[k] += sum[a];
+          nn_[k] = nx[a];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+      const uint32_t s = threadIdx.x + 1024 * k;
+      if (s < W.ns) {
+        sum[s] = ns_[k];
+        nx[s] = (uint16_t)nn_[k];
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t total = sum[W.start];  // the start's cycle length (<= n)
+  for (uint32_t s = threadIdx.x; s < W.ns; s += 1024)
+    seg_off[(size_t)b * kMaxSplit2 + s] = (nx[s] == kNil && !W.dead(s)) ? total - sum[s] : ~0u;
+  if (threadIdx.x == 0) cycle_out[b] = min(total, W.n);
+}
+
+__global__ void __launch_bounds__(kWalkT) k_dec_walk_emit(const uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ slot,
+                                                          const DecRes* __restrict__ res, uint32_t nbmax,
+                                                          const uint32_t* __restrict__ wgmap,
+                                                          const uint32_t* __restrict__ seg_len,
+                                                          const uint32_t* __restrict__ seg_off,
+                                                          const uint32_t* __restrict__ cyc_in,
+                                                          const uint32_t* __restrict__ rbits, uint32_t rperiod,
+                                                          uint8_t* __restrict__ ybuf) {
+  const uint32_t m = wgmap[blockIdx.x];
+  if (m == ~0u) return;
+  const uint32_t b = m >> 8, s = (m & 255u) * kWalkT + threadIdx.x;
+  const uint32_t c = slot[b];
+  const WalkBlock W(res[c]);
+  if (s >= W.ns) return;
+  const uint32_t t0 = seg_off[(size_t)b * kMaxSplit2 + s], cyc = cyc_in[b];
+  if (t0 >= cyc) return;
+  const bool rnd = res[c].rand != 0;
+  const uint32_t len = min(seg_len[(size_t)b * kMaxSplit2 + s], cyc - t0);
+  const uint32_t* Q = qbuf + (size_t)b * nbmax;
+  uint8_t* Y = ybuf + (size_t)c * nbmax;
+  uint32_t j = W.slot_of(s), t = t0;
+  ByteSink sink;
+  sink.init(Y + t0);
+  for (uint32_t k = 0; k < len; k++, t++) {
+    const uint32_t e = Q[j];
+    j = e >> 8;
+    uint32_t y = e & 0xffu;
+    if (rnd) y ^= rand_flip(rbits, rperiod, t);
+    sink.put(y);
+  }
+  sink.finish();
+}
+
+// A walk that closed its cycle early repeats it (periodic blocks): y[t] = raw[t mod cyc].
+__global__ void __launch_bounds__(256) k_dec_walk_repeat(const uint32_t* __restrict__ slot, const DecRes* __restrict__ res,
+                                                         uint32_t nbmax, const uint32_t* __restrict__ cyc_in,
+                                                         const uint32_t* __restrict__ rbits, uint32_t rperiod,
+                                                         uint8_t* __restrict__ ybuf) {
+  const uint32_t b = blockIdx.y, c = slot[b];
+  const uint32_t n = res[c].nblock, cyc = cyc_in[b];
+  if (cyc >= n || cyc == 0) return;
+  const bool rnd = res[c].rand != 0;
+  uint8_t* Y = ybuf + (size_t)c * nbmax;
+  for (uint32_t t = cyc + blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const uint32_t s = t % cyc;
+    uint32_t y = Y[s];
+    if (rnd) y ^= rand_flip(rbits, rperiod, s) ^ rand_flip(rbits, rperiod, t);
+    Y[t] = (uint8_t)y;
+  }
 }
 
 // ---- stage 4: un-RLE1 (bzlib.c:531-677) as a 5-state machine
@@ -776,116 +1121,187 @@ int decode_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, uint8_t* d_out,
     for (auto q = it; q != found.end() && cand.size() < kBatch; ++q)
       if (!(*q & 1)) cand.push_back(*q >> 1);
     const uint32_t nc = (uint32_t)cand.size();
+    const uint32_t symstride = nbmax + 128;
     uint64_t* d_cbit = ws.typed<uint64_t>("dec_cbit", nc);
     uint8_t* lbuf = ws.u8("dec_l", (size_t)nc * nbmax + 64);
+    uint16_t* symbuf = ws.u16("dec_sym", (size_t)nc * symstride);
+    uint8_t* tokbuf = ws.u8("dec_tok", (size_t)nc * symstride);
+    uint8_t* seqbuf = ws.u8("dec_seq", (size_t)nc * 256);
     uint8_t* selbuf = ws.u8("dec_sel", (size_t)nc * kSelCap + 64);
     DecRes* d_res = ws.typed<DecRes>("dec_res", nc);
     HIP_OK(hipMemcpyAsync(d_cbit, cand.data(), 8 * nc, hipMemcpyHostToDevice, st));
     static const bool dbg_on = getenv("BZG_DEC_DEBUG") != nullptr;
     uint64_t* d_dbg = dbg_on ? ws.typed<uint64_t>("dec_dbg", 4 * (size_t)nc) : nullptr;
-    k_dec_huff<<<nc, 64, 0, st>>>(d_in, n, d_cbit, nc, nbmax, lbuf, selbuf, d_res, d_dbg);
+    k_dec_huff<<<nc, 64, 0, st>>>(d_in, n, d_cbit, nc, nbmax, symstride, symbuf, seqbuf, selbuf, d_res, d_dbg);
     HIP_OK(hipGetLastError());
     if (dbg_on) {
       std::vector<uint64_t> h(4 * (size_t)nc);
       HIP_OK(hipMemcpyAsync(h.data(), d_dbg, 8 * h.size(), hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
-      double hc = 0, sc = 0, ns = 0, nbit = 0;
+      double hc = 0, sc = 0, nsy = 0, nbit = 0;
       for (uint32_t k = 0; k < nc; k++) {
         hc += (double)h[4 * k];
         sc += (double)h[4 * k + 1];
-        ns += (double)h[4 * k + 2];
+        nsy += (double)h[4 * k + 2];
         nbit += (double)h[4 * k + 3];
       }
       fprintf(stderr, "[bzg decode] %u candidates: header %.0f clk, symbols %.0f clk / %.0f sym = %.1f clk/sym, %.0f bits\n",
-              nc, hc / nc, sc / nc, ns / nc, sc / std::max(ns, 1.0), nbit / nc);
+              nc, hc / nc, sc / nc, nsy / nc, sc / std::max(nsy, 1.0), nbit / nc);
     }
     std::vector<DecRes> hres(nc);
     HIP_OK(hipMemcpyAsync(hres.data(), d_res, sizeof(DecRes) * nc, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     ds.candidates += nc;
-    // the chain of real blocks through this pass's candidates
+    // the chain of blocks through this pass's candidates; a block whose Huffman phase failed
+    // ends it (it still goes through phase 2, whose errors may come first)
     std::vector<uint32_t> chain;
-    int pending = BZ_OK;
-    bool at_end = false;  // the chain left this pass's window at a non-candidate / EOS
     for (;;) {
       auto ci = std::lower_bound(cand.begin(), cand.end(), pos);
-      if (ci == cand.end() || *ci != pos) {
-        at_end = true;
-        break;
-      }
+      if (ci == cand.end() || *ci != pos) break;
       const uint32_t k = (uint32_t)(ci - cand.begin());
-      if (hres[k].status != 0) {
-        pending = hres[k].status == BZ_UNEXPECTED_EOF ? 1 : BZ_DATA_ERROR;  // 1: EOF marker
-        break;
-      }
       chain.push_back(k);
+      if (hres[k].status != 0) break;
       pos = hres[k].end_bit;
     }
-    (void)at_end;
-    const uint32_t R = (uint32_t)chain.size();
+    uint32_t R = (uint32_t)chain.size();
     int stop = BZ_OK;  // a reason to stop inside this pass's blocks
     if (R) {
       uint32_t* d_slot = ws.u32("dec_slot", R);
       HIP_OK(hipMemcpyAsync(d_slot, chain.data(), 4 * R, hipMemcpyHostToDevice, st));
-      uint32_t* qbuf = ws.u32("dec_q", (size_t)R * nbmax + 16);
-      uint32_t* cyc = ws.u32("dec_cyc", R);
-      uint32_t* info = ws.u32("dec_info", (size_t)R * kRleChunks);
-      uint32_t* btot = ws.u32("dec_btot", 2 * R);
-      k_dec_tt<<<R, 1024, 0, st>>>(lbuf, d_slot, d_res, nbmax, qbuf);
-      HIP_OK(hipGetLastError());
-      // Y overwrites L in place: the walk reads only Q
-      k_dec_walk<<<R, 1024, 0, st>>>(qbuf, d_slot, d_res, nbmax, dw.rbits, dw.rperiod, lbuf, cyc);
-      HIP_OK(hipGetLastError());
-      k_dec_rle_scan<<<R, kRleChunks, 0, st>>>(lbuf, d_slot, d_res, nbmax, info, btot);
-      HIP_OK(hipGetLastError());
-      std::vector<uint32_t> htot(2 * R);
-      HIP_OK(hipMemcpyAsync(htot.data(), btot, 8 * R, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      // output order: block r is written only if every earlier block was; a block that ends
-      // in a pending count byte is corrupt (data error once its output fits)
-      std::vector<uint64_t> hoff(R);
-      uint32_t emit = 0;
-      uint64_t acc = produced;
+      // ---- phase 2: inverse MTF and runs -> L
+      std::vector<uint32_t> cfirst(R + 1, 0), ccand, cj;
       for (uint32_t r = 0; r < R; r++) {
-        if (acc + htot[2 * r] > out_cap) {
-          stop = BZ_OUTBUFF_FULL;
-          break;
+        const uint32_t nch = ceil_div(hres[chain[r]].nsym, kMtfChunk);
+        cfirst[r + 1] = cfirst[r] + nch;
+        for (uint32_t j = 0; j < nch; j++) {
+          ccand.push_back(chain[r]);
+          cj.push_back(j);
         }
-        if (htot[2 * r + 1] == 4) {
-          stop = BZ_DATA_ERROR;
-          break;
-        }
-        hoff[r] = acc;
-        acc += htot[2 * r];
-        emit++;
       }
-      if (emit) {
-        uint64_t* d_boff = ws.typed<uint64_t>("dec_boff", emit);
-        uint32_t* d_bcrc = ws.u32("dec_bcrc", emit);
-        HIP_OK(hipMemcpyAsync(d_boff, hoff.data(), 8 * emit, hipMemcpyHostToDevice, st));
-        k_dec_rle_emit<<<emit, kRleChunks, 0, st>>>(lbuf, d_slot, d_res, nbmax, info, btot, d_boff,
-                                                     ws.crc_table(), ws.xpow2_table(), d_out, d_bcrc);
+      const uint32_t Q = cfirst[R];
+      uint32_t* d_cfirst = ws.u32("dec_cfirst", R + 1);
+      uint32_t* d_ccand = ws.u32("dec_ccand", Q + 1);
+      uint32_t* d_cj = ws.u32("dec_cj", Q + 1);
+      uint32_t* permbuf = ws.u32("dec_perm", (size_t)Q * 64 + 64);
+      uint8_t* initbuf = ws.u8("dec_init", (size_t)Q * 256 + 256);
+      HIP_OK(hipMemcpyAsync(d_cfirst, cfirst.data(), 4 * (R + 1), hipMemcpyHostToDevice, st));
+      if (Q) {
+        HIP_OK(hipMemcpyAsync(d_ccand, ccand.data(), 4 * Q, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(d_cj, cj.data(), 4 * Q, hipMemcpyHostToDevice, st));
+        k_dec_mtf_sym<<<ceil_div(Q, 64), 64, 0, st>>>(symbuf, symstride, d_ccand, d_cj, Q, d_res, tokbuf, permbuf);
         HIP_OK(hipGetLastError());
-        std::vector<uint32_t> hcrc(emit);
-        HIP_OK(hipMemcpyAsync(hcrc.data(), d_bcrc, 4 * emit, hipMemcpyDeviceToHost, st));
+      }
+      k_dec_mtf_chain<<<R, 256, 0, st>>>(d_slot, d_cfirst, d_res, seqbuf, permbuf, initbuf);
+      HIP_OK(hipGetLastError());
+      k_dec_expand<<<R, 1024, 0, st>>>(d_slot, d_cfirst, nbmax, symstride, symbuf, tokbuf, initbuf, d_res, lbuf);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(hres.data(), d_res, sizeof(DecRes) * nc, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      // outcome of each chain block in stream order: a phase-2 rejection at a symbol the
+      // Huffman phase decoded comes first; then the Huffman phase's own failure; then origPtr
+      int pending = BZ_OK;
+      uint32_t ok = 0;
+      for (; ok < R; ok++) {
+        const DecRes& d = hres[chain[ok]];
+        const bool eob = d.status == 0;
+        if (d.err2 < d.nsym || (eob && d.err2 == d.nsym)) {
+          pending = BZ_DATA_ERROR;
+        } else if (!eob) {
+          pending = d.status == BZ_UNEXPECTED_EOF ? 1 : BZ_DATA_ERROR;  // 1: EOF marker
+        } else if (d.origptr >= d.nblock) {
+          pending = BZ_DATA_ERROR;
+        }
+        if (pending != BZ_OK) break;
+      }
+      R = ok;
+      if (R) {
+        uint32_t* qbuf = ws.u32("dec_q", (size_t)R * nbmax + 16);
+        uint32_t* cyc = ws.u32("dec_cyc", R);
+        uint32_t* info = ws.u32("dec_info", (size_t)R * kRleChunks);
+        uint32_t* btot = ws.u32("dec_btot", 2 * R);
+        k_dec_tt<<<R, 1024, 0, st>>>(lbuf, d_slot, d_res, nbmax, qbuf);
+        HIP_OK(hipGetLastError());
+        // Y overwrites L in place: the walk reads only Q
+        static const bool walk1 = getenv("BZG_DEC_WALK1") != nullptr;  // one workgroup per block
+        if (walk1) {
+          k_dec_walk<<<R, 1024, 0, st>>>(qbuf, d_slot, d_res, nbmax, dw.rbits, dw.rperiod, lbuf, cyc);
+          HIP_OK(hipGetLastError());
+        } else {
+          // workgroups of block b go to XCD b % 8, blocks of an XCD in order
+          std::vector<std::vector<uint32_t>> per(kNumXcd);
+          for (uint32_t r = 0; r < R; r++) {
+            const uint32_t nsp = ceil_div(hres[chain[r]].nblock, kSplit2) + 1;
+            for (uint32_t w = 0; w < ceil_div(nsp, kWalkT); w++) per[r % kNumXcd].push_back((r << 8) | w);
+          }
+          size_t G = 0;
+          for (auto& v : per) G = std::max(G, v.size());
+          std::vector<uint32_t> wgmap(kNumXcd * G, ~0u);
+          for (uint32_t x = 0; x < kNumXcd; x++)
+            for (size_t j = 0; j < per[x].size(); j++) wgmap[kNumXcd * j + x] = per[x][j];
+          uint32_t* d_wgmap = ws.u32("dec_wgmap", wgmap.size());
+          uint32_t* seg_nx = ws.u32("dec_segnx", (size_t)R * kMaxSplit2);
+          uint32_t* seg_len = ws.u32("dec_seglen", (size_t)R * kMaxSplit2);
+          uint32_t* seg_off = ws.u32("dec_segoff", (size_t)R * kMaxSplit2);
+          HIP_OK(hipMemcpyAsync(d_wgmap, wgmap.data(), 4 * wgmap.size(), hipMemcpyHostToDevice, st));
+          const uint32_t nwg = (uint32_t)wgmap.size();
+          k_dec_walk_seg<<<nwg, kWalkT, 0, st>>>(qbuf, d_slot, d_res, nbmax, d_wgmap, seg_nx, seg_len);
+          HIP_OK(hipGetLastError());
+          k_dec_walk_rank<<<R, 1024, 0, st>>>(d_slot, d_res, seg_nx, seg_len, seg_off, cyc);
+          HIP_OK(hipGetLastError());
+          k_dec_walk_emit<<<nwg, kWalkT, 0, st>>>(qbuf, d_slot, d_res, nbmax, d_wgmap, seg_len, seg_off, cyc,
+                                                   dw.rbits, dw.rperiod, lbuf);
+          HIP_OK(hipGetLastError());
+          k_dec_walk_repeat<<<dim3(64, R), 256, 0, st>>>(d_slot, d_res, nbmax, cyc, dw.rbits, dw.rperiod, lbuf);
+          HIP_OK(hipGetLastError());
+        }
+        k_dec_rle_scan<<<R, kRleChunks, 0, st>>>(lbuf, d_slot, d_res, nbmax, info, btot);
+        HIP_OK(hipGetLastError());
+        std::vector<uint32_t> htot(2 * R);
+        HIP_OK(hipMemcpyAsync(htot.data(), btot, 8 * R, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
-        for (uint32_t r = 0; r < emit; r++) {
-          produced += htot[2 * r];
-          if (hcrc[r] != hres[chain[r]].crc) {  // bzlib.c: block CRC check after its output
+        // output order: block r is written only if every earlier block was; a block that ends
+        // in a pending count byte is corrupt (data error once its output fits)
+        std::vector<uint64_t> hoff(R);
+        uint32_t emit = 0;
+        uint64_t acc = produced;
+        for (uint32_t r = 0; r < R; r++) {
+          if (acc + htot[2 * r] > out_cap) {
+            stop = BZ_OUTBUFF_FULL;
+            break;
+          }
+          if (htot[2 * r + 1] == 4) {
             stop = BZ_DATA_ERROR;
             break;
           }
-          combined = ((combined << 1) | (combined >> 31)) ^ hcrc[r];
-          ds.blocks++;
+          hoff[r] = acc;
+          acc += htot[2 * r];
+          emit++;
+        }
+        if (emit) {
+          uint64_t* d_boff = ws.typed<uint64_t>("dec_boff", emit);
+          uint32_t* d_bcrc = ws.u32("dec_bcrc", emit);
+          HIP_OK(hipMemcpyAsync(d_boff, hoff.data(), 8 * emit, hipMemcpyHostToDevice, st));
+          k_dec_rle_emit<<<emit, kRleChunks, 0, st>>>(lbuf, d_slot, d_res, nbmax, info, btot, d_boff,
+                                                       ws.crc_table(), ws.xpow2_table(), d_out, d_bcrc);
+          HIP_OK(hipGetLastError());
+          std::vector<uint32_t> hcrc(emit);
+          HIP_OK(hipMemcpyAsync(hcrc.data(), d_bcrc, 4 * emit, hipMemcpyDeviceToHost, st));
+          HIP_OK(hipStreamSynchronize(st));
+          for (uint32_t r = 0; r < emit; r++) {
+            produced += htot[2 * r];
+            if (hcrc[r] != hres[chain[r]].crc) {  // bzlib.c: block CRC check after its output
+              stop = BZ_DATA_ERROR;
+              break;
+            }
+            combined = ((combined << 1) | (combined >> 31)) ^ hcrc[r];
+            ds.blocks++;
+          }
         }
       }
+      if (stop == BZ_OK && pending != BZ_OK) stop = pending == 1 ? eof_code() : BZ_DATA_ERROR;
     }
     if (stop != BZ_OK) {
       rc = stop;
-      break;
-    }
-    if (pending != BZ_OK) {
-      rc = pending == 1 ? eof_code() : BZ_DATA_ERROR;
       break;
     }
   }
