@@ -953,13 +953,22 @@ __global__ void __launch_bounds__(kRleChunks) k_dec_rle_emit(const uint8_t* __re
                                                               const uint32_t* __restrict__ crc_table,
                                                               const uint32_t* __restrict__ xp2_g, uint8_t* __restrict__ out,
                                                               uint32_t* __restrict__ bcrc) {
-  __shared__ uint32_t tab[256];
+  __shared__ uint32_t tab[4][256];  // tab[k][b]: CRC of byte b followed by k zero bytes (slicing by 4)
   __shared__ uint32_t xp2[48];
   __shared__ uint32_t red[kRleChunks / 64];
   const uint32_t b = blockIdx.x, c = slot[b];
   const uint32_t n = res[c].nblock;
   const uint8_t* Y = ybuf + (size_t)c * nbmax;
-  tab[threadIdx.x] = crc_table[threadIdx.x];
+  {
+    uint32_t v = crc_table[threadIdx.x];
+    tab[0][threadIdx.x] = v;
+    __syncthreads();
+#pragma unroll
+    for (int k = 1; k < 4; k++) {
+      v = (v << 8) ^ tab[0][v >> 24];
+      tab[k][threadIdx.x] = v;
+    }
+  }
   if (threadIdx.x < 48) xp2[threadIdx.x] = xp2_g[threadIdx.x];
   __syncthreads();
   uint32_t lo, hi;
@@ -968,15 +977,19 @@ __global__ void __launch_bounds__(kRleChunks) k_dec_rle_emit(const uint8_t* __re
   const uint32_t off = inf >> 3, total = btot[2 * b];
   uint32_t s = inf & 7u;
   uint32_t prev = lo ? Y[lo - 1] : 0u;
-  uint32_t crc = 0, emitted = 0;
+  uint32_t crc = 0, emitted = 0, acc = 0, nacc = 0;  // acc: output bytes not yet in the CRC
   ByteSink sink;
   sink.init(out + boff[b] + off);
   auto emit = [&](uint32_t x) {
-    crc = (crc << 8) ^ tab[(crc >> 24) ^ x];
+    acc = (acc << 8) | x;
+    if (++nacc == 4) {
+      const uint32_t d = crc ^ acc;
+      crc = tab[3][d >> 24] ^ tab[2][(d >> 16) & 255u] ^ tab[1][(d >> 8) & 255u] ^ tab[0][d & 255u];
+      nacc = 0;
+    }
     sink.put(x);
   };
-  for (uint32_t i = lo; i < hi; i++) {
-    const uint32_t x = Y[i];
+  auto step = [&](uint32_t x) {
     if (s == 4) {
       for (uint32_t k = 0; k < x; k++) emit(prev);
       emitted += x;
@@ -987,7 +1000,16 @@ __global__ void __launch_bounds__(kRleChunks) k_dec_rle_emit(const uint8_t* __re
       s = (s == 0 || x != prev) ? 1u : s + 1;
     }
     prev = x;
+  };
+  uint32_t i = lo;
+  for (; i + 16 <= hi; i += 16) {  // chunks start 16-byte aligned
+    const uint4 q = *reinterpret_cast<const uint4*>(Y + i);
+    const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 16; k++) step((wv[k >> 2] >> (8 * (k & 3))) & 0xffu);
   }
+  for (; i < hi; i++) step(Y[i]);
+  for (uint32_t k = 0; k < nacc; k++) crc = (crc << 8) ^ tab[0][(crc >> 24) ^ ((acc >> (8 * (nacc - 1 - k))) & 255u)];
   sink.finish();
   uint32_t part = emitted ? shift8(crc, xp2, (uint64_t)(total - off - emitted)) : 0u;
 #pragma unroll
