@@ -1596,7 +1596,9 @@ __global__ void k_unit_scatter(const Grp* __restrict__ L, uint32_t n, uint32_t* 
 }
 
 // ---------------------------------------------------------------- fallback glue
-__global__ void k_fb_flag(const Grp* __restrict__ D, uint32_t n, uint32_t* __restrict__ uflag, uint32_t* __restrict__ mind) {
+__global__ void __launch_bounds__(kT) k_fb_flag(const Grp* __restrict__ D, uint32_t n, uint32_t* __restrict__ uflag,
+                                                uint32_t* __restrict__ mind) {
+  __shared__ uint32_t wmin[kT / 64];
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t d = 0xffffffffu;
   if (g < n) {
@@ -1606,29 +1608,55 @@ __global__ void k_fb_flag(const Grp* __restrict__ D, uint32_t n, uint32_t* __res
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) d = min(d, (uint32_t)__shfl_xor((int)d, o, 64));
-  if (__lane_id() == 0 && d != 0xffffffffu) atomicMin(mind, d);
+  if (__lane_id() == 0) wmin[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // one atomic per workgroup (tens of millions of deep groups)
+    uint32_t m = wmin[0];
+    for (int w = 1; w < kT / 64; w++) m = min(m, wmin[w]);
+    if (m != 0xffffffffu) atomicMin(mind, m);
+  }
+}
+
+// f(group, member) over the members of groups L[0..n): a lane per group walks a small group
+// itself, the wave walks the large ones of its 64 together (deep groups are mostly pairs, so a
+// workgroup per group left almost every lane idle).
+constexpr uint32_t kLaneGroup = 32;
+template <typename F>
+__device__ __forceinline__ void for_members(const Grp* __restrict__ L, uint32_t n, F&& f) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  Grp gr{0, 0, 0, 0};
+  if (g < n) gr = L[g];
+  const bool big = gr.size > kLaneGroup;
+  if (!big)
+    for (uint32_t e = 0; e < gr.size; e++) f(gr, e);
+  uint64_t m = __ballot(big);
+  while (m) {
+    const int l = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    const Grp G{(uint32_t)__shfl((int)gr.start, l, 64), (uint32_t)__shfl((int)gr.size, l, 64),
+                (uint32_t)__shfl((int)gr.unit, l, 64), (uint32_t)__shfl((int)gr.flags, l, 64)};
+    for (uint32_t e = __lane_id(); e < G.size; e += 64) f(G, e);
+  }
 }
 
 // Deep groups whose data is in the alternate buffer move to the primary SA; the doubling
-// list gets the groups with their flags reset.  One workgroup per group.
-// (The per-group kernels below stride over the groups: one workgroup per group could exceed
-// the 2^32 threads a launch may hold when there are tens of millions of deep groups.)
+// list gets the groups with their flags reset.
 __global__ void __launch_bounds__(kT) k_fb_copy(const Grp* __restrict__ D, uint32_t n, Grp* __restrict__ L0, SortBufs B) {
-  for (uint32_t g = blockIdx.x; g < n; g += gridDim.x) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) {
     const Grp gr = D[g];
-    if (gr.flags & kGrpAlt)
-      for (uint32_t e = threadIdx.x; e < gr.size; e += kT) B.sa[gr.start + e] = B.sa2[gr.start + e];
-    if (threadIdx.x == 0) L0[g] = Grp{gr.start, gr.size, gr.unit, 0};
+    L0[g] = Grp{gr.start, gr.size, gr.unit, 0};
   }
+  for_members(D, n, [&](const Grp& gr, uint32_t e) {
+    if (gr.flags & kGrpAlt) B.sa[gr.start + e] = B.sa2[gr.start + e];
+  });
 }
 
 // Members of a deep group take the group's first slot as rank (after k_fb_isa_all).
 __global__ void __launch_bounds__(kT) k_fb_group_isa(const Grp* __restrict__ L0, uint32_t n, SortBufs B) {
-  for (uint32_t g = blockIdx.x; g < n; g += gridDim.x) {
-    const Grp gr = L0[g];
-    const uint32_t sb = B.units[gr.unit].sbase;
-    for (uint32_t e = threadIdx.x; e < gr.size; e += kT) B.isa[sb + B.sa[gr.start + e]] = gr.start;
-  }
+  for_members(L0, n, [&](const Grp& gr, uint32_t e) {
+    B.isa[B.units[gr.unit].sbase + B.sa[gr.start + e]] = gr.start;
+  });
 }
 
 // ISA of every slot of the listed units from the (complete, primary) SA: every rotation's own
@@ -1649,19 +1677,16 @@ __global__ void __launch_bounds__(kT) k_fb_isa_all(const uint32_t* __restrict__ 
 }
 
 // BWT bytes of the slots of the deep groups (everything else was written when its rotation
-// was ordered), for aperiodic units; one workgroup per deep group.
+// was ordered), for aperiodic units.
 __global__ void __launch_bounds__(kT) k_deep_out(const Grp* __restrict__ L0, uint32_t n, const Unit* __restrict__ units,
                                                  const uint32_t* __restrict__ sa, const uint8_t* __restrict__ text,
                                                  uint8_t* __restrict__ bwt) {
-  for (uint32_t gi = blockIdx.x; gi < n; gi += gridDim.x) {
-    const Grp g = L0[gi];
+  for_members(L0, n, [&](const Grp& g, uint32_t e) {
     const Unit U = units[g.unit];
-    if (U.k != 1) continue;  // periodic roots: the whole last column is written afterwards
-    for (uint32_t e = threadIdx.x; e < g.size; e += kT) {
-      const uint32_t v = sa[g.start + e];
-      bwt[U.toff + g.start + e - U.sbase] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
-    }
-  }
+    if (U.k != 1) return;  // periodic roots: the whole last column is written afterwards
+    const uint32_t v = sa[g.start + e];
+    bwt[U.toff + g.start + e - U.sbase] = text[U.toff + (v == 0 ? U.len - 1 : v - 1)];
+  });
 }
 
 // Last column of the listed units from the SA (periodic roots repeated k times).
@@ -1741,7 +1766,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   {
     static const uint32_t dwave = [] {
       const char* e = getenv("BZG_DWAVE");
-      return e ? (uint32_t)std::max(16, atoi(e)) : 1024u;
+      return e ? (uint32_t)std::max(16, atoi(e)) : 256u;  // tuned: profiles/r02_dwave_sweep.txt
     }();
     B.dwave = dwave;
   }
@@ -2015,14 +2040,14 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
                 k == 0 ? "tiny" : k == 1 ? "tail" : "s1", (unsigned long long)h[k][0], (unsigned long long)h[k][1],
                 (unsigned long long)h[k][2], (unsigned long long)h[k][3]);
     }
-    k_fb_copy<<<std::min<uint32_t>(n_deep, 1u << 16), kT, 0, st>>>(O.deep, n_deep, L0, B);
+    k_fb_copy<<<grid(n_deep), kT, 0, st>>>(O.deep, n_deep, L0, B);
     HIP_OK(hipGetLastError());
     {
       const uint32_t nu = (uint32_t)fb_units.size(), chunks = ceil_div(flen, kT);
       k_fb_isa_all<<<kNumXcd * ceil_div(nu, kNumXcd) * chunks, kT, 0, st>>>(ulist, nu, chunks, units, B);
     }
     HIP_OK(hipGetLastError());
-    k_fb_group_isa<<<std::min<uint32_t>(n_deep, 1u << 16), kT, 0, st>>>(L0, n_deep, B);
+    k_fb_group_isa<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B);
     HIP_OK(hipGetLastError());
     if (debug) {
       std::vector<Grp> hd(n_deep);
@@ -2043,7 +2068,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     if (getenv("BZG_FULL_UNIT_OUT")) {
       k_unit_out<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B.sa, r.blk, bwt);
     } else {
-      k_deep_out<<<std::min<uint32_t>(n_deep, 1u << 16), kT, 0, st>>>(L0, n_deep, units, B.sa, r.blk, bwt);
+      k_deep_out<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, units, B.sa, r.blk, bwt);
     }
     HIP_OK(hipGetLastError());
     k_rank0_isa<<<grid(fb_units.size()), kT, 0, st>>>(ulist, (uint32_t)fb_units.size(), units, B.isa, rank0);
