@@ -192,6 +192,16 @@ __global__ void k_group_tiles(const Grp* __restrict__ L, uint32_t n, uint32_t* _
   if (g < n) cnt[g] = ceil_div(L[g].size, kDTile);
 }
 
+// TG[t] = the group of tile t (TP: exclusive scan of the groups' tile counts), so that a tile
+// finds its group with one load instead of a binary search over TP (a chain of dependent loads).
+__global__ void k_tile_owner(const Grp* __restrict__ L, uint32_t n, const uint32_t* __restrict__ TP,
+                             uint32_t* __restrict__ TG) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const uint32_t t0 = TP[g], c = ceil_div(L[g].size, kDTile);
+  for (uint32_t k = 0; k < c; k++) TG[t0 + k] = g;
+}
+
 // LDS exchange among the lanes of one wave (LDS operations of a wave complete in order)
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
@@ -257,11 +267,11 @@ __device__ __forceinline__ uint32_t s1_next_cache(const Grp& gr) {
   return c ? c - 1 : 3u;
 }
 
-__global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
-                                                SortBufs B, uint32_t* __restrict__ hist) {
+__global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, const uint32_t* __restrict__ TG,
+                                                const uint32_t* __restrict__ TP, SortBufs B, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[256];
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t g = upper_idx(TP, nG, t);
+  const uint32_t g = TG[t];
   const Grp gr = G[g];
   const Unit U = B.units[gr.unit];
   const uint32_t lo = (t - TP[g]) * kDTile, hi = min(gr.size, lo + kDTile);
@@ -324,7 +334,8 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
 // Scatter of one tile into the bucket order; the first tile of a group also emits the
 // group's buckets into the class lists (cscan: exclusive scan of ccnt).  The tile is first
 // reordered by bucket in LDS, so the global stores run along each bucket's range.
-__global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, uint32_t nG, const uint32_t* __restrict__ TP,
+__global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, const uint32_t* __restrict__ TG,
+                                                   const uint32_t* __restrict__ TP,
                                                    SortBufs B, SortOut O, const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ tot, const uint32_t* __restrict__ cscan,
                                                    uint32_t nTot, ClsLists C) {
@@ -336,7 +347,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, ui
   __shared__ uint32_t Lv[kDTile], Lk[kDTile];
   static_assert(kDTile == kPerT * kT, "one element per thread and round");
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t g = upper_idx(TP, nG, t);
+  const uint32_t g = TG[t];
   const Grp gr = G[g];
   const Unit U = B.units[gr.unit];
   const uint32_t lo = (t - TP[g]) * kDTile, hi = min(gr.size, lo + kDTile);
@@ -1797,6 +1808,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   const size_t max_ptiles = S / kSG + 64;
   const size_t max_tot = ccap[7] + max_ptiles;
   uint32_t* TP = ws.u32("sort_TP", max_tiles + 16);
+  uint32_t* TG = ws.u32("sort_TG", max_tiles + 16);
   uint32_t* hist = ws.u32("sort_hist", max_tiles * 256);
   uint32_t* tot = ws.u32("sort_tot", ccap[7] * 256);
   uint32_t* ccnt = ws.u32("sort_ccnt", kNCls * max_tot + 16);
@@ -1852,6 +1864,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_group_tiles<<<grid(n7), kT, 0, st>>>(cur7, n7, TP);
       HIP_OK(hipGetLastError());
       scan_u32(ScanOp::Sum, true, TP, TP, n7, cnt + 17, scratch, st);
+      k_tile_owner<<<grid(n7), kT, 0, st>>>(cur7, n7, TP, TG);
+      HIP_OK(hipGetLastError());
     }
     if (n6) {
       k_group_sizes<<<grid(n6), kT, 0, st>>>(cur6, n6, P);
@@ -1879,7 +1893,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     if (n7) {
-      k_s1_hist<<<ntl, kT, 0, st>>>(cur7, n7, TP, B, hist);
+      k_s1_hist<<<ntl, kT, 0, st>>>(cur7, TG, TP, B, hist);
       HIP_OK(hipGetLastError());
       k_s1_off<<<n7, kT, 0, st>>>(cur7, nTot, TP, hist, tot, ccnt, O.deep, O.n_deep);
       HIP_OK(hipGetLastError());
@@ -1893,7 +1907,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     Cp.l[7] = nxt7;
     Cp.base[6] = Cp.base[7] = 0;
     if (n7) {
-      k_s1_scatter<<<ntl, kT, 0, st>>>(cur7, n7, TP, B, O, hist, tot, ccnt, nTot, Cp);
+      k_s1_scatter<<<ntl, kT, 0, st>>>(cur7, TG, TP, B, O, hist, tot, ccnt, nTot, Cp);
       HIP_OK(hipGetLastError());
       k_s1_single<<<n7, kT, 0, st>>>(cur7, B, tot);
       HIP_OK(hipGetLastError());
