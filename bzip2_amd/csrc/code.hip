@@ -144,9 +144,9 @@ __global__ void k_init_tables(const uint32_t* __restrict__ nmtf_g, const uint32_
 }
 
 struct CfLds {
+  uint16_t chunk[kT * kGroupSize + 8];
   uint32_t lenp[2][kMaxAlpha];       // lengths of tables 0-2 / 3-5 in 10-bit fields
   uint32_t rfreq[kNGroups][kMaxAlpha];
-  uint16_t chunk[kT * kGroupSize + 8];
   uint32_t sh[8];
 };
 
@@ -431,6 +431,11 @@ struct BitWriter {
 // nbits up to 32 may overflow the accumulator when nacc > 32 after a put; put() keeps
 // nacc < 32 on exit, so a put of <= 32 bits never loses bits.
 
+#ifndef BZG_PACK_SLICES
+#define BZG_PACK_SLICES 1
+#endif
+constexpr uint32_t kPackSlices = BZG_PACK_SLICES;  // workgroups per block in k_pack
+
 struct PackLds {
   uint16_t chunk[kT * kGroupSize + 8];
   uint32_t bits[(kT * kGroupSize * kMaxCodeLen + 31) / 32 + 2];  // one step's payload
@@ -447,7 +452,10 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
   __shared__ uint32_t code[kNGroups][kMaxAlpha];
   __shared__ uint32_t sh[8];
   __shared__ PackLds P;
-  const uint32_t b = blockIdx.x;
+  // kPackSlices workgroups per block: slice 0 also writes the block header, tables and
+  // selectors; slice s packs its share of the payload steps from the bit offset of its first
+  // group (p_dat + the bits of the groups before it)
+  const uint32_t b = blockIdx.y, slice = blockIdx.x;
   const uint32_t* info = info_g + (size_t)b * 8;
   const int ng = (int)info[0];
   const uint32_t nsel = info[1];
@@ -469,7 +477,7 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
   const uint64_t p_tab = p_sel + info[4];
   const uint64_t p_dat = p_tab + info[5];
   // header, symbol map, nGroups, nSelectors: lane 0
-  if (threadIdx.x == 0) {
+  if (slice == 0 && threadIdx.x == 0) {
     BitWriter w(out, p0);
     w.put(24, 0x314159);
     w.put(24, 0x265359);
@@ -496,7 +504,7 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
     w.flush();
   }
   // code-length tables: lane t writes table t
-  if (threadIdx.x < (unsigned)ng) {
+  if (slice == 0 && threadIdx.x < (unsigned)ng) {
     const int t = threadIdx.x;
     uint64_t pos = p_tab;
     for (int u = 0; u < t; u++) {
@@ -528,7 +536,7 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
   }
   // selectors (unary MTF codes): thread-blocked ranges
   const uint8_t* smo = selmtf_g + (size_t)b * kMaxSelectors;
-  {
+  if (slice == 0) {
     const uint32_t per = ceil_div(nsel, kT);
     const uint32_t lo = min(nsel, threadIdx.x * per), hi = min(nsel, lo + per);
     uint32_t bits = 0;
@@ -547,8 +555,17 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
   {
     const uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
     const uint16_t* gb = gbits_g + (size_t)b * kMaxSelectors;
+    const uint32_t nsteps = ceil_div(nsel, kT), sps = ceil_div(nsteps, kPackSlices);
+    const uint32_t s0 = min(nsteps, slice * sps), s1 = min(nsteps, s0 + sps);
     uint64_t pos = p_dat;  // bit position of the step
-    for (uint32_t g0 = 0; g0 < nsel; g0 += kT) {
+    {
+      uint32_t before = 0;
+      for (uint32_t g = threadIdx.x; g < s0 * kT; g += kT) before += gb[g];
+      uint32_t tot;
+      block_incl_sum(before, sh, &tot);
+      pos += tot;
+    }
+    for (uint32_t g0 = s0 * kT; g0 < s1 * kT; g0 += kT) {
       const uint32_t lo = g0 * kGroupSize, hi = min((g0 + kT) * kGroupSize, nmtf);
       for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) P.chunk[i - lo] = mv[i];
       const uint32_t g = g0 + threadIdx.x;
@@ -661,7 +678,7 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
   HIP_OK(hipMemsetAsync(out, 0, need, st));
   if (carry.carry_bits) HIP_OK(hipMemcpyAsync(out, &carry.carry_byte, 1, hipMemcpyHostToDevice, st));
   if (nb > 0) {
-    k_pack<<<nb, kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, r.inuse, r.bcrc, origptr, lens, codes, sel, selmtf, gbits, info,
+    k_pack<<<dim3(kPackSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, r.inuse, r.bcrc, origptr, lens, codes, sel, selmtf, gbits, info,
                               bbits, (uint32_t*)out);
     HIP_OK(hipGetLastError());
   }

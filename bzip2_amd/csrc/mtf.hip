@@ -68,7 +68,10 @@ __device__ __forceinline__ ChunkRef chunk_ref(const uint32_t* __restrict__ boff,
   return r;
 }
 
-// 1. signatures
+// 1. signatures.  One lane per chunk walks its chunk backwards in 16-byte words; the words
+// of the next kSigAhead steps are in flight while a word is processed (the walk is otherwise
+// bound by the latency of one load per 16 symbols).
+constexpr uint32_t kSigAhead = 4;
 __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                             const uint32_t* __restrict__ cbase, uint8_t* __restrict__ sig,
                                             uint32_t* __restrict__ siglen) {
@@ -77,18 +80,43 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
   uint8_t* out = sig + (size_t)r.gidx * 256;
   uint32_t cnt = 0;
   uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // seen bytes, in registers
-  for_bytes<false>(L, r.lo, r.hi, [&](uint32_t, uint32_t c) {
-    const uint64_t bit = 1ull << (c & 63);
-    const uint32_t q = c >> 6;
-    const uint64_t w = q == 0 ? s0 : q == 1 ? s1 : q == 2 ? s2 : s3;
-    if (!(w & bit)) {
-      s0 |= q == 0 ? bit : 0ull;
-      s1 |= q == 1 ? bit : 0ull;
-      s2 |= q == 2 ? bit : 0ull;
-      s3 |= q == 3 ? bit : 0ull;
-      out[cnt++] = (uint8_t)c;
+  const uint32_t a_lo = r.lo & ~15u;
+  uint32_t a = (r.hi - 1) & ~15u;  // word being processed (walking down to a_lo)
+  uint4 q[kSigAhead];
+#pragma unroll
+  for (uint32_t k = 0; k < kSigAhead; k++) {
+    const uint32_t ak = a - 16 * k;
+    q[k] = (ak >= a_lo && ak <= a) ? *reinterpret_cast<const uint4*>(L + ak) : make_uint4(0, 0, 0, 0);
+  }
+  for (;;) {
+    const uint4 cur = q[0];
+#pragma unroll
+    for (uint32_t k = 0; k + 1 < kSigAhead; k++) q[k] = q[k + 1];
+    {
+      const uint32_t an = a - 16 * kSigAhead;  // the word kSigAhead steps down
+      q[kSigAhead - 1] = (a >= a_lo + 16 * kSigAhead) ? *reinterpret_cast<const uint4*>(L + an) : make_uint4(0, 0, 0, 0);
     }
-  });
+    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+    for (int k = 15; k >= 0; k--) {
+      const uint32_t i = a + k;
+      if (i >= r.lo && i < r.hi) {
+        const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        const uint64_t bit = 1ull << (c & 63);
+        const uint32_t qq = c >> 6;
+        const uint64_t sw = qq == 0 ? s0 : qq == 1 ? s1 : qq == 2 ? s2 : s3;
+        if (!(sw & bit)) {
+          s0 |= qq == 0 ? bit : 0ull;
+          s1 |= qq == 1 ? bit : 0ull;
+          s2 |= qq == 2 ? bit : 0ull;
+          s3 |= qq == 3 ? bit : 0ull;
+          out[cnt++] = (uint8_t)c;
+        }
+      }
+    }
+    if (a <= a_lo) break;
+    a -= 16;
+  }
   siglen[r.gidx] = cnt;
 }
 
@@ -405,10 +433,12 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
     const uint32_t lo = boff[b] + c * kChunk, hi = min(boff[b + 1], lo + kChunk);
     const uint32_t g = cbase[b] + c;
     const uint32_t base = lo + lane * 16;
+    // every load the chunk needs, issued before any is used
+    const uint4 q = *reinterpret_cast<const uint4*>(ranks + (size_t)g * kChunk + lane * 16);
+    const uint32_t zin_g = zin[g], coff_g = coff[g], fr = finalrun[b], moff_b = mtf_off[b], eob = ninuse[b] + 1;
     uint32_t rk[16];
     uint32_t nzmask = 0;
     {  // chunk-aligned ranks (k_mtf_run): one 16-byte load per lane
-      const uint4 q = *reinterpret_cast<const uint4*>(ranks + (size_t)g * kChunk + lane * 16);
       const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int k = 0; k < 16; k++) rk[k] = base + k < hi ? (wd[k >> 2] >> (8 * (k & 3))) & 0xffu : 0u;
@@ -438,7 +468,7 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
     if (lane == 0) cin = cfl = 0;
     // the run before the chunk's first nonzero rank is zin (it includes the chunk's leading
     // zeros, k_rle2_plan); later runs end inside the chunk
-    const uint32_t run0 = cfl ? cin + lz : zin[g];
+    const uint32_t run0 = cfl ? cin + lz : zin_g;
     uint32_t ecount = 0;
     if (has) {
       ecount += nsym(run0);
@@ -459,7 +489,6 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
       }
     }
     const bool lastchunk = hi == boff[b + 1];
-    const uint32_t fr = finalrun[b];
     const uint32_t tail = (lastchunk && lane == 63) ? nsym(fr) + 1 : 0u;  // final run + EOB
     const uint32_t tot = ecount + tail;
     const uint32_t incl = wave_incl_sum(tot), excl = incl - tot;
@@ -496,14 +525,13 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
     }
     if (tail) {
       put_run(fr);
-      const uint32_t eob = ninuse[b] + 1;
       out[o++] = (uint16_t)eob;
       atomicAdd(&hist[eob], 1u);
     }
     if (runa) atomicAdd(&hist[0], runa);
     if (runb) atomicAdd(&hist[1], runb);
     __builtin_amdgcn_wave_barrier();
-    uint16_t* gout = mtfv + mtf_off[b] + coff[g];
+    uint16_t* gout = mtfv + moff_b + coff_g;
     for (uint32_t i = lane; i < wtot; i += 64) gout[i] = st[i];
   }
   __syncthreads();

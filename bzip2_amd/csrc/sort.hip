@@ -34,7 +34,7 @@ namespace {
 constexpr int kT = 256;
 constexpr uint32_t kBig = 256;        // buckets larger than this are split by S1 byte passes
 #ifndef BZG_DTILE
-#define BZG_DTILE 4096
+#define BZG_DTILE 2048
 #endif
 constexpr uint32_t kDTile = BZG_DTILE;  // rotations per workgroup in an S1 pass
 constexpr uint32_t kPerT = kDTile / kT;

@@ -465,7 +465,10 @@ def test_full_size_single_byte_4gib():
 def test_full_size_random_4gib_properties():
     """BASELINE config 5 at full size: 4 GiB of PRNG bytes.  Properties (the whole-stream
     reference run takes too long here): output size of an incompressible stream
-    (about 1.0044 x input), and the first 256 MiB decode exactly."""
+    (about 1.0044 x input); the whole stream decodes back to the input on the GPU decoder
+    (every block CRC and the combined CRC checked), and its first 256 MiB also through the
+    system decoder (an independent implementation)."""
+    torch = pytest.importorskip("torch")
     n = 1 << 32
     data = np.random.default_rng(0x5EED0005).integers(0, 256, size=n, dtype=np.uint8).tobytes()
     comp = B.stream_compress(_chunks(data, 1 << 28), 9, out_chunk=1 << 24)
@@ -473,6 +476,16 @@ def test_full_size_random_4gib_properties():
     d = bz2.BZ2Decompressor()
     head = d.decompress(comp, max_length=1 << 28)
     assert head == data[: 1 << 28]
+    del head, d
+    d_comp = torch.frombuffer(bytearray(comp), dtype=torch.uint8).to("cuda")
+    del comp
+    d_out = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    rc, got = B.decompress_device(d_comp.data_ptr(), d_comp.numel(), d_out.data_ptr(), n + 64,
+                                  stream_ptr=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rc == B.BZ_OK and got == n
+    d_ref = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+    assert torch.equal(d_out[:n], d_ref)
 
 
 def test_device_api_with_torch_buffers():
