@@ -325,7 +325,7 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
   }
   if (cl == kClsDeep) {  // rare: a bucket still larger than kBig after kDBig characters
     const uint32_t dst_alt = (gr.flags & kGrpIdent) ? 0u : ((gr.flags & kGrpAlt) ^ 1u);
-    deep[atomicAdd(n_deep, 1u)] = Grp{base, total, gr.unit, grp_flags(dst_alt, depth, s1_next_cache(gr))};
+    deep[wave_append(n_deep, true)] = Grp{base, total, gr.unit, grp_flags(dst_alt, depth, s1_next_cache(gr))};
   }
   __syncthreads();
   if (d < (uint32_t)kNCls) ccnt[(size_t)d * nTot + g] = cc[d];
@@ -710,7 +710,7 @@ __global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, con
     const uint32_t dst_alt = (fl & kGrpIdent) ? 0u : ((fl & kGrpAlt) ^ 1u);
     const Grp nb{gstart[j] + start - goff[j], total, gunit[j], grp_flags(dst_alt, depth, s1_next_cache(Grp{0, 0, 0, fl}))};
     if (cl == kClsDeep) {
-      O.deep[atomicAdd(O.n_deep, 1u)] = nb;
+      O.deep[wave_append(O.n_deep, true)] = nb;
     } else {
       const uint32_t q = atomicAdd(&cc[cl], 1u);
       C.l[cl][C.base[cl] + cscan[(size_t)cl * nTot + ibase + t] - cscan[(size_t)cl * nTot] + q] = nb;
@@ -1034,13 +1034,69 @@ __device__ __forceinline__ void text_key8(const uint8_t* t, uint32_t len, uint32
   lo = y;
 }
 
-// ---- tiny buckets: lane l takes rotation l % 8 of bucket 8 * wave + l / 8.  Every step
+// The value of lane ^ M (M = 1..7) of this lane's aligned 8-lane group, by DPP only (no LDS
+// traffic): quad permutes of v, or of its half-row mirror hm = g8_mirror(v) (lane ^ 7).
+__device__ __forceinline__ uint32_t g8_mirror(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+}
+template <int M>
+__device__ __forceinline__ uint32_t g8_xor(uint32_t v, uint32_t hm) {
+  static_assert(M >= 1 && M <= 7, "partner within the 8-lane group");
+  constexpr int kQuad = (M & 3) == 1 ? 0xB1 : (M & 3) == 2 ? 0x4E : 0x1B;  // quad xor 1 / 2 / 3
+  if constexpr (M == 7) return hm;
+  else if constexpr (M < 4) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kQuad, 0xF, 0xF, false);
+  else {  // lane ^ M = (lane ^ 7) ^ (M ^ 7)
+    constexpr int kQ = (M ^ 7) == 1 ? 0xB1 : (M ^ 7) == 2 ? 0x4E : 0x1B;
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)hm, kQ, 0xF, 0xF, false);
+  }
+}
+
+// Buckets of two rotations (most tiny buckets; long repeats make tens of millions of them)
+// go to a kernel with 2 lanes per bucket, the others to 8 lanes per bucket.
+// One workgroup per kSplitPer * kT list entries (thread t: entries [t * kSplitPer, ...) of the
+// workgroup's range, so both outputs keep the list order) and one atomic per output per
+// workgroup: single-address device atomics cost ~10 ns each, one per wave was 5 ms per GB.
+constexpr uint32_t kSplitPer = 16;
+__global__ void __launch_bounds__(kT) k_split_pairs(const Grp* __restrict__ L, uint32_t n, Grp* __restrict__ pairs,
+                                                    Grp* __restrict__ rest, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t base[2];
+  const uint32_t i0 = (blockIdx.x * kT + threadIdx.x) * kSplitPer;
+  Grp g[kSplitPer];
+  uint32_t np = 0, nr = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kSplitPer; k++) {
+    g[k] = i0 + k < n ? L[i0 + k] : Grp{0, 0, 0, 0};
+    np += (i0 + k < n && g[k].size == 2) ? 1u : 0u;
+    nr += (i0 + k < n && g[k].size != 2) ? 1u : 0u;
+  }
+  uint32_t tp, tr;
+  const uint32_t ep = block_incl_sum(np, sh, &tp) - np;
+  const uint32_t er = block_incl_sum(nr, sh, &tr) - nr;
+  if (threadIdx.x == 0) {
+    base[0] = tp ? atomicAdd(cnt, tp) : 0u;
+    base[1] = tr ? atomicAdd(cnt + 1, tr) : 0u;
+  }
+  __syncthreads();
+  uint32_t p = base[0] + ep, r = base[1] + er;
+#pragma unroll
+  for (uint32_t k = 0; k < kSplitPer; k++) {
+    if (i0 + k < n) {
+      if (g[k].size == 2) pairs[p++] = g[k];
+      else rest[r++] = g[k];
+    }
+  }
+}
+
+// ---- tiny buckets: lane l takes rotation l % kW of bucket (64 / kW) * wave + l / kW.  Every step
 // compares the next 16 characters with the rotations of its bucket still tied with it
 // (same class, named by its first lane) and adds the smaller ones to its position.
+template <int kW>
 __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint32_t n_tiny, SortBufs B, SortOut O) {
+  static_assert(kW == 2 || kW == 8, "lanes per bucket");
   const uint32_t lane = __lane_id();
   const uint32_t wv = s2_wg() * (kT / 64) + (threadIdx.x >> 6);
-  const uint32_t bi = wv * 8 + lane / 8, el = lane % 8;
+  const uint32_t bi = wv * (64 / kW) + lane / kW, el = lane % kW;
   bool act = false;
   uint32_t s0 = 0, d = 0, v = 0, unit = 0;
   if (bi < n_tiny) {
@@ -1060,49 +1116,76 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
   uint8_t lastc = 0;  // BWT byte of this rotation, loaded with the first key
   if (act) lastc = t[v == 0 ? U.len - 1 : v - 1];
   bool done = !act;
-  uint32_t cls = act ? (lane & ~7u) : 0xffffffffu;
+  uint32_t cls = act ? (lane & ~(uint32_t)(kW - 1)) : 0xffffffffu;
   uint32_t pos = 0;
-  const int base = (int)(lane & ~7u);
   for (;;) {
     const uint64_t live = __ballot(!done);
     if (live == 0) break;
     // still tied after B.dwave characters: leave to the doubling fallback.  The members of a
     // class and their ranks come from the bucket's 8 lanes (all lanes of the wave still run
     // here, so every shuffle source is active)
-    const bool deep_now = d >= B.dwave;
+    const bool deep_now = d >= B.dwave_tiny;
     if (__ballot(deep_now)) {
-      uint32_t cnt = 0, r = 0;
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const uint32_t cj = (uint32_t)__shfl((int)cls, base + j, 64);
+      uint32_t cnt = 1, r = 0;  // this lane, then the others of its bucket
+      const uint32_t hc = kW == 8 ? g8_mirror(cls) : 0u;
+      auto member = [&](uint32_t src, uint32_t cj) {
         if (cj == cls) {
           cnt++;
-          r += (uint32_t)(base + j) < lane;
+          r += src < lane;
         }
+      };
+      member(lane ^ 1u, g8_xor<1>(cls, hc));
+      if constexpr (kW == 8) {
+        member(lane ^ 2u, g8_xor<2>(cls, hc));
+        member(lane ^ 3u, g8_xor<3>(cls, hc));
+        member(lane ^ 4u, g8_xor<4>(cls, hc));
+        member(lane ^ 5u, g8_xor<5>(cls, hc));
+        member(lane ^ 6u, g8_xor<6>(cls, hc));
+        member(lane ^ 7u, g8_xor<7>(cls, hc));
       }
       if (deep_now && !done) {
         B.sa[s0 + pos + r] = v;
-        if (r == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
+        const uint32_t ds = wave_append(O.n_deep, r == 0);  // one atomic per wave
+        if (r == 0) O.deep[ds] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
       }
       if (deep_now) break;
     }
     uint32_t k[4] = {0u, 0u, 0u, 0u};
     if (!done) text_key16(t, U.len, cyc_pos(v, d, U.len), k);
     const uint64_t khi = ((uint64_t)k[0] << 32) | k[1], klo = ((uint64_t)k[2] << 32) | k[3];
-    uint32_t lt = 0, eq = 0, rep = lane;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const int src = base + j;
-      const uint32_t cj = (uint32_t)__shfl((int)cls, src, 64);
-      const uint64_t hj = __shfl(khi, src, 64);
-      const uint64_t lj = __shfl(klo, src, 64);
-      if (cj == cls) {
-        lt += (hj < khi) || (hj == khi && lj < klo);
-        if (hj == khi && lj == klo) {
-          if (eq == 0) rep = (uint32_t)src;
-          eq++;
-        }
+    // compare with the other 7 lanes of the group (DPP exchanges; this lane counts as equal)
+    uint32_t lt = 0, eq = 1, rep = lane;
+    {
+      uint32_t hc = 0, h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+      if constexpr (kW == 8) {
+        hc = g8_mirror(cls);
+        h0 = g8_mirror(k[0]);
+        h1 = g8_mirror(k[1]);
+        h2 = g8_mirror(k[2]);
+        h3 = g8_mirror(k[3]);
       }
+      auto member = [&](uint32_t src, uint32_t cj, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+        const uint64_t hj = ((uint64_t)a0 << 32) | a1, lj = ((uint64_t)a2 << 32) | a3;
+        if (cj == cls) {
+          lt += (hj < khi) || (hj == khi && lj < klo);
+          if (hj == khi && lj == klo) {
+            rep = min(rep, src);
+            eq++;
+          }
+        }
+      };
+#define BZG_G8(M) member(lane ^ (uint32_t)(M), g8_xor<M>(cls, hc), g8_xor<M>(k[0], h0), g8_xor<M>(k[1], h1), \
+                         g8_xor<M>(k[2], h2), g8_xor<M>(k[3], h3))
+      BZG_G8(1);
+      if constexpr (kW == 8) {
+        BZG_G8(2);
+        BZG_G8(3);
+        BZG_G8(4);
+        BZG_G8(5);
+        BZG_G8(6);
+        BZG_G8(7);
+      }
+#undef BZG_G8
     }
     if (!done) {
       pos += lt;
@@ -1285,7 +1368,8 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
               rank += q < p;
             }
           B.sa[g.start + pos[r] + rank] = v[r];
-          if (rank == 0) O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + pos[r], cnt, g.unit, grp_flags(0u, depth, 2u)};
+          const uint32_t ds = wave_append(O.n_deep, rank == 0);  // one atomic per wave
+          if (rank == 0) O.deep[ds] = Grp{g.start + pos[r], cnt, g.unit, grp_flags(0u, depth, 2u)};
         }
       break;
     }
@@ -1493,7 +1577,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
             if (!tn[r]) {  // last member of its run
               const uint32_t size = p - rsn[r] + 1;
               if (depth >= B.dwave) {  // still tied after B.dwave characters: doubling fallback
-                O.deep[atomicAdd(O.n_deep, 1u)] = Grp{g.start + rsn[r], size, g.unit, grp_flags(0u, depth, 2u)};
+                O.deep[wave_append(O.n_deep, true)] = Grp{g.start + rsn[r], size, g.unit, grp_flags(0u, depth, 2u)};
               } else {
                 atomicAdd(&cc[size_cls(size)], 1u);
                 E.rec[g.start / 2 + atomicAdd(&cc[7], 1u)] = (depth << 17) | (rsn[r] << 9) | size;
@@ -1780,6 +1864,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       return e ? (uint32_t)std::max(16, atoi(e)) : 256u;  // tuned: profiles/r02_dwave_sweep.txt
     }();
     B.dwave = dwave;
+    static const uint32_t dwave_tiny = [] {
+      const char* e = getenv("BZG_DWAVE_TINY");
+      return e ? (uint32_t)std::max(16, atoi(e)) : dwave;
+    }();
+    B.dwave_tiny = dwave_tiny;
   }
   // class lists: a class-c bucket holds more than kClsMax[c-1] rotations
   ClsLists C{};
@@ -1965,6 +2054,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       }
     }
     const size_t max_s2 = ccap[3] + ccap[4] + ccap[5];
+    Grp* tiny2 = ws.typed<Grp>("sort_tiny2", ccap[0]);
+    Grp* tiny8 = ws.typed<Grp>("sort_tiny8", ccap[0]);
     uint32_t* ccnt2 = ws.u32("sort_s2cnt", 6 * max_s2 + 16);
     uint32_t* scratch2 = ws.u32("sort_s2scan", scan_scratch_words(6 * max_s2 + 16) + 64);
     int s2_iters = 0;
@@ -1974,7 +2065,16 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         fprintf(stderr, "[bzg sort S2] iter %d: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", s2_iters,
                 ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5]);
       for (int c = 0; c < 6; c++) check_list(C.l[c], ncls[c], "S2", s2_iters, c);
-      if (ncls[0]) k_tiny<<<ceil_div(ncls[0], 8 * (kT / 64)), kT, 0, st>>>(C.l[0], ncls[0], B, O);
+      if (ncls[0]) {
+        HIP_OK(hipMemsetAsync(cnt + 32, 0, 8, st));
+        k_split_pairs<<<ceil_div(ncls[0], kT * kSplitPer), kT, 0, st>>>(C.l[0], ncls[0], tiny2, tiny8, cnt + 32);
+        HIP_OK(hipGetLastError());
+        uint32_t hn[2];
+        HIP_OK(hipMemcpyAsync(hn, cnt + 32, 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (hn[0]) k_tiny<2><<<ceil_div(hn[0], 32 * (kT / 64)), kT, 0, st>>>(tiny2, hn[0], B, O);
+        if (hn[1]) k_tiny<8><<<ceil_div(hn[1], 8 * (kT / 64)), kT, 0, st>>>(tiny8, hn[1], B, O);
+      }
       if (ncls[1]) k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
       if (ncls[2]) k_bsort<32, 1, 2, false><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O);
       HIP_OK(hipGetLastError());

@@ -32,6 +32,7 @@ struct SortBufs {
   const uint8_t* text;
   const Unit* units;
   uint32_t dwave;  // S2 gives a tied group to the doubling fallback (S3) at this depth
+  uint32_t dwave_tiny;  // the same for groups of <= 8 rotations (k_tiny)
 };
 
 // Largest g with P[g] <= x (P is an exclusive prefix, P[0] = 0).
