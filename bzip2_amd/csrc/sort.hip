@@ -192,14 +192,24 @@ __global__ void k_group_tiles(const Grp* __restrict__ L, uint32_t n, uint32_t* _
   if (g < n) cnt[g] = ceil_div(L[g].size, kDTile);
 }
 
-// TG[t] = the group of tile t (TP: exclusive scan of the groups' tile counts), so that a tile
-// finds its group with one load instead of a binary search over TP (a chain of dependent loads).
+// One record per S1 tile (TP: exclusive scan of the groups' tile counts): the tile's group,
+// its unit and its position, so that a tile reads one 48-byte record instead of a chain of
+// dependent loads (tile -> group -> unit; a binary search over TP before that).
+struct TileRec {
+  Grp g;
+  Unit u;
+  uint32_t gi;  // group index in the list
+  uint32_t k;   // tile index within the group
+  uint32_t pad[2];
+};
 __global__ void k_tile_owner(const Grp* __restrict__ L, uint32_t n, const uint32_t* __restrict__ TP,
-                             uint32_t* __restrict__ TG) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+                             const Unit* __restrict__ units, TileRec* __restrict__ TR) {
+  const uint32_t g = blockIdx.x;  // one wave per group, lanes over its tiles
   if (g >= n) return;
-  const uint32_t t0 = TP[g], c = ceil_div(L[g].size, kDTile);
-  for (uint32_t k = 0; k < c; k++) TG[t0 + k] = g;
+  const Grp gr = L[g];
+  const Unit u = units[gr.unit];
+  const uint32_t t0 = TP[g], c = ceil_div(gr.size, kDTile);
+  for (uint32_t k = threadIdx.x; k < c; k += blockDim.x) TR[t0 + k] = TileRec{gr, u, g, k, {0u, 0u}};
 }
 
 // LDS exchange among the lanes of one wave (LDS operations of a wave complete in order)
@@ -267,14 +277,13 @@ __device__ __forceinline__ uint32_t s1_next_cache(const Grp& gr) {
   return c ? c - 1 : 3u;
 }
 
-__global__ void __launch_bounds__(kT) k_s1_hist(const Grp* __restrict__ G, const uint32_t* __restrict__ TG,
-                                                const uint32_t* __restrict__ TP, SortBufs B, uint32_t* __restrict__ hist) {
+__global__ void __launch_bounds__(kT) k_s1_hist(const TileRec* __restrict__ TR, SortBufs B, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[256];
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t g = TG[t];
-  const Grp gr = G[g];
-  const Unit U = B.units[gr.unit];
-  const uint32_t lo = (t - TP[g]) * kDTile, hi = min(gr.size, lo + kDTile);
+  const TileRec tr = TR[t];
+  const Grp gr = tr.g;
+  const Unit U = tr.u;
+  const uint32_t lo = tr.k * kDTile, hi = min(gr.size, lo + kDTile);
   h[threadIdx.x] = 0;
   uint32_t vv[kPerT], kk[kPerT];
   s1_load<true>(B, gr, U, lo, hi, vv, kk);
@@ -334,8 +343,7 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
 // Scatter of one tile into the bucket order; the first tile of a group also emits the
 // group's buckets into the class lists (cscan: exclusive scan of ccnt).  The tile is first
 // reordered by bucket in LDS, so the global stores run along each bucket's range.
-__global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, const uint32_t* __restrict__ TG,
-                                                   const uint32_t* __restrict__ TP,
+__global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ TR,
                                                    SortBufs B, SortOut O, const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ tot, const uint32_t* __restrict__ cscan,
                                                    uint32_t nTot, ClsLists C) {
@@ -347,10 +355,11 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, co
   __shared__ uint32_t Lv[kDTile], Lk[kDTile];
   static_assert(kDTile == kPerT * kT, "one element per thread and round");
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t g = TG[t];
-  const Grp gr = G[g];
-  const Unit U = B.units[gr.unit];
-  const uint32_t lo = (t - TP[g]) * kDTile, hi = min(gr.size, lo + kDTile);
+  const TileRec tr = TR[t];
+  const uint32_t g = tr.gi;
+  const Grp gr = tr.g;
+  const Unit U = tr.u;
+  const uint32_t lo = tr.k * kDTile, hi = min(gr.size, lo + kDTile);
   const bool dst_alt = !(gr.flags & kGrpIdent) && !(gr.flags & kGrpAlt);
   uint32_t* dst = dst_alt ? B.sa2 : B.sa;
   uint32_t* dstk = dst_alt ? B.sk2 : B.sk;
@@ -404,7 +413,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const Grp* __restrict__ G, co
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
     if (i * kT + threadIdx.x < m && (single[kk[i] >> 24] & 1u)) emit_final(B, O, U, gr.unit, pos[i], vv[i], !dst_alt);
-  if (t != TP[g]) return;
+  if (tr.k != 0) return;
   // ---- bucket emission (digit order within the group)
   const uint32_t depth = grp_depth(gr) + 1;
   const uint32_t cl = bucket_cls(total, depth);
@@ -1897,7 +1906,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   const size_t max_ptiles = S / kSG + 64;
   const size_t max_tot = ccap[7] + max_ptiles;
   uint32_t* TP = ws.u32("sort_TP", max_tiles + 16);
-  uint32_t* TG = ws.u32("sort_TG", max_tiles + 16);
+  TileRec* TR = ws.typed<TileRec>("sort_TR", max_tiles + 16);
   uint32_t* hist = ws.u32("sort_hist", max_tiles * 256);
   uint32_t* tot = ws.u32("sort_tot", ccap[7] * 256);
   uint32_t* ccnt = ws.u32("sort_ccnt", kNCls * max_tot + 16);
@@ -1953,7 +1962,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_group_tiles<<<grid(n7), kT, 0, st>>>(cur7, n7, TP);
       HIP_OK(hipGetLastError());
       scan_u32(ScanOp::Sum, true, TP, TP, n7, cnt + 17, scratch, st);
-      k_tile_owner<<<grid(n7), kT, 0, st>>>(cur7, n7, TP, TG);
+      k_tile_owner<<<n7, 64, 0, st>>>(cur7, n7, TP, units, TR);
       HIP_OK(hipGetLastError());
     }
     if (n6) {
@@ -1982,7 +1991,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     if (n7) {
-      k_s1_hist<<<ntl, kT, 0, st>>>(cur7, TG, TP, B, hist);
+      k_s1_hist<<<ntl, kT, 0, st>>>(TR, B, hist);
       HIP_OK(hipGetLastError());
       k_s1_off<<<n7, kT, 0, st>>>(cur7, nTot, TP, hist, tot, ccnt, O.deep, O.n_deep);
       HIP_OK(hipGetLastError());
@@ -1996,7 +2005,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     Cp.l[7] = nxt7;
     Cp.base[6] = Cp.base[7] = 0;
     if (n7) {
-      k_s1_scatter<<<ntl, kT, 0, st>>>(cur7, TG, TP, B, O, hist, tot, ccnt, nTot, Cp);
+      k_s1_scatter<<<ntl, kT, 0, st>>>(TR, B, O, hist, tot, ccnt, nTot, Cp);
       HIP_OK(hipGetLastError());
       k_s1_single<<<n7, kT, 0, st>>>(cur7, B, tot);
       HIP_OK(hipGetLastError());
