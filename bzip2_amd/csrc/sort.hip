@@ -278,21 +278,26 @@ __device__ __forceinline__ uint32_t s1_next_cache(const Grp& gr) {
 }
 
 __global__ void __launch_bounds__(kT) k_s1_hist(const TileRec* __restrict__ TR, SortBufs B, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[256];
+  // 4 copies of every bin in consecutive words (lane & 3 picks one): lanes of a wave that
+  // count the same character (skewed text) hit 4 banks instead of queueing on one word
+  __shared__ uint32_t h[256 * 4];
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const TileRec tr = TR[t];
   const Grp gr = tr.g;
   const Unit U = tr.u;
   const uint32_t lo = tr.k * kDTile, hi = min(gr.size, lo + kDTile);
-  h[threadIdx.x] = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) h[q * kT + threadIdx.x] = 0;
   uint32_t vv[kPerT], kk[kPerT];
   s1_load<true>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
+  const uint32_t cp = threadIdx.x & 3u;
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[kk[i] >> 24], 1u);
+    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[(kk[i] >> 24) * 4 + cp], 1u);
   __syncthreads();
-  hist[(size_t)t * 256 + threadIdx.x] = h[threadIdx.x];
+  const uint4 c4 = reinterpret_cast<const uint4*>(h)[threadIdx.x];
+  hist[(size_t)t * 256 + threadIdx.x] = c4.x + c4.y + c4.z + c4.w;
 }
 
 __device__ __forceinline__ uint32_t bucket_cls(uint32_t total, uint32_t depth) {
