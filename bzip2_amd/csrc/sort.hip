@@ -352,7 +352,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
                                                    SortBufs B, SortOut O, const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ tot, const uint32_t* __restrict__ cscan,
                                                    uint32_t nTot, ClsLists C) {
-  __shared__ uint32_t cnt[256];
+  __shared__ uint32_t cnt[256 * 4];  // 4 bank-spread copies per bucket (see k_s1_hist)
   __shared__ uint32_t base[256];   // global slot of the bucket's first element - its LDS start
   __shared__ uint32_t single[256];
   __shared__ uint32_t wc[kT / 64][kNCls + 1];
@@ -371,7 +371,8 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   const uint32_t d = threadIdx.x;
   const uint32_t total = tot[(size_t)g * 256 + d];
   const uint32_t gbase = off[(size_t)t * 256 + d];
-  cnt[d] = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) cnt[q * kT + d] = 0;
   {  // bit 0: a bucket of one; bit 1: the bucket stays in S1 (needs its key caches)
     const uint32_t cl = bucket_cls(total, grp_depth(gr) + 1);
     single[d] = (total == 1 ? 1u : 0u) | (cl == 6 || cl == 7 ? 2u : 0u);
@@ -380,21 +381,24 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   s1_load<false>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
   uint32_t rk[kPerT];
+  const uint32_t cp = threadIdx.x & 3u;
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    if (lo + i * kT + threadIdx.x < hi) rk[i] = atomicAdd(&cnt[kk[i] >> 24], 1u);
+    if (lo + i * kT + threadIdx.x < hi) rk[i] = atomicAdd(&cnt[(kk[i] >> 24) * 4 + cp], 1u);
   __syncthreads();
-  {
-    const uint32_t c = cnt[d];
+  {  // bucket d's LDS start, and the start of each of its copies (any order within a bucket)
+    const uint4 c4 = reinterpret_cast<const uint4*>(cnt)[d];
+    const uint32_t c = c4.x + c4.y + c4.z + c4.w;
     const uint32_t lstart = block_incl_sum(c, sh, (uint32_t*)nullptr) - c;
-    cnt[d] = lstart;
+    reinterpret_cast<uint4*>(cnt)[d] =
+        make_uint4(lstart, lstart + c4.x, lstart + c4.x + c4.y, lstart + c4.x + c4.y + c4.z);
     base[d] = gbase - lstart;
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++) {
     if (lo + i * kT + threadIdx.x < hi) {
-      const uint32_t lp = cnt[kk[i] >> 24] + rk[i];
+      const uint32_t lp = cnt[(kk[i] >> 24) * 4 + cp] + rk[i];
       Lv[lp] = vv[i];
       Lk[lp] = kk[i];
     }
@@ -478,10 +482,12 @@ __global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, uint32_t* _
 #define BZG_TS 512
 #endif
 constexpr uint32_t kTS = BZG_TS, kPerTS = 2 * kSG / kTS;
+// (group, digit) bins keep kCp copies in consecutive words (thread & 1 picks one), as in k_s1_hist
+constexpr uint32_t kCp = 2;
 struct S1sLds {
   // (group, digit) bins: counts, then (in place) exclusive tile-relative bases; entry
   // ni * 256 = tile size, so a bin's total is the difference of neighbouring entries
-  uint32_t cur[kSGrp * 256 + 1];
+  uint32_t cur[kSGrp * 256 * kCp + 1];
   // per group: first slot, tile offset, flags, unit, and the unit's text offset, length,
   // first slot and copies
   uint32_t gstart[kSGrp], goff[kSGrp + 1], gfl[kSGrp], gunit[kSGrp], gtoff[kSGrp], glen[kSGrp], gsb[kSGrp], gk[kSGrp];
@@ -507,7 +513,7 @@ __device__ __forceinline__ uint32_t s1s_setup(S1sLds& S, const Grp* __restrict__
     S.gsb[threadIdx.x] = U.sbase;
     S.gk[threadIdx.x] = U.k;
   }
-  for (uint32_t i = threadIdx.x; i < ni * 256; i += kTS) S.cur[i] = 0;
+  for (uint32_t i = threadIdx.x; i < ni * 256 * kCp; i += kTS) S.cur[i] = 0;
   if (threadIdx.x <= (uint32_t)kNCls) S.cc[threadIdx.x] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -569,6 +575,7 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
   const uint32_t rounds = ceil_div(n, kTS);  // uniform
   const S1sOwner own(S, ni);
   const uint32_t lane = __lane_id();
+  const uint32_t cp = threadIdx.x & (kCp - 1);
   uint32_t vv[kPerTS], kk[kPerTS], jj[kPerTS], qq[kPerTS];
   // rotations (identity groups: the offset; slots of identity groups hold stale values,
   // loaded anyway so that no load sits behind a branch)
@@ -605,34 +612,34 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {
     if ((uint32_t)i >= rounds) break;
-    if (i * kTS + threadIdx.x < n) qq[i] = atomicAdd(&S.cur[jj[i] * 256 + (kk[i] >> 24)], 1u);
+    if (i * kTS + threadIdx.x < n) qq[i] = atomicAdd(&S.cur[(jj[i] * 256 + (kk[i] >> 24)) * kCp + cp], 1u);
   }
   __syncthreads();
   // tile-relative bin bases: exclusive scan over the (group, digit) bins, in place
   {
-    constexpr uint32_t kB = (kSGrp * 256 + kTS - 1) / kTS;
+    constexpr uint32_t kB = (kSGrp * 256 * kCp + kTS - 1) / kTS;
     uint32_t c[kB], sum = 0;
 #pragma unroll
     for (int q = 0; q < (int)kB; q++) {
       const uint32_t b = threadIdx.x * kB + q;
-      c[q] = b < ni * 256 ? S.cur[b] : 0u;
+      c[q] = b < ni * 256 * kCp ? S.cur[b] : 0u;
       sum += c[q];
     }
     uint32_t run = block_incl_sum(sum, S.sh, (uint32_t*)nullptr) - sum;
 #pragma unroll
     for (int q = 0; q < (int)kB; q++) {
       const uint32_t b = threadIdx.x * kB + q;
-      if (b < ni * 256) S.cur[b] = run;
+      if (b < ni * 256 * kCp) S.cur[b] = run;
       run += c[q];
     }
-    if (threadIdx.x == 0) S.cur[ni * 256] = n;
+    if (threadIdx.x == 0) S.cur[ni * 256 * kCp] = n;
   }
   __syncthreads();
   // bucket records (one LDS atomic per wave) and class counts
   uint32_t* trec = rec + P[first[t]] / 2;
   for (uint32_t b0 = 0; b0 < ni * 256; b0 += kTS) {
     const uint32_t b = b0 + threadIdx.x;
-    const uint32_t j = b >> 8, total = b < ni * 256 ? S.cur[b + 1] - S.cur[b] : 0u;
+    const uint32_t j = b >> 8, total = b < ni * 256 ? S.cur[(b + 1) * kCp] - S.cur[b * kCp] : 0u;
     const uint32_t cl = total < 2 ? 0xffu : bucket_cls(total, grp_depth(Grp{0, 0, 0, S.gfl[j]}) + 1);
     const uint64_t m = __ballot(cl != 0xffu);
     if (m == 0) continue;
@@ -640,7 +647,7 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
     if (lane == 0) base = atomicAdd(&nr, (uint32_t)__popcll(m));
     base = (uint32_t)__shfl((int)base, 0, 64);
     if (cl != 0xffu) {
-      trec[base + (uint32_t)__popcll(m & lanemask_lt())] = rec_pack(j, S.cur[b], total);
+      trec[base + (uint32_t)__popcll(m & lanemask_lt())] = rec_pack(j, S.cur[b * kCp], total);
       if (cl < (uint32_t)kNCls) atomicAdd(&S.cc[cl], 1u);
     }
   }
@@ -653,7 +660,7 @@ __global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, co
     if (i * kTS + threadIdx.x < n) {
       const uint32_t j = jj[i], fl = S.gfl[j];
       const uint32_t bin = j * 256 + (kk[i] >> 24);
-      const uint32_t x = S.cur[bin] + qq[i], total = S.cur[bin + 1] - S.cur[bin];
+      const uint32_t x = S.cur[bin * kCp + cp] + qq[i], total = S.cur[(bin + 1) * kCp] - S.cur[bin * kCp];
       const uint32_t v = vv[i];
       Lv[x] = v;
       const uint32_t slot = S.gstart[j] + x - S.goff[j];
