@@ -146,7 +146,7 @@ __global__ void k_init_tables(const uint32_t* __restrict__ nmtf_g, const uint32_
 struct CfLds {
   uint16_t chunk[kT * kGroupSize + 8];
   uint32_t lenp[2][kMaxAlpha];       // lengths of tables 0-2 / 3-5 in 10-bit fields
-  uint32_t rfreq[kNGroups][kMaxAlpha];
+  uint32_t rfreq[kNGroups][kMaxAlpha * 2];  // 2 bank-spread copies per counter (thread & 1)
   uint32_t sh[8];
 };
 
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
     S.lenp[1][v] = L[3 * kMaxAlpha + v] | ((uint32_t)L[4 * kMaxAlpha + v] << 10) | ((uint32_t)L[5 * kMaxAlpha + v] << 20);
   }
   if (!final)
-    for (int i = threadIdx.x; i < kNGroups * kMaxAlpha; i += kT) (&S.rfreq[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < kNGroups * kMaxAlpha * 2; i += kT) (&S.rfreq[0][0])[i] = 0;
   uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
   uint32_t mybits = 0;
   for (uint32_t ch = c0; ch < c1; ch++) {
@@ -218,12 +218,13 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
           f1 += v == 1;
           f2 += v == 2;
           f3 += v == 3;
-          if (v > 3) atomicAdd(&S.rfreq[bt][v], 1u);
+          if (v > 3) atomicAdd(&S.rfreq[bt][v * 2 + (threadIdx.x & 1u)], 1u);
         }
-        if (f0) atomicAdd(&S.rfreq[bt][0], f0);
-        if (f1) atomicAdd(&S.rfreq[bt][1], f1);
-        if (f2) atomicAdd(&S.rfreq[bt][2], f2);
-        if (f3) atomicAdd(&S.rfreq[bt][3], f3);
+        const uint32_t cp = threadIdx.x & 1u;
+        if (f0) atomicAdd(&S.rfreq[bt][0 + cp], f0);
+        if (f1) atomicAdd(&S.rfreq[bt][2 + cp], f1);
+        if (f2) atomicAdd(&S.rfreq[bt][4 + cp], f2);
+        if (f3) atomicAdd(&S.rfreq[bt][6 + cp], f3);
       }
     }
   }
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
   } else {
     uint32_t* rf = rf_g + (size_t)b * kNGroups * kMaxAlpha;
     for (int i = threadIdx.x; i < ng * kMaxAlpha; i += kT) {
-      const uint32_t v = (&S.rfreq[0][0])[i];
+      const uint32_t v = (&S.rfreq[0][0])[2 * i] + (&S.rfreq[0][0])[2 * i + 1];
       if (v) atomicAdd(&rf[i], v);
     }
   }

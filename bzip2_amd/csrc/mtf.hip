@@ -419,11 +419,13 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
                                                         const uint32_t* __restrict__ finalrun,
                                                         const uint32_t* __restrict__ mtf_off,
                                                         uint16_t* __restrict__ mtfv, uint32_t* __restrict__ freq) {
-  __shared__ uint32_t hist[kMaxAlpha];
+  // 4 bank-spread copies of every symbol counter (lane & 3 picks one): the ranks are skewed
+  // towards 1..3, so one copy made the lanes of a wave queue on a few LDS words
+  __shared__ uint32_t hist[kMaxAlpha * 4];
   // the chunk's symbols (<= kChunk ranks + carried-in and final runs + EOB), written out
   // coalesced once the wave has placed them
   __shared__ uint16_t stage[kEW][kChunk + 96];
-  for (int i = threadIdx.x; i < kMaxAlpha; i += 64 * kEW) hist[i] = 0;
+  for (int i = threadIdx.x; i < kMaxAlpha * 4; i += 64 * kEW) hist[i] = 0;
   __syncthreads();
   const uint32_t b = blockIdx.y, lane = __lane_id();
   uint16_t* st = stage[threadIdx.x >> 6];
@@ -518,7 +520,7 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
             first = false;
             zz = 0;
             out[o++] = (uint16_t)(rk[k] + 1);
-            atomicAdd(&hist[rk[k] + 1], 1u);
+            atomicAdd(&hist[(rk[k] + 1) * 4 + (lane & 3u)], 1u);
           }
         }
       }
@@ -526,17 +528,20 @@ __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restric
     if (tail) {
       put_run(fr);
       out[o++] = (uint16_t)eob;
-      atomicAdd(&hist[eob], 1u);
+      atomicAdd(&hist[eob * 4], 1u);
     }
-    if (runa) atomicAdd(&hist[0], runa);
-    if (runb) atomicAdd(&hist[1], runb);
+    if (runa) atomicAdd(&hist[0 * 4 + (lane & 3u)], runa);
+    if (runb) atomicAdd(&hist[1 * 4 + (lane & 3u)], runb);
     __builtin_amdgcn_wave_barrier();
     uint16_t* gout = mtfv + moff_b + coff_g;
     for (uint32_t i = lane; i < wtot; i += 64) gout[i] = st[i];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kMaxAlpha; i += 64 * kEW)
-    if (hist[i]) atomicAdd(&freq[(size_t)b * kMaxAlpha + i], hist[i]);
+  for (int i = threadIdx.x; i < kMaxAlpha; i += 64 * kEW) {
+    const uint4 c4 = reinterpret_cast<const uint4*>(hist)[i];
+    const uint32_t c = c4.x + c4.y + c4.z + c4.w;
+    if (c) atomicAdd(&freq[(size_t)b * kMaxAlpha + i], c);
+  }
 }
 
 }  // namespace
