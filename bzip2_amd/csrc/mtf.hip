@@ -120,70 +120,117 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
   siglen[r.gidx] = cnt;
 }
 
-// 2. list chaining, one wave per block; lane l holds list positions 4l..4l+3
-__global__ void __launch_bounds__(64) k_compose(const uint32_t* __restrict__ boff, const uint32_t* __restrict__ cbase,
-                                                const uint32_t* __restrict__ inuse, const uint8_t* __restrict__ sig,
-                                                const uint32_t* __restrict__ siglen, uint32_t* __restrict__ init) {
-  __shared__ uint8_t list[256];
-  __shared__ uint8_t nlist[256];
-  __shared__ uint32_t mem[8];
-  const uint32_t b = blockIdx.x, lane = threadIdx.x;
+// 2. list chaining.  list_{c+1} = sig(c) ++ (list_c - sig(c)) is a composition of maps of the
+// form F_s(L) = s ++ (L - s), and F_t(F_s(L)) = F_{t ++ (s - t)}(L): the chain is split into
+// kCW segments of chunks, one wave each.  Phase 1: every wave chains its segment from the
+// empty list (= the segment's combined signature).  Phase 2: wave 0 chains the kCW segment
+// signatures from the block's initial list (the in-use bytes ascending, compress.c:124-140),
+// giving each segment's first list.  Phase 3: every wave chains its segment again from that
+// list and publishes each chunk's initial list.  Critical path: about 2 nch / kCW + kCW steps
+// instead of nch.  A lane holds list positions 4l..4l+3.
+constexpr uint32_t kCW = 16;
+
+// list <- sig ++ (list - sig) for the list[0, len) of one wave; sw = this lane's 4 signature
+// bytes, sl the signature length.  Returns the new length.
+__device__ __forceinline__ uint32_t compose_step(uint8_t* list, uint8_t* nlist, uint32_t* mem, uint32_t len,
+                                                 uint32_t sl, uint32_t sw, uint32_t lane) {
+  if (lane < 8) mem[lane] = 0;
+  wave_sync();
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    if (lane * 4 + k < sl) {
+      const uint32_t s = (sw >> (8 * k)) & 0xffu;
+      atomicOr(&mem[s >> 5], 1u << (s & 31));
+      nlist[lane * 4 + k] = (uint8_t)s;
+    }
+  }
+  wave_sync();
+  uint32_t keep = 0;
+  uint8_t e[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t pos = lane * 4 + k;
+    e[k] = list[pos];
+    const bool valid = pos < len && !((mem[e[k] >> 5] >> (e[k] & 31)) & 1u);
+    keep |= (valid ? 1u : 0u) << k;
+  }
+  const uint32_t kc = __builtin_popcount(keep);
+  const uint32_t incl = wave_incl_sum(kc);
+  uint32_t p = sl + incl - kc;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if ((keep >> k) & 1u) nlist[p++] = e[k];
+  wave_sync();
+  reinterpret_cast<uint32_t*>(list)[lane] = reinterpret_cast<const uint32_t*>(nlist)[lane];
+  wave_sync();
+  return sl + (uint32_t)__shfl((int)incl, 63, 64);
+}
+
+__global__ void __launch_bounds__(64 * kCW) k_compose(const uint32_t* __restrict__ boff, const uint32_t* __restrict__ cbase,
+                                                      const uint32_t* __restrict__ inuse, const uint8_t* __restrict__ sig,
+                                                      const uint32_t* __restrict__ siglen, uint32_t* __restrict__ init) {
+  __shared__ uint8_t list[kCW][256];
+  __shared__ uint8_t nlist[kCW][256];
+  __shared__ uint32_t mem[kCW][8];
+  __shared__ uint8_t segsig[kCW][256];
+  __shared__ uint8_t start[kCW][256];
+  __shared__ uint32_t seglen[kCW];
+  const uint32_t b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t n = boff[b + 1] - boff[b];
   const uint32_t nch = ceil_div(n, kChunk);
-  // initial list: in-use bytes ascending
-  uint32_t nu = 0;
+  const uint32_t per = ceil_div(nch, kCW);
+  const uint32_t c0 = min(nch, w * per), c1 = min(nch, c0 + per);
+  const uint32_t gb = cbase[b];
+  auto chain = [&](bool publish, uint32_t len) {
+    // the next chunk's signature is loaded one step ahead
+    uint32_t sl_n = c0 < c1 ? siglen[gb + c0] : 0u;
+    uint32_t sw_n = c0 < c1 ? reinterpret_cast<const uint32_t*>(sig + (size_t)(gb + c0) * 256)[lane] : 0u;
+    for (uint32_t c = c0; c < c1; c++) {
+      const uint32_t g = gb + c;
+      const uint32_t sl = sl_n, sw = sw_n;
+      if (c + 1 < c1) {
+        sl_n = siglen[g + 1];
+        sw_n = reinterpret_cast<const uint32_t*>(sig + (size_t)(g + 1) * 256)[lane];
+      }
+      if (publish) reinterpret_cast<uint32_t*>(init + (size_t)g * 64)[lane] = reinterpret_cast<const uint32_t*>(list[w])[lane];
+      len = compose_step(list[w], nlist[w], mem[w], len, sl, sw, lane);
+    }
+    return len;
+  };
+  // phase 1: the segment's signature
   {
-    const uint32_t w = inuse[b * 8 + (lane >> 3)];  // lane covers bytes 4l..4l+3
-    uint32_t cnt = 0;
-    for (int k = 0; k < 4; k++) cnt += (w >> ((lane * 4 + k) & 31)) & 1u;
-    uint32_t incl = wave_incl_sum(cnt);
+    const uint32_t len = chain(false, 0u);
+    reinterpret_cast<uint32_t*>(segsig[w])[lane] = reinterpret_cast<const uint32_t*>(list[w])[lane];
+    if (lane == 0) seglen[w] = len;
+  }
+  // the block's initial list: in-use bytes ascending (every wave needs its length)
+  uint32_t nu = 0;
+  uint32_t wd = inuse[b * 8 + (lane >> 3)];  // lane covers bytes 4l..4l+3
+  uint32_t cnt = 0;
+  for (int k = 0; k < 4; k++) cnt += (wd >> ((lane * 4 + k) & 31)) & 1u;
+  const uint32_t incl = wave_incl_sum(cnt);
+  nu = (uint32_t)__shfl((int)incl, 63, 64);
+  __syncthreads();
+  // phase 2 (wave 0): each segment's first list
+  if (w == 0) {
     uint32_t p = incl - cnt;
     for (int k = 0; k < 4; k++) {
       const uint32_t byte = lane * 4 + k;
-      if ((w >> (byte & 31)) & 1u) list[p++] = (uint8_t)byte;
+      if ((wd >> (byte & 31)) & 1u) list[0][p++] = (uint8_t)byte;
     }
-    nu = __shfl(incl, 63, 64);
+    wave_sync();
+    uint32_t len = nu;
+    for (uint32_t s = 0; s < kCW; s++) {
+      reinterpret_cast<uint32_t*>(start[s])[lane] = reinterpret_cast<const uint32_t*>(list[0])[lane];
+      wave_sync();
+      len = compose_step(list[0], nlist[0], mem[0], len, seglen[s], reinterpret_cast<const uint32_t*>(segsig[s])[lane], lane);
+    }
   }
   __syncthreads();
-  // the next chunk's signature is loaded one step ahead (lane l: bytes 4l..4l+3)
-  uint32_t sl_n = nch ? siglen[cbase[b]] : 0u;
-  uint32_t sw_n = nch ? reinterpret_cast<const uint32_t*>(sig + (size_t)cbase[b] * 256)[lane] : 0u;
-  for (uint32_t c = 0; c < nch; c++) {
-    const uint32_t g = cbase[b] + c;
-    const uint32_t sl = sl_n, sw = sw_n;
-    if (c + 1 < nch) {
-      sl_n = siglen[g + 1];
-      sw_n = reinterpret_cast<const uint32_t*>(sig + (size_t)(g + 1) * 256)[lane];
-    }
-    // publish the initial list of chunk c
-    reinterpret_cast<uint32_t*>(init + (size_t)g * 64)[lane] = reinterpret_cast<const uint32_t*>(list)[lane];
-    if (lane < 8) mem[lane] = 0;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      if (lane * 4 + k < sl) {
-        const uint32_t s = (sw >> (8 * k)) & 0xffu;
-        atomicOr(&mem[s >> 5], 1u << (s & 31));
-        nlist[lane * 4 + k] = (uint8_t)s;
-      }
-    }
-    __syncthreads();
-    uint32_t keep = 0;
-    uint8_t e[4];
-    for (int k = 0; k < 4; k++) {
-      const uint32_t pos = lane * 4 + k;
-      e[k] = list[pos];
-      const bool valid = pos < nu && !((mem[e[k] >> 5] >> (e[k] & 31)) & 1u);
-      keep |= (valid ? 1u : 0u) << k;
-    }
-    const uint32_t kc = __builtin_popcount(keep);
-    uint32_t p = sl + wave_incl_sum(kc) - kc;
-    for (int k = 0; k < 4; k++)
-      if ((keep >> k) & 1u) nlist[p++] = e[k];
-    __syncthreads();
-    reinterpret_cast<uint32_t*>(list)[lane] = reinterpret_cast<const uint32_t*>(nlist)[lane];
-    __syncthreads();
-  }
+  // phase 3: publish every chunk's initial list
+  reinterpret_cast<uint32_t*>(list[w])[lane] = reinterpret_cast<const uint32_t*>(start[w])[lane];
+  wave_sync();
+  (void)chain(true, nu);
 }
 
 // 3. per-chunk MTF from the chunk's initial list, fused with the chunk's zero-run summary.
@@ -590,7 +637,7 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
   const dim3 g2(ceil_div(maxch, kT), nb);
   k_sig<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, sig, siglen);
   HIP_OK(hipGetLastError());
-  k_compose<<<nb, 64, 0, st>>>(r.boff, cbase, r.inuse, sig, siglen, init);
+  k_compose<<<nb, 64 * kCW, 0, st>>>(r.boff, cbase, r.inuse, sig, siglen, init);
   HIP_OK(hipGetLastError());
   k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, init, ranks, lead, trail, inner);
   HIP_OK(hipGetLastError());
