@@ -111,7 +111,10 @@ __device__ __forceinline__ int n_groups(uint32_t nmtf) {  // compress.c:266-270
 //         k_huff: BZ2_hbMakeCodeLengths for every (block, table), one wave each };
 //   k_cf (final mode): payload bits of every group under the final tables;
 //   k_final: canonical codes, selector MTF, table and header bit counts.
-constexpr uint32_t kCfSlices = 8;  // workgroups per block in k_cf
+#ifndef BZG_CF_SLICES
+#define BZG_CF_SLICES 8
+#endif
+constexpr uint32_t kCfSlices = BZG_CF_SLICES;  // workgroups per block in k_cf
 
 __global__ void k_init_tables(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ freq_g,
                               const uint32_t* __restrict__ ninuse, uint8_t* __restrict__ lens_g,
