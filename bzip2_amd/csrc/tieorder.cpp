@@ -1,5 +1,29 @@
 // tieorder.cpp -- origPtr of exactly periodic blocks.
 //
+// DERIVED WORK NOTICE: the exchange model below follows the B* substring sort and the
+// tandem-repeat / Larsson-Sadakane rank refinement of the reference's blocksort.c, which is
+// divsufsort:
+//
+//   divsufsort
+//   Copyright (c) 2003-2007 Yuta Mori All Rights Reserved.
+//
+//   Permission is hereby granted, free of charge, to any person obtaining a copy of this
+//   software and associated documentation files (the "Software"), to deal in the Software
+//   without restriction, including without limitation the rights to use, copy, modify,
+//   merge, publish, distribute, sublicense, and/or sell copies of the Software, and to
+//   permit persons to whom the Software is furnished to do so, subject to the following
+//   conditions:
+//
+//   The above copyright notice and this permission notice shall be included in all copies
+//   or substantial portions of the Software.
+//
+//   THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND, EXPRESS OR IMPLIED,
+//   INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY, FITNESS FOR A
+//   PARTICULAR PURPOSE AND NONINFRINGEMENT. IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT
+//   HOLDERS BE LIABLE FOR ANY CLAIM, DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF
+//   CONTRACT, TORT OR OTHERWISE, ARISING FROM, OUT OF OR IN CONNECTION WITH THE SOFTWARE
+//   OR THE USE OR OTHER DEALINGS IN THE SOFTWARE.
+//
 // A block T = w^k (w primitive, |w| = p, k >= 2) has k identical copies of every rotation.
 // The BWT does not depend on their order, but origPtr does: it is the slot of rotation 0
 // among its k copies, and the reference leaves that choice to the exchange sequence of its
