@@ -1,0 +1,26 @@
+// copyrank.h -- A5: which of the k identical copies of rotation 0 the reference ranks first
+// in a block w^k.  See copyrank.cpp for the
+// derivation; the one-B*-per-period closed form also runs on the device (origptr.hip).
+#pragma once
+#include <cstdint>
+
+namespace bzg {
+
+struct CopyRankFailure {};
+
+// B* structure of the cyclic root w (|w| = p >= 2, primitive): number of B* offsets q.
+int32_t root_bstar_count(const uint8_t* w, int32_t p);
+
+// Closed form for q == 1 (copyrank.cpp section 4); -1 when q != 1.
+int32_t copy_rank_single(const uint8_t* w, int32_t p, int32_t k);
+
+// Copy index r of rotation 0 of the block w^k (k >= 2, w primitive, |w| >= 2).
+int32_t copy_rank(const uint8_t* w, int32_t p, int32_t k);
+
+// Rank of rotation 0 among the p distinct rotations of w.
+int32_t root_rotation_rank(const uint8_t* w, int32_t p);
+
+// Smallest period p dividing n with t = t[0,p)^(n/p); n when aperiodic.
+int32_t primitive_period(const uint8_t* t, int32_t n);
+
+}  // namespace bzg

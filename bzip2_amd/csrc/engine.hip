@@ -14,7 +14,7 @@
 #include <thread>
 
 #include "../../include/bzg.h"
-#include "tieorder.h"
+#include "copyrank.h"
 #include "stages.h"
 
 #define BZ_OK 0
@@ -182,25 +182,18 @@ struct Engine {
     MtfResult m;
     uint32_t* origptr = ws.u32("origptr", nb + 2);
     SortStats ss;
-    std::vector<uint32_t> hboff(nb + 1), hper(nb);
+    std::vector<uint32_t> hboff(nb + 1), hper(nb), hbq(nb);
+    CopyRankJob a5;
     if (nb > 0) {
       HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, s));
       HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipMemcpyAsync(hbq.data(), r.bq, 4 * nb, hipMemcpyDeviceToHost, s));
       HIP_OK(hipStreamSynchronize(s));
       uint8_t* bwt = ws.u8("bwt", hboff[nb] + 16);
       uint32_t* rank0 = ws.u32("rank0", nb + 2);
+      copyrank_begin(r, hboff, hper, hbq, a5, s);  // host copy ranks, if any, overlap the sort
       sort_blocks(r, hboff, hper, bwt, rank0, &ss, s);
-      bool periodic = false;
-      for (uint32_t b = 0; b < nb; b++) periodic |= hper[b] != hboff[b + 1] - hboff[b];
-      if (periodic) {
-        std::vector<uint32_t> hr(nb);
-        HIP_OK(hipMemcpyAsync(hr.data(), rank0, 4 * nb, hipMemcpyDeviceToHost, s));
-        HIP_OK(hipStreamSynchronize(s));
-        resolve_origptrs(r.blk, hboff, hper, hr);  // periodic roots: reference tie rank (A5)
-        HIP_OK(hipMemcpyAsync(origptr, hr.data(), 4 * nb, hipMemcpyHostToDevice, s));
-      } else {  // every origPtr is the sorted rank of rotation 0
-        HIP_OK(hipMemcpyAsync(origptr, rank0, 4 * nb, hipMemcpyDeviceToDevice, s));
-      }
+      copyrank_finish(ws, r, rank0, origptr, a5, s);  // origPtr on the device (A5)
       HIP_OK(hipEventRecord(ev[2], s));
       mtf_stage(ws, r, bwt, nb, hboff[nb], m, s, &hboff);
       HIP_OK(hipEventRecord(ev[3], s));
@@ -459,7 +452,7 @@ static int guarded(F&& f) {
     return BZ_OUTBUFF_FULL;
   } catch (const HipFailure& x) {
     return x.err == hipErrorOutOfMemory ? BZ_MEM_ERROR : BZ_CONFIG_ERROR;
-  } catch (const ResolverFailure&) {
+  } catch (const CopyRankFailure&) {
     return BZ_CONFIG_ERROR;
   } catch (const std::bad_alloc&) {
     return BZ_MEM_ERROR;
@@ -1005,8 +998,15 @@ void bzg_release(void) {
 int32_t bzg_periodic_origptr(const uint8_t* block, int32_t n) {
   if (!block || n <= 0) return -1;
   try {
-    return periodic_origptr(block, n);
-  } catch (const ResolverFailure&) {
+    const int32_t p = primitive_period(block, n);
+    if (p == n) return -1;  // not periodic: the sort's rank is the origPtr
+    if (p == 1) return 0;   // one symbol: no B* rotation
+    const int32_t k = n / p;
+    const int32_t single = copy_rank_single(block, p, k);  // the device's closed form
+    return root_rotation_rank(block, p) * k + (single >= 0 ? single : copy_rank(block, p, k));
+  } catch (const CopyRankFailure&) {
+    return -1;
+  } catch (const std::bad_alloc&) {
     return -1;
   }
 }
@@ -1065,21 +1065,22 @@ int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, u
     HIP_OK(hipMemcpy(r.blk, blocks, total, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice));
     block_info_stage(e.ws, r, e.stream);
-    std::vector<uint32_t> hboff(offsets, offsets + nb + 1), hper(nb), hr(nb);
+    std::vector<uint32_t> hboff(offsets, offsets + nb + 1), hper(nb), hbq(nb);
     HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, e.stream));
+    HIP_OK(hipMemcpyAsync(hbq.data(), r.bq, 4 * nb, hipMemcpyDeviceToHost, e.stream));
     HIP_OK(hipStreamSynchronize(e.stream));
     uint8_t* bwt = e.ws.u8("bwt", total + 16);
     uint32_t* rank0 = e.ws.u32("rank0", nb + 2);
+    uint32_t* d_orig = e.ws.u32("origptr", nb + 2);
+    CopyRankJob a5;
+    copyrank_begin(r, hboff, hper, hbq, a5, e.stream);
     bwt_stage(e.ws, r, hboff, hper, bwt, rank0, nullptr, e.stream);
-    HIP_OK(hipMemcpyAsync(hr.data(), rank0, 4 * nb, hipMemcpyDeviceToHost, e.stream));
+    copyrank_finish(e.ws, r, rank0, d_orig, a5, e.stream);
+    HIP_OK(hipMemcpyAsync(origptr, d_orig, 4 * nb, hipMemcpyDeviceToHost, e.stream));
     HIP_OK(hipStreamSynchronize(e.stream));
-    resolve_origptrs(r.blk, hboff, hper, hr);
     HIP_OK(hipMemcpy(bwt_out, bwt, total, hipMemcpyDeviceToHost));
-    for (uint32_t b = 0; b < nb; b++) origptr[b] = (int32_t)hr[b];
     return BZ_OK;
   } catch (const HipFailure&) {
-    return BZ_CONFIG_ERROR;
-  } catch (const ResolverFailure&) {
     return BZ_CONFIG_ERROR;
   }
 }

@@ -743,6 +743,7 @@ void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st) {
   HIP_OK(hipGetLastError());
   k_period<<<B, kT, 0, st>>>(res.blk, res.boff, res.period);
   HIP_OK(hipGetLastError());
+  copyrank_count_stage(res, ws, st);
 }
 
 }  // namespace bzg

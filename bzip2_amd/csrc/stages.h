@@ -4,8 +4,10 @@
 // (sort.hip) -> MTF/RUNA-RUNB (mtf.hip) -> table optimisation, Huffman codes and bit
 // packing (code.hip).
 #pragma once
+#include <exception>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -56,6 +58,7 @@ struct Rle1Result {
   uint32_t* inuse = nullptr;    // 8 words per block
   uint32_t* ninuse = nullptr;
   uint32_t* period = nullptr;   // primitive period of each block
+  uint32_t* bq = nullptr;       // B* offsets of each periodic block's root (origptr.hip)
 };
 void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool final_batch,
                 bool tail_merge, Rle1Result& res, hipStream_t st);
@@ -70,6 +73,22 @@ void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t s
 void seg_walk_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, uint32_t fill_in,
                     bool final_region, std::vector<uint64_t>& cuts, uint64_t& last_chunk, uint32_t& last_fill,
                     hipStream_t st);
+
+// ---- stage A5 (origptr.hip) ----------------------------------------------------------
+// B* offsets per periodic root (part of block_info_stage); the host copy rank of the roots
+// with more than one (started before the sort, overlapping it); origptr after the sort.
+struct CopyRankJob {
+  std::vector<int32_t> r;
+  std::vector<uint8_t> roots;
+  std::thread th;
+  std::exception_ptr err;
+  ~CopyRankJob();
+};
+void copyrank_count_stage(Rle1Result& r, Workspace& ws, hipStream_t st);
+void copyrank_begin(const Rle1Result& r, const std::vector<uint32_t>& hboff, const std::vector<uint32_t>& hper,
+                    const std::vector<uint32_t>& hbq, CopyRankJob& job, hipStream_t st);
+void copyrank_finish(Workspace& ws, const Rle1Result& r, const uint32_t* rank0, uint32_t* origptr, CopyRankJob& job,
+                     hipStream_t st);
 
 // ---- stage A4 ------------------------------------------------------------------------
 // Sorts the rotations of every block (of its primitive root when periodic) and writes the

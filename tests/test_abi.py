@@ -111,8 +111,9 @@ def test_decoder_streaming_small_chunks(lib):
 
 
 def test_periodic_resolver_matches_reference(lib):
-    """A5: origPtr of exactly periodic blocks (bzip2_amd/csrc/tieorder.cpp) against the
-    reference build: the SURVEY.md 8a KATs and random periodic blocks."""
+    """A5: origPtr of exactly periodic blocks (bzip2_amd/csrc/copyrank.cpp, with the closed
+    form the device uses for one B* per period) against the reference build: the SURVEY.md 8a
+    KATs and random periodic blocks."""
     from tests import oracles as O
     if not O.has_ref():
         pytest.skip("oracle/_ref not built")
@@ -154,6 +155,34 @@ def test_periodic_origptr_fuzz(lib):
             k = rng.randint(2, 180000)
         blk = w * min(k, 900000 // len(w))
         assert B.periodic_origptr(blk) == O.ref_blocksort(blk)[1], (w, len(blk) // len(w))
+
+
+def test_periodic_origptr_fuzz_wide(lib):
+    """A5 copy-rank model on roots the short fuzz rarely draws: text-like roots up to 3,000
+    bytes, dense binary/ternary roots with hundreds of B* offsets (the rank stage runs out of
+    budget and finishes by doubling), near-periodic roots (classes with equal B* substrings),
+    up to full 900 kB blocks."""
+    from tests import datagen, oracles as O
+    if not O.has_ref():
+        pytest.skip("oracle/_ref not built")
+    import random
+    rng = random.Random(31337)
+    txt = datagen.text(100_000, 77)
+    for _ in range(160):
+        mode = rng.random()
+        if mode < 0.35:
+            s = rng.randrange(0, len(txt) - 3000)
+            w = txt[s:s + rng.randint(2, 3000)]
+        elif mode < 0.7:
+            w = bytes(rng.randrange(rng.choice([2, 3])) for _ in range(rng.randint(8, 400)))
+        else:
+            u = bytes(rng.randrange(4) for _ in range(rng.randint(1, 8)))
+            w = u * rng.randint(2, 30) + bytes([rng.randrange(4)])
+        k = rng.randint(2, max(2, 900_000 // len(w)))
+        blk = (w * k)[:900_000]
+        if len(set(blk)) == 1 or len(blk) < 2 * len(w):
+            continue
+        assert B.periodic_origptr(blk) == O.ref_blocksort(blk)[1], (len(w), w[:24], len(blk) // len(w))
 
 
 def _libc():

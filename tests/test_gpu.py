@@ -159,6 +159,63 @@ def test_bwt_matches_oracle(case):
         assert orig[b] == o, (case, b, len(blk))
 
 
+def _periodic_blocks(seed):
+    """Exactly periodic blocks w^k of every A5 regime: one B* per period (device closed form;
+    single-byte runs after RLE1, k around the 1024-item radix block and the 8-item limits),
+    several B* per period (host model: short and long roots, dense small alphabets, text)."""
+    rng = random.Random(seed)
+    parts = []
+    for c in (0x00, 0x61, 0xFB, 0xFF):
+        parts.append(bytes([c] * 4 + [0xFB]) * rng.choice([2, 9, 1025, 1026, 1027, 19997, 179997]))
+    for w, k in ((b"ab", 4096), (b"abc", 17), (b"abc", 1026), (b"aab", 300), (b"abcabcabd", 11109),
+                 (b"bababac", 4096)):
+        parts.append(w * k)
+    for _ in range(40):
+        mode = rng.random()
+        if mode < 0.4:
+            w = bytes(rng.randrange(rng.choice([2, 3, 4, 256])) for _ in range(rng.randint(2, 12)))
+        elif mode < 0.7:
+            w = bytes(rng.randrange(rng.choice([2, 3])) for _ in range(rng.randint(8, 300)))
+        else:
+            w = datagen.text(rng.randint(20, 3000), rng.randrange(1000))
+        k = rng.randint(2, max(2, min(60_000, 900_000 // len(w))))
+        if len(set(w)) > 1:
+            parts.append(w * k)
+    offs = [0]
+    for p_ in parts:
+        offs.append(offs[-1] + len(p_))
+    return b"".join(parts), offs
+
+
+def test_periodic_blocks_origptr_vs_reference():
+    """A5 on the device (origptr.hip) and the host copy-rank model (copyrank.cpp) through the
+    stage ABI: every periodic block's origPtr and last column against the reference build."""
+    if not O.has_ref():
+        pytest.skip("needs oracle/_ref")
+    blocks, offs = _periodic_blocks(42)
+    bwt, orig = gpu_bwt(blocks, offs)
+    for b in range(len(offs) - 1):
+        blk = blocks[offs[b]:offs[b + 1]]
+        want_l, want_o = O.ref_blocksort(blk)
+        assert orig[b] == want_o, (b, blk[:16], len(blk))
+        assert bwt[offs[b]:offs[b + 1]] == want_l, (b, len(blk))
+
+
+def test_periodic_blocks_stream_vs_reference():
+    """Whole streams made of exactly periodic blocks (|w| divides the -1 block size 99,981):
+    several roots per stream, RLE1 single-byte blocks included."""
+    if not O.has_ref():
+        pytest.skip("needs oracle/_ref")
+    rng = random.Random(7)
+    segs = [bytes([0x61]) * 450_000]
+    for ln in (3, 7, 9, 21, 23, 27, 63, 69, 161, 189, 207):
+        w = bytes(rng.randrange(rng.choice([2, 3, 26])) for _ in range(ln))
+        if len(set(w)) > 1:
+            segs.append(w * (99_981 // ln) * 2)
+    data = b"".join(segs)
+    assert B.buff_to_buff_compress(data, 1) == O.ref_compress(data, 1)
+
+
 def _long_repeat_blocks():
     """Aperiodic blocks with long repeats: deep string-tile groups (kDWave), deep S1 buckets
     (kDBig) and big radix-round groups all end in the doubling fallback."""
