@@ -390,19 +390,28 @@ __global__ void __launch_bounds__(kT) k_final(const uint32_t* __restrict__ nmtf_
 }
 
 // Bit offsets of every block, the combined CRC, the trailer position.
+// Bit offset of every block and the running combined CRC (compress.c:826-828), continuing
+// from the previous part of the batch: chain[0] = start bit, chain[1] = combined CRC in; the
+// part's end replaces them (parts are chained in stream order on one stream).
 __global__ void k_offsets(const uint32_t* __restrict__ info, const uint32_t* __restrict__ bcrc, uint32_t nb,
-                          uint64_t start_bit, uint32_t comb_in, uint64_t* __restrict__ boffbits,
-                          uint64_t* __restrict__ out_total, uint32_t* __restrict__ comb_out) {
+                          uint64_t* __restrict__ chain, uint64_t* __restrict__ boffbits) {
   if (threadIdx.x != 0) return;
-  uint64_t pos = start_bit;
-  uint32_t comb = comb_in;
+  uint64_t pos = chain[0];
+  uint32_t comb = (uint32_t)chain[1];
   for (uint32_t b = 0; b < nb; b++) {
     boffbits[b] = pos;
     pos += info[(size_t)b * 8 + 3];
     comb = ((comb << 1) | (comb >> 31)) ^ bcrc[b];
   }
-  *out_total = pos;
-  *comb_out = comb;
+  chain[0] = pos;
+  chain[1] = comb;
+}
+
+__global__ void k_chain_init(uint64_t* __restrict__ chain, uint64_t start_bit, uint32_t comb) {
+  if (threadIdx.x == 0) {
+    chain[0] = start_bit;
+    chain[1] = comb;
+  }
 }
 
 // MSB-first bit writer ORing big-endian 32-bit words into a zeroed buffer.
@@ -619,7 +628,10 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
 
 // Stream header ("BZh" + level) and/or trailer (0x177245385090 + combined CRC).
 __global__ void k_frame(uint32_t* __restrict__ out, int header, uint64_t hdr_bit, int level, int trailer,
-                        const uint64_t* __restrict__ tpos, const uint32_t* __restrict__ comb) {
+                        const uint64_t* __restrict__ chain) {
+  const uint64_t* tpos = chain;
+  const uint32_t comb_v = (uint32_t)chain[1];
+  const uint32_t* comb = &comb_v;
   if (threadIdx.x != 0) return;
   if (header) {
     BitWriter w(out, hdr_bit);
@@ -640,55 +652,64 @@ __global__ void k_frame(uint32_t* __restrict__ out, int header, uint64_t hdr_bit
 
 }  // namespace
 
-uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, const uint32_t* origptr, uint32_t nb,
-                    int level, bool final_batch, StreamCarry& carry, uint8_t* out, uint64_t out_cap, hipStream_t st) {
+void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_t nb, CodeTables& t, hipStream_t st) {
   const size_t nbx = std::max<uint32_t>(nb, 1);
-  uint8_t* lens = ws.u8("code_lens", nbx * kNGroups * kMaxAlpha);
-  uint32_t* codes = ws.u32("code_codes", nbx * kNGroups * kMaxAlpha);
-  uint8_t* sel = ws.u8("code_sel", nbx * kMaxSelectors);
-  uint8_t* selmtf = ws.u8("code_selmtf", nbx * kMaxSelectors);
-  uint16_t* gbits = ws.u16("code_gbits", nbx * kMaxSelectors);
-  uint32_t* info = ws.u32("code_info", nbx * 8);
-  uint64_t* bbits = ws.typed<uint64_t>("code_bbits", nbx + 2);
-  uint32_t* comb = ws.u32("code_comb", 4);
+  t.lens = ws.u8("code_lens", nbx * kNGroups * kMaxAlpha);
+  t.codes = ws.u32("code_codes", nbx * kNGroups * kMaxAlpha);
+  t.sel = ws.u8("code_sel", nbx * kMaxSelectors);
+  t.selmtf = ws.u8("code_selmtf", nbx * kMaxSelectors);
+  t.gbits = ws.u16("code_gbits", nbx * kMaxSelectors);
+  t.info = ws.u32("code_info", nbx * 8);
+  t.bbits = ws.typed<uint64_t>("code_bbits", nbx + 2);
   uint32_t* rf = ws.u32("code_rf", nbx * kNGroups * kMaxAlpha);
-  if (nb > 0) {
-    HIP_OK(hipMemsetAsync(info, 0, nbx * 8 * 4, st));
-    k_init_tables<<<nb, 64, 0, st>>>(m.nmtf, m.freq, r.ninuse, lens, rf);
+  if (nb == 0) return;
+  HIP_OK(hipMemsetAsync(t.info, 0, nbx * 8 * 4, st));
+  k_init_tables<<<nb, 64, 0, st>>>(m.nmtf, m.freq, r.ninuse, t.lens, rf);
+  HIP_OK(hipGetLastError());
+  for (int it = 0; it < kIters; it++) {
+    k_cf<<<dim3(kCfSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 0);
     HIP_OK(hipGetLastError());
-    for (int it = 0; it < kIters; it++) {
-      k_cf<<<dim3(kCfSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, lens, sel, rf, gbits, info, 0);
-      HIP_OK(hipGetLastError());
-      k_huff<<<nb * kNGroups, 64, 0, st>>>(m.nmtf, r.ninuse, rf, lens);
-      HIP_OK(hipGetLastError());
-    }
-    k_cf<<<dim3(kCfSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, lens, sel, rf, gbits, info, 1);
-    HIP_OK(hipGetLastError());
-    k_final<<<nb, kT, 0, st>>>(m.nmtf, r.ninuse, r.inuse, lens, codes, sel, selmtf, info);
+    k_huff<<<nb * kNGroups, 64, 0, st>>>(m.nmtf, r.ninuse, rf, t.lens);
     HIP_OK(hipGetLastError());
   }
+  k_cf<<<dim3(kCfSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 1);
+  HIP_OK(hipGetLastError());
+  k_final<<<nb, kT, 0, st>>>(m.nmtf, r.ninuse, r.inuse, t.lens, t.codes, t.sel, t.selmtf, t.info);
+  HIP_OK(hipGetLastError());
+}
+
+uint64_t code_emit(Workspace& ws, const std::vector<CodePart>& parts, int level, bool final_batch, StreamCarry& carry,
+                   uint8_t* out, uint64_t out_cap, hipStream_t st) {
+  uint64_t* chain = ws.typed<uint64_t>("code_chain", 4);
   const bool header = !carry.header_done;
   const uint64_t start_bit = carry.carry_bits + (header ? 32 : 0);
-  k_offsets<<<1, 64, 0, st>>>(info, r.bcrc, nb, start_bit, carry.combined_crc, bbits, bbits + nbx, comb);
+  k_chain_init<<<1, 64, 0, st>>>(chain, start_bit, carry.combined_crc);
   HIP_OK(hipGetLastError());
-  uint64_t total_bits;
-  uint32_t comb_h;
-  HIP_OK(hipMemcpyAsync(&total_bits, bbits + nbx, 8, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(&comb_h, comb, 4, hipMemcpyDeviceToHost, st));
+  for (const CodePart& p : parts) {
+    if (p.nb == 0) continue;
+    k_offsets<<<1, 64, 0, st>>>(p.t->info, p.r->bcrc, p.nb, chain, p.t->bbits);
+    HIP_OK(hipGetLastError());
+  }
+  uint64_t hch[2];
+  HIP_OK(hipMemcpyAsync(hch, chain, 16, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
+  const uint64_t total_bits = hch[0];
+  const uint32_t comb_h = (uint32_t)hch[1];
   const uint64_t end_bits = total_bits + (final_batch ? 80 : 0);
   const uint64_t need = ceil_div64(end_bits, 32) * 4 + 8;
   if (need > out_cap) throw OutBuffFull{};
   HIP_OK(hipMemsetAsync(out, 0, need, st));
   if (carry.carry_bits) HIP_OK(hipMemcpyAsync(out, &carry.carry_byte, 1, hipMemcpyHostToDevice, st));
-  if (nb > 0) {
-    k_pack<<<dim3(kPackSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, r.inuse, r.bcrc, origptr, lens, codes, sel, selmtf, gbits, info,
-                              bbits, (uint32_t*)out);
+  for (const CodePart& p : parts) {
+    if (p.nb == 0) continue;
+    const CodeTables& t = *p.t;
+    k_pack<<<dim3(kPackSlices, p.nb), kT, 0, st>>>(p.m->mtfv, p.m->mtf_off, p.m->nmtf, p.r->inuse, p.r->bcrc, p.origptr,
+                                                 t.lens, t.codes, t.sel, t.selmtf, t.gbits, t.info, t.bbits,
+                                                 (uint32_t*)out);
     HIP_OK(hipGetLastError());
   }
   if (header || final_batch) {
-    k_frame<<<1, 64, 0, st>>>((uint32_t*)out, header ? 1 : 0, carry.carry_bits, level, final_batch ? 1 : 0,
-                              bbits + nbx, comb);
+    k_frame<<<1, 64, 0, st>>>((uint32_t*)out, header ? 1 : 0, carry.carry_bits, level, final_batch ? 1 : 0, chain);
     HIP_OK(hipGetLastError());
   }
   carry.header_done = true;
@@ -707,6 +728,14 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
     carry.carry_byte = 0;
   }
   return full;
+}
+
+uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, const uint32_t* origptr, uint32_t nb,
+                    int level, bool final_batch, StreamCarry& carry, uint8_t* out, uint64_t out_cap, hipStream_t st) {
+  CodeTables t;
+  code_tables(ws, r, m, nb, t, st);
+  std::vector<CodePart> parts{CodePart{&r, &m, &t, origptr, nb}};
+  return code_emit(ws, parts, level, final_batch, carry, out, out_cap, st);
 }
 
 void code_lengths_test(const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len, uint8_t* d_lens,

@@ -10,6 +10,7 @@
 #include <vector>
 #include <cstring>
 #include <exception>
+#include <future>
 #include <mutex>
 #include <thread>
 
@@ -28,11 +29,26 @@ namespace bzg {
 // ---------------------------------------------------------------- workspace
 Workspace::~Workspace() { release_all(); }
 
+void Workspace::drop(Buf& b) {
+  if (!b.p) return;
+  if (b.async)
+    (void)hipFreeAsync(b.p, stream_);
+  else
+    (void)hipFree(b.p);
+  total_ -= b.bytes;
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
 void Workspace::release_all() {
-  for (auto& kv : bufs_)
-    if (kv.second.p) (void)hipFree(kv.second.p);
+  bool any_async = false;
+  for (auto& kv : bufs_) {
+    any_async |= kv.second.async && kv.second.p;
+    drop(kv.second);
+  }
   bufs_.clear();
   total_ = 0;
+  if (any_async) (void)hipStreamSynchronize(stream_);
   if (crc_) (void)hipFree(crc_);
   if (xp2_) (void)hipFree(xp2_);
   crc_ = xp2_ = nullptr;
@@ -42,21 +58,25 @@ void* Workspace::get(const std::string& name, size_t bytes) {
   bytes = std::max<size_t>(bytes, 64);
   Buf& b = bufs_[name];
   if (b.bytes >= bytes) return b.p;
+  static const bool sync_free = getenv("BZG_WS_SYNC_FREE") != nullptr;
+  const bool async = stream_ != nullptr && !sync_free;
   if (b.p) {
-    HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipFree(b.p));
-    total_ -= b.bytes;
-    b.p = nullptr;
-    b.bytes = 0;
+    // the old buffer may still be read by work queued on this workspace's stream: an async
+    // free is ordered after it; a synchronous one waits for that stream only
+    if (!b.async && stream_) HIP_OK(hipStreamSynchronize(stream_));
+    else if (!b.async) HIP_OK(hipDeviceSynchronize());
+    drop(b);
   }
   const size_t grow = bytes + bytes / 8;  // headroom so small growth does not realloc
   void* p = nullptr;
-  if (hipMalloc(&p, grow) != hipSuccess) {
+  const hipError_t e = async ? hipMallocAsync(&p, grow, stream_) : hipMalloc(&p, grow);
+  if (e != hipSuccess) {
     (void)hipGetLastError();  // clear the sticky error of the failed allocation
     throw HipFailure(hipErrorOutOfMemory);
   }
   b.p = p;
   b.bytes = grow;
+  b.async = async;
   total_ += grow;
   return b.p;
 }
@@ -102,88 +122,85 @@ const uint32_t* Workspace::xpow2_table() {
 // Streams of several host threads therefore run on separate HIP streams and device buffers,
 // as the reference keeps all compression state per bz_stream (bzlib.c:144-207).
 struct Engine {
+  static constexpr int kSortStreams = 3;
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // the second half of a batch's block sort
+  hipStream_t sstream[kSortStreams] = {};  // block sorts of the batch's parts
   Workspace ws;
-  Workspace ws2;
+  std::vector<std::unique_ptr<Workspace>> pws;  // one per part of a batch
+  std::vector<hipEvent_t> psorted;              // per part: its sort is done
   hipEvent_t ev[6];
-  hipEvent_t ev2;
+  hipEvent_t ev_rle;
 
   explicit Engine(int dev) : device(dev) {
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    for (auto& x : sstream) HIP_OK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     for (auto& e : ev) HIP_OK(hipEventCreate(&e));
-    HIP_OK(hipEventCreateWithFlags(&ev2, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_rle, hipEventDisableTiming));
+    ws.set_stream(stream);
   }
 
-  // The block sort of a batch.  Large batches are sorted as two halves of their blocks on two
-  // streams, each driven by its own host thread and workspace: the sorter's host
-  // synchronisations (list sizes between passes) and its narrow late passes then overlap
-  // with the other half's kernels.
-  void sort_blocks(const Rle1Result& r, const std::vector<uint32_t>& hboff, const std::vector<uint32_t>& hper,
-                   uint8_t* bwt, uint32_t* rank0, SortStats* ss, hipStream_t s) {
-    const uint32_t nb = r.nblocks;
-    static const bool one_stream = getenv("BZG_ONE_STREAM") != nullptr;  // per-kernel profiling
-    if (nb < 64 || one_stream) {
-      bwt_stage(ws, r, hboff, hper, bwt, rank0, ss, s);
-      return;
+  void release_idle() {
+    ws.release_all();
+    for (auto& w : pws) w->release_all();
+  }
+
+  // One part of a batch: consecutive blocks [b0, b1) with their own device view (block
+  // offsets relative to the part), workspace and results.
+  struct Part {
+    uint32_t b0 = 0, b1 = 0;
+    Rle1Result r;
+    std::vector<uint32_t> hboff, hper, hbq;
+    Workspace* w = nullptr;
+    CopyRankJob a5;
+    SortStats ss;
+    MtfResult m;
+    CodeTables t;
+    float sort_ms = 0;
+  };
+
+  Workspace* part_ws(size_t p) {
+    while (pws.size() <= p) pws.emplace_back(new Workspace());
+    while (psorted.size() <= p) {
+      hipEvent_t e;
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      psorted.push_back(e);
     }
-    const uint32_t mid = nb / 2;
-    Rle1Result ra = r, rb = r;
-    ra.nblocks = mid;
-    rb.nblocks = nb - mid;
-    rb.blk = r.blk + hboff[mid];
-    std::vector<uint32_t> ha(hboff.begin(), hboff.begin() + mid + 1), pa(hper.begin(), hper.begin() + mid);
-    std::vector<uint32_t> hb(hboff.begin() + mid, hboff.end()), pb(hper.begin() + mid, hper.end());
-    for (auto& x : hb) x -= hboff[mid];
-    HIP_OK(hipEventRecord(ev2, s));  // the second stream starts after this batch's RLE1
-    HIP_OK(hipStreamWaitEvent(stream2, ev2, 0));
-    SortStats sb;
-    std::exception_ptr err;
-    const int dev = device;
-    std::thread th([&] {
-      try {
-        HIP_OK(hipSetDevice(dev));  // the current device is per host thread
-        bwt_stage(ws2, rb, hb, pb, bwt + hboff[mid], rank0 + mid, &sb, stream2);
-      } catch (...) {
-        err = std::current_exception();
-      }
-    });
-    try {
-      bwt_stage(ws, ra, ha, pa, bwt, rank0, ss, s);
-    } catch (...) {
-      th.join();
-      throw;
-    }
-    th.join();
-    if (err) std::rethrow_exception(err);
-    HIP_OK(hipEventRecord(ev2, stream2));
-    HIP_OK(hipStreamWaitEvent(s, ev2, 0));
-    if (ss) {
-      ss->iterations = std::max(ss->iterations, sb.iterations);
-      ss->unsorted_elems += sb.unsorted_elems;
-      ss->s2_iters = std::max(ss->s2_iters, sb.s2_iters);
-    }
+    return pws[p].get();
+  }
+
+  // Parts per batch and concurrent sort streams (BZG_PARTS / BZG_SORT_STREAMS).  Batches of
+  // fewer than 64 blocks are one part on one stream.
+  static int cfg(const char* name, int dflt, int lo, int hi) {
+    const char* e = getenv(name);
+    return std::min(hi, std::max(lo, e ? atoi(e) : dflt));
   }
 
   // Compress one batch.  Throws HipFailure on device errors, OutBuffFull when out_cap is short.
+  //
+  // The blocks are cut into parts.  Each part is sorted on one of the sort streams by its own
+  // host thread (the sorter synchronises with the host between passes, so several parts keep
+  // the device busy); as soon as a part's sort is done the calling thread queues its origPtr,
+  // MTF and table optimisation on the main stream, where they overlap the sorts of the later
+  // parts.  The bit offsets and the packing of all parts follow in block order.
   void batch(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
              uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
     const int level = st->level;
     const bool end_seg = flags & BZG_FLAG_END_SEGMENT;
     const bool tail_merge = (flags & BZG_FLAG_TAIL_MERGE) && end_seg;
     const bool trailer = (flags & BZG_FLAG_TRAILER) && end_seg;
+    ws.set_stream(s);
     HIP_OK(hipEventRecord(ev[0], s));
     Rle1Result r;
     rle1_stage(ws, d_in, n, level, end_seg, tail_merge, r, s);
     HIP_OK(hipEventRecord(ev[1], s));
     const uint32_t nb = r.nblocks;
-    MtfResult m;
     uint32_t* origptr = ws.u32("origptr", nb + 2);
-    SortStats ss;
     std::vector<uint32_t> hboff(nb + 1), hper(nb), hbq(nb);
-    CopyRankJob a5;
+    std::unique_ptr<Part[]> parts;
+    uint32_t K = 0, nparts = 0;
+    float mtf_ms = 0, tab_ms = 0, last_post = 0;
+    uint64_t sort_iters = 0, sort_unsorted = 0;
     if (nb > 0) {
       HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, s));
       HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, s));
@@ -191,22 +208,153 @@ struct Engine {
       HIP_OK(hipStreamSynchronize(s));
       uint8_t* bwt = ws.u8("bwt", hboff[nb] + 16);
       uint32_t* rank0 = ws.u32("rank0", nb + 2);
-      copyrank_begin(r, hboff, hper, hbq, a5, s);  // host copy ranks, if any, overlap the sort
-      sort_blocks(r, hboff, hper, bwt, rank0, &ss, s);
-      copyrank_finish(ws, r, rank0, origptr, a5, s);  // origPtr on the device (A5)
-      HIP_OK(hipEventRecord(ev[2], s));
-      mtf_stage(ws, r, bwt, nb, hboff[nb], m, s, &hboff);
-      HIP_OK(hipEventRecord(ev[3], s));
-    } else {
-      HIP_OK(hipEventRecord(ev[2], s));
-      HIP_OK(hipEventRecord(ev[3], s));
+      static const bool one_stream = getenv("BZG_ONE_STREAM") != nullptr;  // per-kernel profiling
+      const int want = nb < 64 || one_stream ? 1 : cfg("BZG_PARTS", 2, 1, 16);
+      K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)want, nb / 16));
+      const int S = nb < 64 || one_stream ? 1 : std::min<int>((int)K, cfg("BZG_SORT_STREAMS", 2, 1, kSortStreams));
+      parts.reset(new Part[K]);
+      nparts = K;
+      for (uint32_t p = 0; p < K; p++) {
+        Part& P = parts[p];
+        P.b0 = (uint32_t)((uint64_t)nb * p / K);
+        P.b1 = (uint32_t)((uint64_t)nb * (p + 1) / K);
+        const uint32_t pn = P.b1 - P.b0, base = hboff[P.b0];
+        P.w = part_ws(p);
+        P.w->set_stream(s);
+        P.hboff.assign(hboff.begin() + P.b0, hboff.begin() + P.b1 + 1);
+        for (auto& x : P.hboff) x -= base;
+        P.hper.assign(hper.begin() + P.b0, hper.begin() + P.b1);
+        P.hbq.assign(hbq.begin() + P.b0, hbq.begin() + P.b1);
+        P.r = r;
+        P.r.nblocks = pn;
+        P.r.blk = r.blk + base;
+        P.r.boff = P.w->u32("part_boff", pn + 2);
+        HIP_OK(hipMemcpyAsync(P.r.boff, P.hboff.data(), 4ull * (pn + 1), hipMemcpyHostToDevice, s));
+        P.r.binst = nullptr;
+        P.r.bcrc = r.bcrc + P.b0;
+        P.r.inuse = r.inuse + 8ull * P.b0;
+        P.r.ninuse = r.ninuse + P.b0;
+        P.r.period = r.period + P.b0;
+        P.r.bq = r.bq + P.b0;
+      }
+      HIP_OK(hipEventRecord(ev_rle, s));  // the sort streams start after RLE1 and the views
+      std::vector<std::promise<void>> sorted(K);
+      std::vector<std::future<void>> sorted_f;
+      for (auto& x : sorted) sorted_f.push_back(x.get_future());
+      const int dev = device;
+      auto sorter = [&, dev](int t) {
+        try {
+          HIP_OK(hipSetDevice(dev));  // the current device is per host thread
+        } catch (...) {
+          for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) sorted[p].set_exception(std::current_exception());
+          return;
+        }
+        hipStream_t ss = S == 1 ? s : sstream[t];
+        bool failed = false;
+        for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) {
+          if (failed) {
+            sorted[p].set_exception(std::make_exception_ptr(HipFailure(hipErrorUnknown)));
+            continue;
+          }
+          try {
+            Part& P = parts[p];
+            P.w->set_stream(ss);
+            if (ss != s) HIP_OK(hipStreamWaitEvent(ss, ev_rle, 0));
+            copyrank_begin(P.r, P.hboff, P.hper, P.hbq, P.a5, ss);  // host copy ranks overlap the sort
+            bwt_stage(*P.w, P.r, P.hboff, P.hper, bwt + hboff[P.b0], rank0 + P.b0, &P.ss, ss);
+            HIP_OK(hipEventRecord(psorted[p], ss));
+            sorted[p].set_value();
+          } catch (...) {
+            failed = true;
+            sorted[p].set_exception(std::current_exception());
+          }
+        }
+      };
+      std::vector<std::thread> th;
+      std::exception_ptr err;
+      if (S > 1)
+        for (int t = 0; t < S; t++) th.emplace_back(sorter, t);
+      else
+        sorter(0);
+      hipEvent_t e0, e1, e2;
+      HIP_OK(hipEventCreate(&e0));
+      HIP_OK(hipEventCreate(&e1));
+      HIP_OK(hipEventCreate(&e2));
+      static const bool overlap = getenv("BZG_OVERLAP") && atoi(getenv("BZG_OVERLAP")) != 0;
+      try {
+        if (!overlap) {
+          // measured (profiles/r03_pipeline_sweep.txt): MTF and tables beside the later
+          // sorts slow both more than they overlap; the default runs them once over the
+          // whole batch after every part is sorted
+          for (uint32_t p = 0; p < K; p++) {
+            sorted_f[p].get();
+            HIP_OK(hipStreamWaitEvent(s, psorted[p], 0));
+          }
+          for (auto& x : th) x.join();
+          th.clear();
+          HIP_OK(hipEventRecord(e0, s));
+          for (uint32_t p = 0; p < K; p++) {
+            parts[p].w->set_stream(s);
+            copyrank_finish(*parts[p].w, parts[p].r, rank0 + parts[p].b0, origptr + parts[p].b0, parts[p].a5, s);
+          }
+          K = 1;  // one part over the whole batch from here on
+          Part& P = parts[0];
+          P.b0 = 0;
+          P.b1 = nb;
+          P.r = r;
+          P.hboff = hboff;
+          P.w = &ws;
+          mtf_stage(ws, r, bwt, nb, hboff[nb], P.m, s, &hboff);
+          HIP_OK(hipEventRecord(e1, s));
+          code_tables(ws, r, P.m, nb, P.t, s);
+          HIP_OK(hipEventRecord(e2, s));
+          HIP_OK(hipEventSynchronize(e2));
+          (void)hipEventElapsedTime(&mtf_ms, e0, e1);
+          (void)hipEventElapsedTime(&tab_ms, e1, e2);
+          last_post = mtf_ms + tab_ms;
+        }
+        for (uint32_t p = 0; p < K && overlap; p++) {
+          Part& P = parts[p];
+          sorted_f[p].get();
+          P.w->set_stream(s);
+          HIP_OK(hipStreamWaitEvent(s, psorted[p], 0));
+          HIP_OK(hipEventRecord(e0, s));
+          copyrank_finish(*P.w, P.r, rank0 + P.b0, origptr + P.b0, P.a5, s);  // origPtr on the device (A5)
+          mtf_stage(*P.w, P.r, bwt + hboff[P.b0], P.r.nblocks, P.hboff.back(), P.m, s, &P.hboff);
+          HIP_OK(hipEventRecord(e1, s));
+          code_tables(*P.w, P.r, P.m, P.r.nblocks, P.t, s);
+          HIP_OK(hipEventRecord(e2, s));
+          HIP_OK(hipEventSynchronize(e2));  // timing only: the next part's sort is waited for anyway
+          float a = 0, b = 0;
+          (void)hipEventElapsedTime(&a, e0, e1);
+          (void)hipEventElapsedTime(&b, e1, e2);
+          mtf_ms += a;
+          tab_ms += b;
+          last_post = a + b;
+        }
+      } catch (...) {
+        err = std::current_exception();
+      }
+      for (auto& x : th) x.join();
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      (void)hipEventDestroy(e2);
+      if (err) std::rethrow_exception(err);
+      for (uint32_t p = 0; p < nparts; p++) {
+        const Part& P = parts[p];
+        sort_iters = std::max<uint64_t>(sort_iters, (uint64_t)P.ss.iterations);
+        sort_unsorted += P.ss.unsorted_elems;
+      }
     }
+    HIP_OK(hipEventRecord(ev[2], s));
     StreamCarry c;
     c.combined_crc = st->combined_crc;
     c.carry_bits = st->carry_bits;
     c.carry_byte = st->carry_byte;
     c.header_done = st->header_done;
-    *out_bytes = code_stage(ws, r, m, origptr, nb, level, trailer, c, d_out, out_cap, s);
+    std::vector<CodePart> cp;
+    for (uint32_t p = 0; p < K; p++) cp.push_back(CodePart{&parts[p].r, &parts[p].m, &parts[p].t, origptr + parts[p].b0, parts[p].r.nblocks});
+    *out_bytes = code_emit(ws, cp, level, trailer, c, d_out, out_cap, s);
     HIP_OK(hipEventRecord(ev[4], s));
     HIP_OK(hipEventSynchronize(ev[4]));
     st->combined_crc = c.combined_crc;
@@ -216,18 +364,26 @@ struct Engine {
     st->blocks_done += nb;
     *consumed = end_seg ? n : r.consumed;
     last = bzg_stats{};
+    float pipe_ms = 0, emit_ms = 0;
     (void)hipEventElapsedTime(&last.rle1_ms, ev[0], ev[1]);
-    (void)hipEventElapsedTime(&last.bwt_ms, ev[1], ev[2]);
-    (void)hipEventElapsedTime(&last.mtf_ms, ev[2], ev[3]);
-    (void)hipEventElapsedTime(&last.code_ms, ev[3], ev[4]);
+    (void)hipEventElapsedTime(&pipe_ms, ev[1], ev[2]);
+    (void)hipEventElapsedTime(&emit_ms, ev[2], ev[4]);
     (void)hipEventElapsedTime(&last.total_ms, ev[0], ev[4]);
+    // with the parts overlapped, the BWT figure is the sort pipeline up to the last part's
+    // tables minus the post-sort work of that last part; MTF and tables are their own
+    // durations summed over the parts (they run beside the sorts of later parts)
+    last.mtf_ms = mtf_ms;
+    last.code_ms = tab_ms + emit_ms;
+    last.bwt_ms = std::max(0.f, pipe_ms - last_post);
     last.nblocks = nb;
-    last.sort_iterations = (uint32_t)ss.iterations;
+    last.sort_iterations = (int)sort_iters;
     last.rle_bytes = nb ? hboff[nb] : 0;
-    last.sort_unsorted = ss.unsorted_elems;
-    if (nb) {
-      std::vector<uint32_t> nm(nb);
-      HIP_OK(hipMemcpy(nm.data(), m.nmtf, 4 * nb, hipMemcpyDeviceToHost));
+    last.sort_unsorted = sort_unsorted;
+    for (uint32_t p = 0; p < K; p++) {
+      const Part& P = parts[p];
+      if (!P.r.nblocks) continue;
+      std::vector<uint32_t> nm(P.r.nblocks);
+      HIP_OK(hipMemcpy(nm.data(), P.m.nmtf, 4 * P.r.nblocks, hipMemcpyDeviceToHost));
       for (uint32_t x : nm) last.mtf_symbols += x;
     }
   }
@@ -402,11 +558,13 @@ class EnginePool {
     std::lock_guard<std::mutex> g(mu_);
     for (int d = 0; d < ndev_; d++)
       for (Engine* e : idle_[d]) {
-        DeviceScope ds(e->device);
-        (void)hipStreamSynchronize(e->stream);
-        (void)hipStreamSynchronize(e->stream2);
-        e->ws.release_all();
-        e->ws2.release_all();
+        try {  // a C entry point calls this: nothing may escape
+          DeviceScope ds(e->device);
+          (void)hipStreamSynchronize(e->stream);
+          for (auto x : e->sstream) (void)hipStreamSynchronize(x);
+          e->release_idle();
+        } catch (...) {
+        }
       }
   }
 

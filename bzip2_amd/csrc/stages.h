@@ -33,12 +33,19 @@ class Workspace {
   const uint32_t* xpow2_table(); // 48 entries: x^(8*2^k) mod P
   size_t bytes_reserved() const { return total_; }
   void release_all();
+  // The stream that uses the workspace from now on: growth frees and allocates in that
+  // stream's order (hipFreeAsync / hipMallocAsync) instead of synchronising the device, so
+  // concurrent engines on one device never wait for each other.
+  void set_stream(hipStream_t s) { stream_ = s; }
 
  private:
   struct Buf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool async = false;
   };
+  void drop(Buf& b);
+  hipStream_t stream_ = nullptr;
   std::map<std::string, Buf> bufs_;
   size_t total_ = 0;
   uint32_t* crc_ = nullptr;
@@ -125,6 +132,28 @@ struct StreamCarry {
 // Test hook: BZ2_hbMakeCodeLengths on n tables (kMaxAlpha frequencies each) on the GPU.
 void code_lengths_test(const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len, uint8_t* d_lens,
                        hipStream_t st);
+// The per-block tables of nb blocks (selectors, code lengths, canonical codes, bit counts).
+struct CodeTables {
+  uint8_t* lens = nullptr;
+  uint32_t* codes = nullptr;
+  uint8_t* sel = nullptr;
+  uint8_t* selmtf = nullptr;
+  uint16_t* gbits = nullptr;
+  uint32_t* info = nullptr;
+  uint64_t* bbits = nullptr;
+};
+void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_t nb, CodeTables& t, hipStream_t st);
+// One part of a batch (consecutive blocks, in stream order) ready to be packed.
+struct CodePart {
+  const Rle1Result* r;
+  const MtfResult* m;
+  const CodeTables* t;
+  const uint32_t* origptr;
+  uint32_t nb;
+};
+// Bit offsets across the parts, then the packed stream (header / trailer as needed).
+uint64_t code_emit(Workspace& ws, const std::vector<CodePart>& parts, int level, bool final_batch, StreamCarry& carry,
+                   uint8_t* out, uint64_t out_cap, hipStream_t st);
 uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, const uint32_t* origptr,
                     uint32_t nblocks, int level, bool final_batch, StreamCarry& carry, uint8_t* out,
                     uint64_t out_cap, hipStream_t st);
