@@ -349,7 +349,9 @@ int BZ2_bzBuffToBuffDecompress(char* dest, unsigned int* destLen, char* source, 
     uint64_t got = 0;
     const int g = bzg_decompress_host(source, sourceLen, dest, *destLen, &got);
     if (g == BZ_OK) *destLen = (unsigned)got;
-    return g;
+    // a device that cannot hold the decode workspace (or fails) leaves the stream to the
+    // CPU decoder below, which needs only the caller's buffers
+    if (g != BZ_MEM_ERROR && g != BZ_CONFIG_ERROR) return g;
   }
   bz_stream z;
   std::memset(&z, 0, sizeof(z));

@@ -6,7 +6,9 @@
 // state machine that suspends whenever the next field or Huffman symbol needs more input
 // bits than are available, so it accepts input in arbitrary pieces and consumes input only
 // up to the last bit it used (concatenated streams and BZ2_bzReadGetUnused keep working).
-// Randomised blocks (written only by bzip2 < 0.9.5) are rejected with BZ_DATA_ERROR.
+// Randomised blocks (written only by bzip2 < 0.9.5) are decoded as the reference does: every
+// byte of the inverse BWT walk is XORed with the format's random mask before un-RLE1
+// (bzlib_private.h:163-179, bzlib.c:535-581).
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -16,6 +18,10 @@
 #include "decode.h"
 
 namespace {
+
+const int32_t kRNums[512] = {
+#include "rnums.inc"
+};
 
 uint32_t g_crc[256];
 bool g_crc_ok = false;
@@ -43,6 +49,7 @@ struct DState {
   int level;
   uint32_t stored_bcrc, comb_crc;
   int32_t origptr;
+  bool randomised;
   uint32_t map16;
   int map_i;
   uint8_t seq2byte[256];
@@ -137,10 +144,19 @@ bool finish_block(DState* s) {
   int run = 0, last = -1;
   const size_t base = s->out.size();
   s->out.reserve(base + (size_t)n + 64);
+  int32_t r_togo = 0, r_pos = 0;  // the random mask of a randomised block, one step per walk byte
   for (int32_t k = 0; k < n; k++) {
     pos = tt[pos];
-    const uint32_t ch = pos & 0xffu;
+    uint32_t ch = pos & 0xffu;
     pos >>= 8;
+    if (s->randomised) {
+      if (r_togo == 0) {
+        r_togo = kRNums[r_pos];
+        r_pos = (r_pos + 1) & 511;
+      }
+      r_togo--;
+      ch ^= r_togo == 1 ? 1u : 0u;
+    }
     if (run == 4) {
       for (uint32_t r = 0; r < ch; r++) {
         s->out.push_back((uint8_t)last);
@@ -199,7 +215,7 @@ int advance(DState* s) {
         break;
       case kRandBit:
         if (!need(s, 1)) return BZ_OK;
-        if (take(s, 1)) return BZ_DATA_ERROR;  // randomised block (pre-0.9.5 encoders)
+        s->randomised = take(s, 1) != 0;  // randomised block (pre-0.9.5 encoders)
         s->ph = kOrigPtr;
         break;
       case kOrigPtr:

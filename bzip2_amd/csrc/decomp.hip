@@ -156,12 +156,14 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
   uint32_t ninuse = 0, g = 0, nsel = 0, alpha = 0;
 
   // ---- block header (decompress.c:306-352): magic (found by the scan), CRC, rand bit, origPtr
-  if (p + 48 + 32 + 1 + 24 + 16 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
+  // the reference checks origPtr before it reads the 16 mapping bits (decompress.c:348-351)
+  if (p + 48 + 32 + 1 + 24 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
   p += 48;
   bcrc = W.get(p, 32);
   rnd = W.get(p, 1);
   origptr = W.get(p, 24);
   if (origptr > nbmax) { status = BZ_DATA_ERROR; goto done; }
+  if (p + 16 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
   // ---- symbol map (decompress.c:354-370)
   {
     const uint32_t used16 = W.get(p, 16);

@@ -140,7 +140,14 @@ struct Engine {
     ws.set_stream(stream);
   }
 
+  // Back to the engine's own stream once a call is over: a caller's stream may be destroyed
+  // after the call, and later growth or release must not be ordered on it.
+  void own_streams() {
+    ws.set_stream(stream);
+    for (auto& w : pws) w->set_stream(stream);
+  }
   void release_idle() {
+    own_streams();
     ws.release_all();
     for (auto& w : pws) w->release_all();
   }
@@ -399,6 +406,7 @@ static constexpr uint64_t kMaxBatch = 1500ull * 1000 * 1000;
 
 void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
+  ws.set_stream(s);
   uint64_t done_in = 0, done_out = 0;
   bzg_stats acc{};
   for (;;) {
@@ -584,10 +592,13 @@ static EnginePool& pool() {
 
 // One engine of a device for the duration of a call, with the device made current.
 struct Lease {
+  DeviceScope ds;  // first: if switching the device throws, no engine has been taken yet
   Engine* e;
-  DeviceScope ds;
-  explicit Lease(int dev) : e(pool().acquire(dev)), ds(dev) {}
-  ~Lease() { pool().release(e); }
+  explicit Lease(int dev) : ds(dev), e(pool().acquire(dev)) {}
+  ~Lease() {
+    e->own_streams();
+    pool().release(e);
+  }
   Engine* operator->() const { return e; }
   Lease(const Lease&) = delete;
   Lease& operator=(const Lease&) = delete;
@@ -628,7 +639,8 @@ static void publish_stats(const bzg_stats& s) {
 // rank drives one region at a time; kept on its own engine so the walk finds the map.
 struct SegState {
   std::mutex mu;
-  Engine* e = nullptr;
+  Engine* e = nullptr;          // the engine of the current region's device
+  std::vector<Engine*> by_dev;  // one per device, created on first use, kept for the process
   const uint8_t* in = nullptr;
   uint64_t n = 0;
   int level = 0;
@@ -945,6 +957,15 @@ static std::vector<int> multi_devices(uint64_t n) {
     const int k = std::min(atoi(ng), ndev);
     for (int d = 0; d < k; d++) devs.push_back(d);
   }
+  // a device listed more often than it has engines would block the call: clamp the repeats
+  {
+    const char* c = getenv("BZG_ENGINES_PER_DEVICE");
+    const int cap = c ? std::max(1, atoi(c)) : 4;
+    std::vector<int> seen(std::max(ndev, 1), 0), kept;
+    for (int d : devs)
+      if (seen[d]++ < cap) kept.push_back(d);
+    devs.swap(kept);
+  }
   // worth it only for inputs of several blocks per device; shards within one batch
   if (devs.size() < 2 || n < (uint64_t)devs.size() * 4000000ull || n / devs.size() + 1 > kMaxBatch) devs.clear();
   return devs;
@@ -995,12 +1016,15 @@ int bzg_seg_map(const void* d_in, uint64_t n, int level, void* stream) {
   S.in = nullptr;
   return guarded([&] {
     const int dev = current_device();
-    if (!S.e || S.e->device != dev) {
+    if (S.by_dev.size() <= (size_t)dev) S.by_dev.resize(dev + 1, nullptr);
+    if (!S.by_dev[dev]) {
       DeviceScope ds(dev);
-      S.e = new Engine(dev);  // one per process, never destroyed
+      S.by_dev[dev] = new Engine(dev);
     }
+    S.e = S.by_dev[dev];
     DeviceScope ds(dev);
     hipStream_t s = stream ? (hipStream_t)stream : S.e->stream;
+    S.e->ws.set_stream(s);
     seg_map_stage(S.e->ws, (const uint8_t*)d_in, n, s);
     S.in = (const uint8_t*)d_in;
     S.n = n;
@@ -1130,6 +1154,7 @@ int bzg_decompress_host(const void* src, uint64_t n, void* dst, uint64_t dst_cap
     if (n) HIP_OK(hipMemcpyAsync(din, src, n, hipMemcpyHostToDevice, L->stream));
     DecodeStats ds;
     uint64_t got = 0;
+    L->ws.set_stream(L->stream);
     const int rc = decode_stage(L->ws, din, n, dout, dst_cap, &got, &ds, L->stream);
     if (got) HIP_OK(hipMemcpyAsync(dst, dout, got, hipMemcpyDeviceToHost, L->stream));
     HIP_OK(hipStreamSynchronize(L->stream));
@@ -1150,7 +1175,19 @@ void bzg_last_stats(bzg_stats* out) {
 }
 
 void bzg_release(void) {
-  if (pool().devices() > 0) pool().release_idle_memory();
+  if (pool().devices() <= 0) return;
+  pool().release_idle_memory();
+  SegState& S = seg_state();  // the chunk-map engines' workspaces too
+  std::lock_guard<std::mutex> g(S.mu);
+  for (Engine* e : S.by_dev)
+    if (e) try {
+        DeviceScope ds(e->device);
+        (void)hipStreamSynchronize(e->stream);
+        e->release_idle();
+      } catch (...) {
+      }
+  S.in = nullptr;
+  S.n = 0;
 }
 
 int32_t bzg_periodic_origptr(const uint8_t* block, int32_t n) {

@@ -273,3 +273,49 @@ def test_file_api_argument_errors(lib, tmp_path):
     assert e.value == B.BZ_SEQUENCE_ERROR  # only after STREAM_END
     L.BZ2_bzReadClose(ctypes.byref(e), h)
     c.fclose(f)
+
+
+def test_randomised_block_streaming_decoder(lib, tmp_path):
+    """BZ2_bzDecompress in small pieces and BZ2_bzRead decode a randomised block (the format's
+    pre-0.9.5 random mask, bzlib.c:535-581) to the reference's output
+    (tests/golden/randomised.bz2, made by tests/golden/make_randomised.py)."""
+    from tests import oracles as O
+    g = os.path.join(ROOT, "tests", "golden")
+    comp = open(os.path.join(g, "randomised.bz2"), "rb").read()
+    want = open(os.path.join(g, "randomised.out"), "rb").read()
+    if O.has_ref():
+        rc, ref_out = O.ref_decompress(comp, len(want) + 64)
+        assert rc == 0 and ref_out == want
+    strm = B.bz_stream()
+    assert lib.BZ2_bzDecompressInit(ctypes.byref(strm), 0, 0) == 0
+    inb = ctypes.create_string_buffer(comp, len(comp))
+    ob = ctypes.create_string_buffer(1000)
+    out, pos, rc = bytearray(), 0, 0
+    while rc != B.BZ_STREAM_END:
+        step = min(97, len(comp) - pos)
+        strm.next_in = ctypes.cast(ctypes.byref(inb, pos), ctypes.c_void_p)
+        strm.avail_in = step
+        strm.next_out = ctypes.cast(ob, ctypes.c_void_p)
+        strm.avail_out = 1000
+        rc = lib.BZ2_bzDecompress(ctypes.byref(strm))
+        assert rc in (0, B.BZ_STREAM_END), rc
+        out += ob.raw[: 1000 - strm.avail_out]
+        pos += step - strm.avail_in
+    lib.BZ2_bzDecompressEnd(ctypes.byref(strm))
+    assert bytes(out) == want
+    assert B.buff_to_buff_decompress(comp, len(want) + 10) == want
+    L = _file_api(lib)
+    p = tmp_path / "r.bz2"
+    p.write_bytes(comp)
+    c = _libc()
+    f = c.fopen(str(p).encode(), b"rb")
+    e = ctypes.c_int(0)
+    h = L.BZ2_bzReadOpen(ctypes.byref(e), f, 0, 0, None, 0)
+    got = bytearray()
+    big = ctypes.create_string_buffer(4096)
+    while e.value == B.BZ_OK:
+        n = L.BZ2_bzRead(ctypes.byref(e), h, big, 4096)
+        got += big.raw[:n]
+    assert e.value == B.BZ_STREAM_END and bytes(got) == want
+    L.BZ2_bzReadClose(ctypes.byref(e), h)
+    c.fclose(f)

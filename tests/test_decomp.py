@@ -140,6 +140,17 @@ def damaged_cases(s: bytes, rng: random.Random, nflip: int, ntrunc: int):
         yield bytes(b)
     for _ in range(ntrunc):
         yield s[: rng.randrange(len(s))]
+    for _ in range(ntrunc):  # a flip and a cut a few bytes after it
+        b = bytearray(s)
+        pos = rng.randrange(len(b) - 8)
+        b[pos] ^= 1 << rng.randrange(8)
+        yield bytes(b[: pos + rng.randint(1, 6)])
+    # the first block's origPtr (stream bits 113..136) out of range, cut inside the next 16
+    # bits: the reference reports the origPtr (decompress.c:348-351) before it needs them
+    for cut in (17, 18, 19):
+        b = bytearray(s)
+        b[14] |= 0x40
+        yield bytes(b[:cut])
     yield s[:3]
     yield b"BZh0" + s[4:]
     yield b"BZx9"
