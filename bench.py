@@ -138,6 +138,7 @@ def main():
 
     if mode == "stream" and rank != 0:
         stream_parity(None, d_in, a, world)  # sends this rank's shard to rank 0
+        stream_ref_check(d_in, a, world)
     if rank == 0:
         ratio = out_bytes / a.bytes
         rho = stats["rle_bytes"] / a.bytes
@@ -180,6 +181,7 @@ def main():
         }
         if mode == "stream" and last_stream[0] is not None:
             result["stream_check"] = stream_parity(last_stream[0], d_in, a, world)
+            result["stream_check"]["reference"] = stream_ref_check(d_in, a, world)
         pmc = pmc_traffic(a)
         if pmc is not None:
             rl = result["roofline"]
@@ -231,6 +233,38 @@ def stream_parity(stream, d_in, a, world):
     torch.cuda.empty_cache()
     return {"bytes": int(s.numel()), "ranks": world, "equals_single_device_stream": eq,
             "against": f"bzg_compress_device over all {n * world} B on one device"}
+
+
+def stream_ref_check(d_in, a, world, per_rank: int = 3_000_000):
+    """Outside the timed region, every rank: the first per_rank bytes of each rank's shard form
+    one sample stream compressed by the same sharded path (cut chain, halo, gather over the
+    job's backend), with a shard boundary every per_rank bytes; rank 0 compares it byte for
+    byte with the reference build (oracle/_ref) on the concatenated sample."""
+    import torch.distributed as dist
+    from bzip2_amd import shard
+
+    rank = dist.get_rank() if world > 1 else 0
+    gloo = world > 1 and dist.get_backend() == "gloo"
+    k = min(per_rank, d_in.numel())
+    piece = d_in[:k].contiguous()
+    res = shard.compress_sharded(piece, rank * k, world * k, a.level)
+    if rank != 0:
+        dist.send(piece.cpu() if gloo else piece, 0)
+        return None
+    parts = [piece.cpu()]
+    for r in range(1, world):
+        tmp = torch.empty(k, dtype=torch.uint8, device="cpu" if gloo else "cuda")
+        dist.recv(tmp, r)
+        parts.append(tmp.cpu())
+    sample = torch.cat(parts).numpy().tobytes()
+    from tests import oracles as O
+
+    if not O.has_ref():
+        return {"sample_bytes": len(sample), "ranks": world, "bit_exact": None, "against": "oracle/_ref absent"}
+    want = O.ref_compress(sample, a.level)
+    got = res.cpu().numpy().tobytes()
+    return {"sample_bytes": len(sample), "ranks": world, "shard_bytes": k, "bit_exact": got == want,
+            "against": "reference (oracle/_ref BZ2_bzBuffToBuffCompress on the concatenated sample)"}
 
 
 def time_device(d, n, level, d_out, cap, steps, warmup=1):

@@ -193,10 +193,12 @@ def last_decode_stats() -> dict:
 
 
 def stream_compress(chunks, level: int = 9, finish_with_last: bool = False, out_chunk: int = 1 << 16,
-                    flush_after=()) -> bytes:
+                    flush_after=(), progress=None) -> bytes:
     """Drive BZ2_bzCompress like a streaming caller: every chunk with BZ_RUN (or, for the last
     chunk when finish_with_last, with BZ_FINISH directly), then BZ_FINISH until
-    BZ_STREAM_END.  Chunk indices listed in flush_after are followed by BZ_FLUSH."""
+    BZ_STREAM_END.  Chunk indices listed in flush_after are followed by BZ_FLUSH.  A list
+    passed as progress receives (input bytes given, output bytes received) after each RUN
+    chunk."""
     L = lib()
     strm = bz_stream()
     rc = L.BZ2_bzCompressInit(ctypes.byref(strm), level, 0, 30)
@@ -227,6 +229,8 @@ def stream_compress(chunks, level: int = 9, finish_with_last: bool = False, out_
                 break
             while strm.avail_in > 0:
                 pump(BZ_RUN, (BZ_RUN_OK,))
+            if progress is not None:
+                progress.append((sum(len(x) for x in chunks[: i + 1]), len(out)))
             if i in flush_after:
                 while pump(BZ_FLUSH, (BZ_FLUSH_OK, BZ_RUN_OK)) != BZ_RUN_OK:
                     pass

@@ -6,11 +6,15 @@
 // FINISHING and must be repeated with an unchanged avail_in until BZ_RUN_OK / BZ_STREAM_END.
 // Input is staged on the host and compressed by the device in batches; output may lag input
 // (the concatenated bytes are what the reference emits for the same call pattern):
-//   * RUN-mode bytes are staged; once kStageMax bytes are staged the complete blocks among
-//     them are compressed (RUN semantics: a full block is cut, bzlib.c:383-386);
+//   * RUN-mode bytes are staged; once the stage limit is reached the complete blocks among
+//     them are compressed (RUN semantics: a full block is cut, bzlib.c:383-386).  The limit
+//     starts at two blocks' worth, so a streaming caller sees output about as soon as the
+//     reference would emit it, and doubles with every device batch up to kStageMax, where a
+//     batch amortises its launch and synchronisation cost;
 //   * FLUSH / FINISH compress everything staged as the end of a segment; the final length-1
 //     run chunk joins a full block only when bytes arrived with the FLUSH/FINISH call
 //     (bzlib.c:276-308).
+#include <algorithm>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -37,6 +41,7 @@ struct CState {
   unsigned avail_in_expect;
   bool segment_done;
   bool tail_merge;
+  size_t stage_limit;
   std::vector<uint8_t> staged;
   std::vector<uint8_t> out;
   size_t out_pos;
@@ -119,6 +124,7 @@ int BZ2_bzCompressInit(bz_stream* strm, int blockSize100k, int verbosity, int wo
   s->avail_in_expect = 0;
   s->segment_done = false;
   s->tail_merge = false;
+  s->stage_limit = 2 * (size_t)100000 * (size_t)blockSize100k + 64;
   s->out_pos = 0;
   bzg_stream_init(&s->st, blockSize100k);
   strm->state = s;
@@ -138,9 +144,10 @@ int BZ2_bzCompress(bz_stream* strm, int action) {
       case kModeRunning:
         if (action == BZ_RUN) {
           bool progress = take_input(s);
-          if (s->staged.size() >= kStageMax) {
+          if (s->staged.size() >= s->stage_limit) {
             int rc = run_device(s, false, false);
             if (rc != BZ_OK) return rc;
+            s->stage_limit = std::min(2 * s->stage_limit, kStageMax);
           }
           progress |= drain(s);
           return progress ? BZ_RUN_OK : BZ_PARAM_ERROR;

@@ -861,13 +861,24 @@ static int compress_host_multi(const uint8_t* src, uint64_t n, int level, uint8_
       sh[d].hi = nx;
     }
   }
-  // 4. compress the ranges, shift the bits to their byte offsets on the device
+  // 4. compress the ranges, shift the bits to their byte offsets on the device.  A range is
+  // built from the shards already on the devices: in place when it lies in the own shard,
+  // else the own part plus the tail of later shards copied device to device (xGMI peer copies
+  // between GPUs) -- the input crosses PCIe once.
   parallel([&](Shard& S) {
     if (S.hi <= S.lo) return;
     Engine& E = *S.eng;
     const uint64_t len = S.hi - S.lo;
-    uint8_t* din = E.ws.u8("mg_in", len + 64);
-    HIP_OK(hipMemcpyAsync(din, src + S.lo, len, hipMemcpyHostToDevice, E.stream));
+    const uint8_t* din = S.d_shard + (S.lo - S.s);
+    if (S.hi > S.e) {
+      uint8_t* buf = E.ws.u8("mg_in", len + 64);
+      HIP_OK(hipMemcpyAsync(buf, S.d_shard + (S.lo - S.s), S.e - S.lo, hipMemcpyDeviceToDevice, E.stream));
+      for (size_t j = (size_t)(&S - sh.data()) + 1; j < N && sh[j].s < S.hi; j++) {
+        const uint64_t a = sh[j].s, b = std::min(S.hi, sh[j].e);
+        HIP_OK(hipMemcpyPeerAsync(buf + (a - S.lo), S.dev, sh[j].d_shard, sh[j].dev, b - a, E.stream));
+      }
+      din = buf;
+    }
     const uint64_t cap = bzg_bound(len) + 64;
     uint8_t* dout = E.ws.u8("mg_out", cap);
     bzg_stream_state st;
@@ -892,7 +903,17 @@ static int compress_host_multi(const uint8_t* src, uint64_t n, int level, uint8_
   }
   const uint64_t out_len = (total_bits + 80 + 7) / 8;
   if (out_len > dst_cap) return BZ_OUTBUFF_FULL;
-  std::memset(dst, 0, out_len);
+  // 5. gather on the first device: every range's shifted bytes but its first (shared with the
+  // previous range's last byte, OR-ed on the host) are peer-copied to their byte offset, then
+  // one copy to the caller's buffer
+  uint8_t* gat = nullptr;
+  {
+    Engine& E0 = *sh[0].eng;
+    DeviceScope ds0(sh[0].dev);
+    gat = E0.ws.u8("mg_gather", out_len + 64);
+    HIP_OK(hipMemsetAsync(gat, 0, out_len, E0.stream));
+    HIP_OK(hipStreamSynchronize(E0.stream));
+  }
   std::vector<uint8_t> head(N, 0);
   parallel([&](Shard& S) {
     const size_t d = &S - sh.data();
@@ -905,11 +926,16 @@ static int compress_host_multi(const uint8_t* src, uint64_t n, int level, uint8_
     k_shift_bits<<<(unsigned)std::min<uint64_t>(ceil_div64(nb, 256), 65536), 256, 0, E.stream>>>(dout, S.nbits, s8,
                                                                                                dsh);
     HIP_OK(hipGetLastError());
-    // byte 0 is shared with the previous range's last byte: OR-ed on the host below
     HIP_OK(hipMemcpyAsync(&head[d], dsh, 1, hipMemcpyDeviceToHost, E.stream));
-    if (nb > 1) HIP_OK(hipMemcpyAsync(dst + off[d] / 8 + 1, dsh + 1, nb - 1, hipMemcpyDeviceToHost, E.stream));
+    if (nb > 1) HIP_OK(hipMemcpyPeerAsync(gat + off[d] / 8 + 1, sh[0].dev, dsh + 1, S.dev, nb - 1, E.stream));
     HIP_OK(hipStreamSynchronize(E.stream));
   });
+  {
+    Engine& E0 = *sh[0].eng;
+    DeviceScope ds0(sh[0].dev);
+    HIP_OK(hipMemcpyAsync(dst, gat, out_len, hipMemcpyDeviceToHost, E0.stream));
+    HIP_OK(hipStreamSynchronize(E0.stream));
+  }
   uint32_t comb = 0;
   bzg_stats acc{};
   for (size_t d = 0; d < N; d++) {

@@ -359,6 +359,23 @@ def test_streaming_chunked_and_flush():
     assert B.stream_compress(chunks, 2, flush_after=(0, 1)) == O.ref_stream_compress(chunks, 2, flush_after=(0, 1))
 
 
+def test_streaming_emits_blocks_as_they_fill():
+    """BZ_RUN output appears about when the reference would emit it (bzlib.c:383-386): the
+    first complete blocks come back after about two blocks of input, not after the whole
+    staging limit; the whole stream still equals the reference's."""
+    if not O.has_ref():
+        pytest.skip("needs oracle/_ref for the streaming reference")
+    data = datagen.text(6_000_000, 62)
+    chunks = [data[i:i + 5000] for i in range(0, len(data), 5000)]
+    prog = []
+    got = B.stream_compress(chunks, 1, progress=prog)
+    assert got == O.ref_stream_compress(chunks, 1)
+    first = next(inp for inp, outb in prog if outb > 0)
+    assert first <= 400_000, first  # -1 blocks hold ~100 kB: output after ~2-4 blocks of input
+    half = next(outb for inp, outb in prog if inp >= len(data) // 2)
+    assert half >= len(got) // 4, (half, len(got))  # output keeps pace in the middle
+
+
 def test_concurrent_streams_four_threads():
     """Four host threads at once, each running BZ2_bzBuffToBuffCompress and chunked
     BZ2_bzCompress loops on its own inputs (the reference is reentrant per bz_stream,
@@ -492,6 +509,8 @@ def test_multi_device_host_path(monkeypatch, level):
     monkeypatch.setenv("BZG_DEVICES", "0,0,0,0")  # a stream whose last byte opens no block
     data = b"a" * (255 * 19996 * 3 + 4) + b"b"
     assert B.buff_to_buff_compress(data, 1) == expected(data, 1)
+    monkeypatch.setenv("BZG_DEVICES", "0,0,0,0,0,0")  # more repeats than engines per device: clamped
+    assert B.buff_to_buff_compress(txt, level) == expected(txt, level)
 
 
 def test_round_trip_large_properties():
