@@ -43,7 +43,7 @@ EXPORTS = [
 ENGINE_EXPORTS = [
     "bzg_stream_init", "bzg_compress_device", "bzg_compress_host", "bzg_compress_host_stream",
     "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_stage_code_lengths", "bzg_last_stats",
-    "bzg_release", "bzg_device_ok", "bzg_periodic_origptr", "bzg_seg_map", "bzg_seg_walk",
+    "bzg_release", "bzg_device_ok", "bzg_periodic_origptr", "bzg_qperiodic_bwt", "bzg_seg_map", "bzg_seg_walk",
     "bzg_find_magics", "bzg_decompress_device", "bzg_decompress_host", "bzg_last_decode_stats",
 ]
 
@@ -128,6 +128,8 @@ def lib() -> ctypes.CDLL:
         L.bzg_find_magics.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64), vp]
         L.bzg_seg_walk.argtypes = [u32, ci, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.bzg_periodic_origptr.restype = ctypes.c_int32
+        L.bzg_qperiodic_bwt.argtypes = [vp, u32, vp, ctypes.POINTER(u32)]
+        L.bzg_qperiodic_bwt.restype = u32
         L.bzg_decompress_device.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64), vp]
         L.bzg_decompress_host.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64)]
         L.bzg_last_decode_stats.argtypes = [ctypes.POINTER(bzg_decode_stats)]
@@ -316,6 +318,16 @@ def code_lengths(tables, max_len: int = 17):
 def periodic_origptr(block: bytes) -> int:
     """origPtr the reference assigns to an exactly periodic block (host replay, A5)."""
     return int(lib().bzg_periodic_origptr(bytes(block), len(block)))
+
+
+def qperiodic_bwt(block: bytes):
+    """(period, BWT, origPtr) of a quasi-periodic block by the analytic order the GPU sort
+    uses for it (qsa.cpp, host); None when the block is not quasi-periodic."""
+    n = len(block)
+    out = ctypes.create_string_buffer(max(n, 1))
+    o = ctypes.c_uint32(0)
+    p = int(lib().bzg_qperiodic_bwt(bytes(block), n, out, ctypes.byref(o)))
+    return (p, out.raw[:n], o.value) if p else None
 
 
 def last_stats() -> dict:

@@ -146,8 +146,9 @@ __global__ void k_init_tables(const uint32_t* __restrict__ nmtf_g, const uint32_
   }
 }
 
+constexpr uint32_t kCfVec = (kT * kGroupSize + 8 * kT - 1) / (8 * kT);  // 16-byte words per thread per chunk
 struct CfLds {
-  uint16_t chunk[kT * kGroupSize + 8];
+  alignas(16) uint16_t chunk[kT * kGroupSize + 8];
   uint32_t lenp[2][kMaxAlpha];       // lengths of tables 0-2 / 3-5 in 10-bit fields
   uint32_t rfreq[kNGroups][kMaxAlpha * 2];  // 2 bank-spread copies per counter (thread & 1)
   uint32_t sh[8];
@@ -178,11 +179,27 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
     for (int i = threadIdx.x; i < kNGroups * kMaxAlpha * 2; i += kT) (&S.rfreq[0][0])[i] = 0;
   uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
   uint32_t mybits = 0;
+  // a chunk (kT groups) is read as 16-byte words (block offsets are multiples of 8 values);
+  // the next chunk's words are loaded into registers while this one is costed
+  uint4 q[kCfVec];
+  auto load_chunk = [&](uint32_t ch) {
+    const uint32_t lo = ch * kT * kGroupSize, hi = min(lo + kT * kGroupSize, nmtf);
+#pragma unroll
+    for (uint32_t k = 0; k < kCfVec; k++) {
+      const uint32_t i = lo + 8 * (threadIdx.x + k * kT);
+      q[k] = i < hi ? *reinterpret_cast<const uint4*>(mv + i) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  load_chunk(c0);
   for (uint32_t ch = c0; ch < c1; ch++) {
     const uint32_t g0 = ch * kT;
-    const uint32_t lo = g0 * kGroupSize, hi = min((g0 + kT) * kGroupSize, nmtf);
     __syncthreads();
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) S.chunk[i - lo] = mv[i];
+#pragma unroll
+    for (uint32_t k = 0; k < kCfVec; k++) {
+      const uint32_t j = 8 * (threadIdx.x + k * kT);
+      if (j < kT * kGroupSize) *reinterpret_cast<uint4*>(S.chunk + j) = q[k];
+    }
+    if (ch + 1 < c1) load_chunk(ch + 1);
     __syncthreads();
     const uint32_t g = g0 + threadIdx.x;
     if (g < nsel) {
@@ -450,7 +467,7 @@ struct BitWriter {
 constexpr uint32_t kPackSlices = BZG_PACK_SLICES;  // workgroups per block in k_pack
 
 struct PackLds {
-  uint16_t chunk[kT * kGroupSize + 8];
+  alignas(16) uint16_t chunk[kT * kGroupSize + 8];
   uint32_t bits[(kT * kGroupSize * kMaxCodeLen + 31) / 32 + 2];  // one step's payload
 };
 
@@ -462,7 +479,7 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
                                              const uint16_t* __restrict__ gbits_g, const uint32_t* __restrict__ info_g,
                                              const uint64_t* __restrict__ boffbits, uint32_t* __restrict__ out) {
   __shared__ uint8_t len[kNGroups][kMaxAlpha + 2];
-  __shared__ uint32_t code[kNGroups][kMaxAlpha];
+  __shared__ uint32_t code[kNGroups][kMaxAlpha];  // code | length << 24 (one LDS read per symbol)
   __shared__ uint32_t sh[8];
   __shared__ PackLds P;
   // kPackSlices workgroups per block: slice 0 also writes the block header, tables and
@@ -477,7 +494,8 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
   const uint16_t* mv = mtfv + mtf_off[b];
   for (int i = threadIdx.x; i < ng * kMaxAlpha; i += kT) {
     len[i / kMaxAlpha][i % kMaxAlpha] = lens_g[(size_t)b * kNGroups * kMaxAlpha + i];
-    code[i / kMaxAlpha][i % kMaxAlpha] = codes_g[(size_t)b * kNGroups * kMaxAlpha + i];
+    code[i / kMaxAlpha][i % kMaxAlpha] =
+        codes_g[(size_t)b * kNGroups * kMaxAlpha + i] | ((uint32_t)lens_g[(size_t)b * kNGroups * kMaxAlpha + i] << 24);
   }
   __syncthreads();
   const uint64_t p0 = boffbits[b];
@@ -578,9 +596,25 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
       block_incl_sum(before, sh, &tot);
       pos += tot;
     }
+    // a step's symbols are read as 16-byte words (block offsets are multiples of 8 values);
+    // the next step's words are loaded into registers while this one is encoded
+    uint4 q[kCfVec];
+    auto load_step = [&](uint32_t g0) {
+      const uint32_t lo = g0 * kGroupSize, hi = min(lo + kT * kGroupSize, nmtf);
+#pragma unroll
+      for (uint32_t k = 0; k < kCfVec; k++) {
+        const uint32_t i = lo + 8 * (threadIdx.x + k * kT);
+        q[k] = i < hi ? *reinterpret_cast<const uint4*>(mv + i) : make_uint4(0, 0, 0, 0);
+      }
+    };
+    if (s0 < s1) load_step(s0 * kT);
     for (uint32_t g0 = s0 * kT; g0 < s1 * kT; g0 += kT) {
-      const uint32_t lo = g0 * kGroupSize, hi = min((g0 + kT) * kGroupSize, nmtf);
-      for (uint32_t i = lo + threadIdx.x; i < hi; i += kT) P.chunk[i - lo] = mv[i];
+#pragma unroll
+      for (uint32_t k = 0; k < kCfVec; k++) {
+        const uint32_t j = 8 * (threadIdx.x + k * kT);
+        if (j < kT * kGroupSize) *reinterpret_cast<uint4*>(P.chunk + j) = q[k];
+      }
+      if (g0 + kT < s1 * kT) load_step(g0 + kT);
       const uint32_t g = g0 + threadIdx.x;
       const uint32_t mybits = g < nsel ? gb[g] : 0u;
       uint32_t stepbits;
@@ -598,9 +632,9 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
         uint32_t na = bp & 31;                    // bits in acc, counted from the word start
         uint32_t wi = bp >> 5;
         for (uint32_t i = 0; i < n; i++) {
-          const uint32_t v = c[i];
-          const uint32_t l = len[t][v];
-          acc |= ((uint64_t)code[t][v] << (64 - l)) >> na;
+          const uint32_t cl = code[t][c[i]];
+          const uint32_t l = cl >> 24;
+          acc |= ((uint64_t)(cl & 0xffffffu) << (64 - l)) >> na;
           na += l;
           if (na >= 32) {
             atomicOr(&P.bits[wi++], (uint32_t)(acc >> 32));

@@ -157,7 +157,7 @@ struct Engine {
   struct Part {
     uint32_t b0 = 0, b1 = 0;
     Rle1Result r;
-    std::vector<uint32_t> hboff, hper, hbq;
+    std::vector<uint32_t> hboff, hper, hbq, hqp;
     Workspace* w = nullptr;
     CopyRankJob a5;
     SortStats ss;
@@ -203,7 +203,7 @@ struct Engine {
     HIP_OK(hipEventRecord(ev[1], s));
     const uint32_t nb = r.nblocks;
     uint32_t* origptr = ws.u32("origptr", nb + 2);
-    std::vector<uint32_t> hboff(nb + 1), hper(nb), hbq(nb);
+    std::vector<uint32_t> hboff(nb + 1), hper(nb), hbq(nb), hqp(nb);
     std::unique_ptr<Part[]> parts;
     uint32_t K = 0, nparts = 0;
     float mtf_ms = 0, tab_ms = 0, last_post = 0;
@@ -212,6 +212,7 @@ struct Engine {
       HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, s));
       HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, s));
       HIP_OK(hipMemcpyAsync(hbq.data(), r.bq, 4 * nb, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipMemcpyAsync(hqp.data(), r.qper, 4 * nb, hipMemcpyDeviceToHost, s));
       HIP_OK(hipStreamSynchronize(s));
       uint8_t* bwt = ws.u8("bwt", hboff[nb] + 16);
       uint32_t* rank0 = ws.u32("rank0", nb + 2);
@@ -232,6 +233,7 @@ struct Engine {
         for (auto& x : P.hboff) x -= base;
         P.hper.assign(hper.begin() + P.b0, hper.begin() + P.b1);
         P.hbq.assign(hbq.begin() + P.b0, hbq.begin() + P.b1);
+        P.hqp.assign(hqp.begin() + P.b0, hqp.begin() + P.b1);
         P.r = r;
         P.r.nblocks = pn;
         P.r.blk = r.blk + base;
@@ -243,6 +245,7 @@ struct Engine {
         P.r.ninuse = r.ninuse + P.b0;
         P.r.period = r.period + P.b0;
         P.r.bq = r.bq + P.b0;
+        P.r.qper = r.qper + P.b0;
       }
       HIP_OK(hipEventRecord(ev_rle, s));  // the sort streams start after RLE1 and the views
       std::vector<std::promise<void>> sorted(K);
@@ -268,7 +271,7 @@ struct Engine {
             P.w->set_stream(ss);
             if (ss != s) HIP_OK(hipStreamWaitEvent(ss, ev_rle, 0));
             copyrank_begin(P.r, P.hboff, P.hper, P.hbq, P.a5, ss);  // host copy ranks overlap the sort
-            bwt_stage(*P.w, P.r, P.hboff, P.hper, bwt + hboff[P.b0], rank0 + P.b0, &P.ss, ss);
+            bwt_stage(*P.w, P.r, P.hboff, P.hper, bwt + hboff[P.b0], rank0 + P.b0, &P.ss, ss, P.hqp.data());
             HIP_OK(hipEventRecord(psorted[p], ss));
             sorted[p].set_value();
           } catch (...) {
@@ -1286,16 +1289,17 @@ int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, u
     HIP_OK(hipMemcpy(r.blk, blocks, total, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice));
     block_info_stage(e.ws, r, e.stream);
-    std::vector<uint32_t> hboff(offsets, offsets + nb + 1), hper(nb), hbq(nb);
+    std::vector<uint32_t> hboff(offsets, offsets + nb + 1), hper(nb), hbq(nb), hqp(nb);
     HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, e.stream));
     HIP_OK(hipMemcpyAsync(hbq.data(), r.bq, 4 * nb, hipMemcpyDeviceToHost, e.stream));
+    HIP_OK(hipMemcpyAsync(hqp.data(), r.qper, 4 * nb, hipMemcpyDeviceToHost, e.stream));
     HIP_OK(hipStreamSynchronize(e.stream));
     uint8_t* bwt = e.ws.u8("bwt", total + 16);
     uint32_t* rank0 = e.ws.u32("rank0", nb + 2);
     uint32_t* d_orig = e.ws.u32("origptr", nb + 2);
     CopyRankJob a5;
     copyrank_begin(r, hboff, hper, hbq, a5, e.stream);
-    bwt_stage(e.ws, r, hboff, hper, bwt, rank0, nullptr, e.stream);
+    bwt_stage(e.ws, r, hboff, hper, bwt, rank0, nullptr, e.stream, hqp.data());
     copyrank_finish(e.ws, r, rank0, d_orig, a5, e.stream);
     HIP_OK(hipMemcpyAsync(origptr, d_orig, 4 * nb, hipMemcpyDeviceToHost, e.stream));
     HIP_OK(hipStreamSynchronize(e.stream));

@@ -242,8 +242,13 @@ __global__ void __launch_bounds__(64 * kCW) k_compose(const uint32_t* __restrict
 #define BZG_MTF_REGW 8
 #endif
 constexpr int kRegW = BZG_MTF_REGW;  // list words (4 positions each) held in registers
+#ifndef BZG_MTF_ROWMIN
+#define BZG_MTF_ROWMIN 64
+#endif
+constexpr uint32_t kRowMin = BZG_MTF_ROWMIN;  // chunks with more distinct symbols go to k_mtf_row
 __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
-                                                const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
+                                                const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ siglen,
+                                                const uint32_t* __restrict__ init,
                                                 uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
                                                 uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
   __shared__ uint32_t lst[64 - kRegW][kT];
@@ -253,7 +258,10 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
   const ChunkRef r = chunk_ref(boff, cbase);
   const uint32_t t = threadIdx.x, lane = __lane_id();
   uint32_t* sw = stg[t >> 6];
-  const uint32_t len = r.valid ? r.hi - r.lo : 0u;
+  // chunks with many distinct symbols are left to k_mtf_row (their ranks mostly miss the
+  // register words)
+  const bool mine = r.valid && siglen[r.gidx] <= kRowMin;
+  const uint32_t len = mine ? r.hi - r.lo : 0u;
   const uint32_t* src = init + (size_t)(r.valid ? r.gidx : 0u) * 64;
   uint32_t W[kRegW];
 #pragma unroll
@@ -365,12 +373,27 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
   // chunk g's ranks go to ranks[g * kChunk, g * kChunk + len): chunk-aligned, so the wave's
   // lanes complete rank words together and every window goes out as full 64-byte segments
   const uint32_t g0 = (uint32_t)__shfl((int)r.gidx, 0, 64);
+  // the next window's 64 bytes are loaded while this one is processed (a lane's loads hit a
+  // line of its own, so their latency is exposed unless it overlaps the steps)
+  uint4 cur[4], nxt[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    cur[k] = make_uint4(0, 0, 0, 0);
+    if (16u * k < len) __builtin_memcpy(&cur[k], L + r.lo + 16 * k, 16);  // unaligned; the column is padded
+  }
   for (uint32_t w0 = 0; w0 < kChunk; w0 += 64) {
     if (__ballot(len > w0) == 0) break;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      nxt[k] = make_uint4(0, 0, 0, 0);
+      if (w0 + 64 + 16u * k < len) __builtin_memcpy(&nxt[k], L + r.lo + w0 + 64 + 16 * k, 16);
+    }
     for (uint32_t jj = 0; jj < 64; jj += 16) {
       const uint32_t j0 = w0 + jj;
-      uint4 q = make_uint4(0, 0, 0, 0);
-      if (j0 < len) __builtin_memcpy(&q, L + r.lo + j0, 16);  // unaligned; the column is padded
+      const uint4 q = cur[0];
+      cur[0] = cur[1];  // register moves: no dynamic indexing of cur
+      cur[1] = cur[2];
+      cur[2] = cur[3];
       const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int e = 0; e < 16; e++)
@@ -387,11 +410,165 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
       }
     }
     wave_sync();
+#pragma unroll
+    for (int k = 0; k < 4; k++) cur[k] = nxt[k];
   }
-  if (!r.valid) return;
+  if (!mine) return;
   lead[r.gidx] = seen ? ld : 0xffffffffu;  // all-zero chunk marker
   trail[r.gidx] = z;
   inner[r.gidx] = cnt;
+}
+
+// Chunks with more than kRowMin distinct symbols (high-entropy blocks: most ranks lie past
+// k_mtf_run's register words, where its list search and shift walk LDS word by word), listed
+// as (block << 11 | chunk).
+__global__ void __launch_bounds__(kT) k_mtf_pick(const uint32_t* __restrict__ boff, const uint32_t* __restrict__ cbase,
+                                                 const uint32_t* __restrict__ siglen, uint32_t* __restrict__ hi_list,
+                                                 uint32_t* __restrict__ n_hi) {
+  const ChunkRef r = chunk_ref(boff, cbase);
+  const bool hi = r.valid && siglen[r.gidx] > kRowMin;
+  const uint32_t p = wave_append(n_hi, hi);
+  if (hi) hi_list[p] = (r.b << 11) | r.c;
+}
+
+// MTF of one chunk by a row of 16 lanes: lane l holds list positions 16 l .. 16 l + 15 in four
+// words, so a symbol is found by one SWAR test per word and a ballot (the list holds every
+// symbol once: exactly one lane of the row matches), and the move to front is a one-byte
+// shift of the lanes before the match (the byte crossing a lane boundary comes from the
+// previous lane by a DPP row shift) and a partial shift in the matching lane.  A wave runs
+// four chunks in lockstep.  Ranks are staged in LDS, then stored as 16-byte words; the
+// zero-run summary is read from them afterwards.
+constexpr uint32_t kRowChunks = kT / 16;
+__global__ void __launch_bounds__(kT) k_mtf_row(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
+                                                const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
+                                                const uint32_t* __restrict__ hi_list, const uint32_t* __restrict__ n_hi,
+                                                uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
+                                                uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
+  // (rows 4 words apart: the four rows of a wave read and write different banks)
+  __shared__ uint32_t sym[kRowChunks][kChunk / 4 + 4];  // the chunk's BWT bytes
+  __shared__ uint32_t rk[kRowChunks][kChunk / 4 + 4];   // its ranks
+  __shared__ uint32_t part[kRowChunks][16][4];      // zero-run summaries of the lanes' slices
+  const uint32_t nh = *n_hi;
+  if (blockIdx.x * kRowChunks >= nh) return;
+  const uint32_t t = threadIdx.x, lane = __lane_id(), row = lane >> 4, rl = lane & 15;
+  const uint32_t ci = (t >> 4);  // chunk of this row within the workgroup
+  const uint32_t i = blockIdx.x * kRowChunks + ci;
+  const bool valid = i < nh;
+  uint32_t len = 0, lo = 0, g = 0;
+  if (valid) {
+    const uint32_t e = hi_list[i], b = e >> 11, c = e & 2047u;
+    lo = boff[b] + c * kChunk;
+    len = min(boff[b + 1], lo + kChunk) - lo;
+    g = cbase[b] + c;
+  }
+  uint8_t* sb = reinterpret_cast<uint8_t*>(sym[ci]);
+  for (uint32_t j = rl; j < kChunk / 4; j += 16) {
+    uint32_t w = 0;
+    for (uint32_t k = 0; k < 4; k++)
+      if (4 * j + k < len) w |= (uint32_t)L[lo + 4 * j + k] << (8 * k);
+    sym[ci][j] = w;
+  }
+  uint32_t W0 = 0, W1 = 0, W2 = 0, W3 = 0;
+  if (valid) {
+    const uint4 q = reinterpret_cast<const uint4*>(init + (size_t)g * 64)[rl];
+    W0 = q.x, W1 = q.y, W2 = q.z, W3 = q.w;
+  }
+  __syncthreads();
+  // the wave runs to its longest chunk (uniform loop bound)
+  uint32_t wl = len;
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
+  uint8_t* rb = reinterpret_cast<uint8_t*>(rk[ci]);
+  const uint32_t rowshift = 16 * row;
+  for (uint32_t j = 0; j < wl; j++) {
+    const bool act = j < len;
+    const uint32_t c = sb[j];  // one address per row: broadcast
+    const uint32_t pat = c * 0x01010101u;
+    const uint32_t x0 = W0 ^ pat, x1 = W1 ^ pat, x2 = W2 ^ pat, x3 = W3 ^ pat;
+    const uint32_t z0 = (x0 - 0x01010101u) & ~x0 & 0x80808080u;
+    const uint32_t z1 = (x1 - 0x01010101u) & ~x1 & 0x80808080u;
+    const uint32_t z2 = (x2 - 0x01010101u) & ~x2 & 0x80808080u;
+    const uint32_t z3 = (x3 - 0x01010101u) & ~x3 & 0x80808080u;
+    const uint32_t local = z0 ? (__builtin_ctz(z0) >> 3)
+                       : z1 ? 4 + (__builtin_ctz(z1) >> 3)
+                       : z2 ? 8 + (__builtin_ctz(z2) >> 3)
+                       : z3 ? 12 + (__builtin_ctz(z3) >> 3) : 16u;
+    const uint64_t m = __ballot(act && local < 16);
+    const uint32_t rowbits = (uint32_t)(m >> rowshift) & 0xffffu;
+    const uint32_t lane0 = rowbits ? (uint32_t)__builtin_ctz(rowbits) : 16u;
+    // bytes of this lane that shift: all before the match, up to the match in its lane
+    const uint32_t nshift = !act ? 0u : rl < lane0 ? 16u : rl == lane0 ? local + 1 : 0u;
+    if (act && rl == lane0) rb[j] = (uint8_t)(16 * rl + local);
+    // the top byte of the previous lane (the symbol itself into lane 0 of the row)
+    uint32_t cin = (uint32_t)__builtin_amdgcn_mov_dpp((int)(W3 >> 24), 0x111, 0xF, 0xF, false);  // row_shr:1
+    if (rl == 0) cin = c;
+    const uint32_t s0 = (W0 << 8) | cin;
+    const uint32_t s1 = __builtin_amdgcn_alignbyte(W1, W0, 3);
+    const uint32_t s2 = __builtin_amdgcn_alignbyte(W2, W1, 3);
+    const uint32_t s3 = __builtin_amdgcn_alignbyte(W3, W2, 3);
+    auto msk = [](uint32_t n, uint32_t k) {  // bytes [0, n - 4k) of word k
+      const uint32_t b = n > 4 * k ? min(n - 4 * k, 4u) : 0u;
+      return (uint32_t)((1ull << (8 * b)) - 1ull);
+    };
+    const uint32_t m0 = msk(nshift, 0), m1 = msk(nshift, 1), m2 = msk(nshift, 2), m3 = msk(nshift, 3);
+    W0 = (s0 & m0) | (W0 & ~m0);
+    W1 = (s1 & m1) | (W1 & ~m1);
+    W2 = (s2 & m2) | (W2 & ~m2);
+    W3 = (s3 & m3) | (W3 & ~m3);
+  }
+  __syncthreads();
+  // ranks out (16-byte words) and the zero-run summary: lane rl takes ranks [64 rl, 64 rl + 64)
+  if (valid) {
+    for (uint32_t q = rl; q < kChunk / 16; q += 16)
+      if (16 * q < len) reinterpret_cast<uint4*>(ranks + (size_t)g * kChunk)[q] = reinterpret_cast<const uint4*>(rk[ci])[q];
+  }
+  {
+    uint32_t ld = 0, z = 0, cnt = 0;
+    bool seen = false;
+    const uint32_t a = 64 * rl, e = min(len, a + 64);
+    for (uint32_t j = a; j < e; j++) {
+      if (rb[j] == 0) {
+        z++;
+        continue;
+      }
+      if (!seen) {
+        ld = z;
+        seen = true;
+      } else {
+        cnt += nsym(z);
+      }
+      z = 0;
+      cnt++;
+    }
+    part[ci][rl][0] = seen ? ld : (e > a ? e - a : 0u);  // leading zeros (all, if none ranked)
+    part[ci][rl][1] = z;
+    part[ci][rl][2] = cnt;
+    part[ci][rl][3] = seen ? 1u : 0u;
+  }
+  __syncthreads();
+  if (valid && rl == 0) {  // chain the 16 slices as k_mtf_run would have walked them
+    uint32_t ld = 0, z = 0, cnt = 0;
+    bool seen = false;
+    for (uint32_t k = 0; k < 16; k++) {
+      const uint32_t pl = part[ci][k][0], pt = part[ci][k][1], pc = part[ci][k][2];
+      if (!part[ci][k][3]) {
+        z += pl;
+        continue;
+      }
+      // the slice's leading zeros end the carried run at its first ranked symbol
+      if (!seen) {
+        ld = z + pl;
+        seen = true;
+        cnt += pc;
+      } else {
+        cnt += nsym(z + pl) + pc;
+      }
+      z = pt;
+    }
+    lead[g] = seen ? ld : 0xffffffffu;
+    trail[g] = z;
+    inner[g] = cnt;
+  }
 }
 
 // 4b. per block (one wave): carried zero runs, chunk output offsets, nMTF.  The zero run
@@ -605,15 +782,14 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
     HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
   }
-  std::vector<uint32_t> hcb(nb + 1), hmo(nb + 1);
+  std::vector<uint32_t> hcb(nb + 1), hmo(nb + 1, 0u);
   uint32_t maxch = 0;
   for (uint32_t b = 0; b < nb; b++) {
     const uint32_t nch = ceil_div(hboff[b + 1] - hboff[b], kChunk);
     hcb[b + 1] = hcb[b] + nch;
     maxch = std::max(maxch, nch);
-    hmo[b] = hboff[b] + b;  // nMTF <= n + 1
+    hmo[b + 1] = (hmo[b] + (hboff[b + 1] - hboff[b]) + 1 + 7) & ~7u;  // nMTF <= n + 1; 16-byte aligned blocks
   }
-  hmo[nb] = hboff[nb] + nb;
   const uint32_t nchunks = hcb[nb];
   uint32_t* cbase = ws.u32("mtf_cbase", nb + 1);
   uint32_t* moff = ws.u32("mtf_off", nb + 1);
@@ -639,7 +815,16 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
   HIP_OK(hipGetLastError());
   k_compose<<<nb, 64 * kCW, 0, st>>>(r.boff, cbase, r.inuse, sig, siglen, init);
   HIP_OK(hipGetLastError());
-  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, init, ranks, lead, trail, inner);
+  uint32_t* hi_list = ws.u32("mtf_hilist", nchunks + 16);
+  uint32_t* n_hi = ws.u32("mtf_nhi", 16);
+  HIP_OK(hipMemsetAsync(n_hi, 0, 4, st));
+  k_mtf_pick<<<g2, kT, 0, st>>>(r.boff, cbase, siglen, hi_list, n_hi);
+  HIP_OK(hipGetLastError());
+  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, siglen, init, ranks, lead, trail, inner);
+  HIP_OK(hipGetLastError());
+  // grid for every chunk; workgroups past the picked count exit at once
+  k_mtf_row<<<ceil_div(nchunks, kRowChunks), kT, 0, st>>>(bwt, r.boff, cbase, init, hi_list, n_hi, ranks, lead, trail,
+                                                          inner);
   HIP_OK(hipGetLastError());
   k_rle2_plan<<<nb, 64, 0, st>>>(r.boff, cbase, lead, trail, inner, zin, coff, finalrun,
                                                 res.nmtf);

@@ -10,8 +10,9 @@
 //   e(i)  = r<=2 ? 1 : r==3 ? 1+last(i) : last(i)   output bytes produced by input byte i
 //   last(i) = chunk ends at i (next byte differs, end of input, or r == 254)
 // The output offset of byte i is the exclusive prefix sum of e; a chunk starts at r == 0.
-#include "stages.h"
+#include "qsa.h"
 #include "scan.h"
+#include "stages.h"
 
 namespace bzg {
 
@@ -33,23 +34,113 @@ __device__ __forceinline__ void load16(const uint8_t* __restrict__ x, uint64_t n
   }
 }
 
-// Pass 1: per tile, the largest run-start position in the tile (0 if none).
-__global__ void __launch_bounds__(kT) k_run_starts(const uint8_t* __restrict__ x, uint64_t n,
-                                                   uint32_t* __restrict__ tile_max) {
-  __shared__ uint32_t sh[kT / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
-  uint8_t v[kPer];
-  load16(x, n, base, v);
-  uint8_t prev = (base > 0 && base - 1 < n) ? x[base - 1] : 0;
-  uint32_t m = 0;
+// Per thread: its run-start bits and whether some byte of it ends a run of 4 (x[i-3..i]
+// equal; the 3 bytes before the thread come from one aligned word).  Without such a byte every
+// byte of the thread sits at chunk offset r <= 2: it emits itself and starts a chunk iff it
+// starts a run, whatever run enters the thread.  On text ~99% of threads are like that.
+struct RunBits {
+  uint32_t starts;  // bit k: byte base + k starts a run
+  uint32_t last1;   // 1 + the thread's last run start (0: none)
+  uint32_t nvalid;  // bytes of the thread below n
+  bool longrun;
+};
+__device__ __forceinline__ RunBits run_bits(const uint8_t* __restrict__ x, uint64_t n, uint64_t base,
+                                            const uint8_t (&v)[kPer]) {
+  uint32_t pw = 0;  // x[base - 4 .. base - 1]; base is a multiple of 16
+  if (base >= 4 && base <= n) pw = *reinterpret_cast<const uint32_t*>(x + base - 4);
+  uint32_t a3 = (pw >> 8) & 0xffu, a2 = (pw >> 16) & 0xffu, a1 = pw >> 24;  // x[i-3], x[i-2], x[i-1]
+  RunBits r{0u, 0u, base < n ? (uint32_t)min<uint64_t>(kPer, n - base) : 0u, false};
+  uint32_t lng = 0;
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
-    uint64_t i = base + k;
-    if (i < n && (i == 0 || v[k] != prev)) m = (uint32_t)i;
-    prev = v[k];
+    const uint64_t i = base + k;
+    const uint32_t c = v[k];
+    const bool ok = i < n;
+    if (ok && (i == 0 || c != a1)) {
+      r.starts |= 1u << k;
+      r.last1 = (uint32_t)i + 1u;
+    }
+    lng |= (ok && i >= 3 && c == a1 && c == a2 && c == a3) ? 1u : 0u;
+    a3 = a2;
+    a2 = a1;
+    a1 = c;
   }
-  m = block_incl_max(m, sh);
-  if (threadIdx.x == kT - 1) tile_max[blockIdx.x] = m;
+  r.longrun = lng != 0;
+  return r;
+}
+
+// Pass 1: per tile, its last run start (for the carry scan) and its output size up to the
+// part that depends on the run entering the tile:  S = output bytes of the bytes from the
+// tile's first run start on, h = the bytes before it (they continue the run that starts at the
+// carried run start), ends = that run ends at the tile's byte h - 1.  k_rle_fix adds the h
+// bytes' output once the carries are known (closed form).  tinfo = S | h << 16 | ends << 31.
+__global__ void __launch_bounds__(kT) k_rle_count(const uint8_t* __restrict__ x, uint64_t n,
+                                                  uint32_t* __restrict__ tmax, uint32_t* __restrict__ tinfo) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t thr[kT];
+  const uint64_t ts = (uint64_t)blockIdx.x * kTile, base = ts + (uint64_t)threadIdx.x * kPer;
+  uint8_t v[kPer];
+  load16(x, n, base, v);
+  const RunBits rb = run_bits(x, n, base, v);
+  const uint32_t len = (uint32_t)min<uint64_t>(kTile, n - ts);
+  const bool general = __syncthreads_or(rb.longrun);
+  const uint32_t incl = block_incl_max(rb.last1, sh);
+  if (threadIdx.x == kT - 1) tmax[blockIdx.x] = incl ? incl - 1u : 0u;
+  if (!general) {  // every byte emits itself
+    if (threadIdx.x == 0) tinfo[blockIdx.x] = len;
+    return;
+  }
+  thr[threadIdx.x] = incl;
+  __syncthreads();
+  uint32_t m1 = threadIdx.x ? thr[threadIdx.x - 1] : 0u;  // 1 + run start of the byte (0: before the tile)
+  const uint8_t next_after = (base + kPer < n) ? x[base + kPer] : 0;
+  uint32_t s = 0, h = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t i = base + k;
+    if (i >= n) break;
+    if ((rb.starts >> k) & 1u) m1 = (uint32_t)i + 1u;
+    if (m1 == 0) {
+      h++;
+    } else if (!rb.longrun) {
+      s++;
+    } else {
+      uint32_t r = (uint32_t)i - (m1 - 1u);
+      if (r >= 255u) r %= 255u;
+      const uint8_t nx = (k + 1 < kPer) ? v[k + 1] : next_after;
+      const bool last = (i + 1 >= n) || (nx != v[k]) || (r == 254);
+      s += r <= 2 ? 1u : (r == 3 ? 1u + (last ? 1u : 0u) : (last ? 1u : 0u));
+    }
+  }
+  uint32_t tot;
+  block_incl_sum(s | (h << 16), sh, &tot);
+  if (threadIdx.x == 0) {
+    const uint32_t H = tot >> 16;
+    const uint32_t ends = (H < len) || (ts + len >= n) || (x[ts + len] != x[ts + len - 1]);
+    tinfo[blockIdx.x] = (tot & 0xffffu) | (H << 16) | (ends << 31);
+  }
+}
+
+// Output bytes of chunk offsets [a, a + h) of one run (r = offset mod 255), the run ending at
+// offset a + h - 1 iff `ends`: offsets with r <= 3 emit their byte, r == 254 closes a chunk
+// (count byte), and the run's end closes a chunk of 4 or more.
+__device__ __forceinline__ uint64_t rle_cnt(uint64_t x, uint32_t lo, uint32_t w) {
+  const uint64_t q = x / 255u, r = x % 255u;
+  return q * w + (uint64_t)min<uint64_t>(r > lo ? r - lo : 0u, w);
+}
+__global__ void k_rle_fix(const uint32_t* __restrict__ carry, const uint32_t* __restrict__ tinfo, uint64_t tiles,
+                          uint32_t* __restrict__ tsum) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tiles) return;
+  const uint32_t info = tinfo[t], h = (info >> 16) & 0x1fffu;
+  uint64_t e = 0;
+  if (h) {
+    const uint64_t a = t * kTile - carry[t], b = a + h;
+    const uint32_t re = (uint32_t)((b - 1) % 255u);
+    e = rle_cnt(b, 0, 4) - rle_cnt(a, 0, 4) + rle_cnt(b, 254, 1) - rle_cnt(a, 254, 1) +
+        (((info >> 31) && re >= 3 && re <= 253) ? 1u : 0u);
+  }
+  tsum[t] = (info & 0xffffu) + (uint32_t)e;
 }
 
 struct ByteInfo {
@@ -58,22 +149,11 @@ struct ByteInfo {
   bool last;  // chunk ends here
 };
 
-// Recomputes per-byte info for this thread's 16 bytes given the tile's run-start carry.
-// `thr` needs kT words.
-__device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_t n, uint64_t base,
-                                          const uint8_t (&v)[kPer], uint32_t carry_start,
-                                          uint32_t* sh, uint32_t* thr, ByteInfo (&bi)[kPer]) {
-  uint8_t prev = (base > 0 && base - 1 < n) ? x[base - 1] : 0;
-  uint32_t m = 0;
-  uint32_t st[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    uint64_t i = base + k;
-    if (i < n && (i == 0 || v[k] != prev)) m = (uint32_t)i;
-    st[k] = m;
-    prev = v[k];
-  }
-  const uint32_t incl = block_incl_max(m, sh);
+// The run start carried into this thread (block max scan over the tile's run starts from the
+// tile's carry); every thread of the workgroup must call it.  `thr` needs kT words.
+__device__ __forceinline__ uint32_t run_before(uint32_t last_start, uint32_t carry_start, uint32_t* sh,
+                                               uint32_t* thr) {
+  const uint32_t incl = block_incl_max(last_start, sh);
   thr[threadIdx.x] = incl;
   __syncthreads();
   uint32_t before = carry_start;
@@ -82,11 +162,20 @@ __device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_
     before = before > w ? before : w;
   }
   __syncthreads();
+  return before;
+}
+
+// Per-byte info of this thread's 16 bytes given the run start carried into the thread.
+__device__ __forceinline__ void byte_info_from(const uint8_t* __restrict__ x, uint64_t n, uint64_t base,
+                                               const uint8_t (&v)[kPer], uint32_t before, ByteInfo (&bi)[kPer]) {
+  uint8_t prev = (base > 0 && base - 1 < n) ? x[base - 1] : 0;
+  uint32_t rs = before;
   const uint8_t next_after = (base + kPer < n) ? x[base + kPer] : 0;
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     uint64_t i = base + k;
-    uint32_t rs = st[k] > before ? st[k] : before;
+    if (i < n && (i == 0 || v[k] != prev)) rs = (uint32_t)i;
+    prev = v[k];
     uint32_t r = (uint32_t)(i - rs) % 255u;  // run offsets fit 32 bits (n < 2^32)
     uint8_t nx = (k + 1 < kPer) ? v[k + 1] : next_after;
     bool last = (i + 1 >= n) || (nx != v[k]) || (r == 254);
@@ -96,23 +185,19 @@ __device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_
   }
 }
 
-// Pass 2: per tile, total output bytes.
-__global__ void __launch_bounds__(kT) k_emit_count(const uint8_t* __restrict__ x, uint64_t n,
-                                                   const uint32_t* __restrict__ carry,
-                                                   uint32_t* __restrict__ tile_sum) {
-  __shared__ uint32_t sh[kT / 64];
-  __shared__ uint32_t thr[kT];
-  const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
-  uint8_t v[kPer];
-  load16(x, n, base, v);
-  ByteInfo bi[kPer];
-  byte_info(x, n, base, v, carry[blockIdx.x], sh, thr, bi);
-  uint32_t s = 0;
+// Both of the above (every thread must call it).
+__device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_t n, uint64_t base,
+                                          const uint8_t (&v)[kPer], uint32_t carry_start,
+                                          uint32_t* sh, uint32_t* thr, ByteInfo (&bi)[kPer]) {
+  uint8_t prev = (base > 0 && base - 1 < n) ? x[base - 1] : 0;
+  uint32_t m = 0;
 #pragma unroll
-  for (int k = 0; k < kPer; k++) s += bi[k].e;
-  uint32_t tot;
-  block_incl_sum(s, sh, &tot);
-  if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
+  for (int k = 0; k < kPer; k++) {
+    uint64_t i = base + k;
+    if (i < n && (i == 0 || v[k] != prev)) m = (uint32_t)i;
+    prev = v[k];
+  }
+  byte_info_from(x, n, base, v, run_before(m, carry_start, sh, thr), bi);
 }
 
 // Pass 3: write block bytes, chunk-start bitmap and chunk-start -> input position map.
@@ -132,11 +217,20 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
   const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
   uint8_t v[kPer];
   load16(x, n, base, v);
+  const RunBits rb = run_bits(x, n, base, v);
+  // per-byte chunk info only for threads holding a run of 4+ (the carry scan only when the
+  // tile has one): the others emit their bytes unchanged
   ByteInfo bi[kPer];
-  byte_info(x, n, base, v, carry[blockIdx.x], sh, thr, bi);
-  uint32_t s = 0;
+  if (__syncthreads_or(rb.longrun)) {
+    const uint32_t before = run_before(rb.last1 ? rb.last1 - 1u : 0u, carry[blockIdx.x], sh, thr);
+    if (rb.longrun) byte_info_from(x, n, base, v, before, bi);
+  }
+  uint32_t s = rb.nvalid;
+  if (rb.longrun) {
+    s = 0;
 #pragma unroll
-  for (int k = 0; k < kPer; k++) s += bi[k].e;
+    for (int k = 0; k < kPer; k++) s += bi[k].e;
+  }
   uint32_t tot;
   uint32_t incl = block_incl_sum(s, sh, &tot);
   const uint32_t t0 = out_base[blockIdx.x];
@@ -145,26 +239,39 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
   // chunk-start bits of this thread's outputs span <= 2 words (<= 32 output bytes)
   const uint32_t w0 = pos >> 5;
   uint32_t bits0 = 0, bits1 = 0;
+  if (!rb.longrun) {
+    const uint32_t sh5 = pos & 31u;
+    bits0 = rb.starts << sh5;
+    bits1 = sh5 ? rb.starts >> (32u - sh5) : 0u;
+    if (base < n && n - base <= kPer) *last_len1 = (rb.starts >> (n - 1 - base)) & 1u;
+    if (out != nullptr) {
+      const uint32_t lp = pos - t0 + lofs;
 #pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint64_t i = base + k;
-    if (i >= n) break;
-    const ByteInfo b = bi[k];
-    if (i + 1 == n) *last_len1 = (b.r == 0) ? 1u : 0u;
-    if (b.r == 0) {
-      const uint32_t w = pos >> 5;
-      if (w == w0) bits0 |= 1u << (pos & 31);
-      else bits1 |= 1u << (pos & 31);
+      for (int k = 0; k < kPer; k++)
+        if ((uint32_t)k < rb.nvalid) ob[lp + k] = v[k];
     }
-    const uint32_t lp = pos - t0 + lofs;
-    if (out == nullptr) {  // chunk map only (seg_map_stage): no block bytes
-    } else if (b.r <= 3) {
-      ob[lp] = v[k];
-      if (b.r == 3 && b.last) ob[lp + 1] = 0;
-    } else if (b.last) {
-      ob[lp] = (uint8_t)(b.r - 3);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint64_t i = base + k;
+      if (i >= n) break;
+      const ByteInfo b = bi[k];
+      if (i + 1 == n) *last_len1 = (b.r == 0) ? 1u : 0u;
+      if (b.r == 0) {
+        const uint32_t w = pos >> 5;
+        if (w == w0) bits0 |= 1u << (pos & 31);
+        else bits1 |= 1u << (pos & 31);
+      }
+      const uint32_t lp = pos - t0 + lofs;
+      if (out == nullptr) {  // chunk map only (seg_map_stage): no block bytes
+      } else if (b.r <= 3) {
+        ob[lp] = v[k];
+        if (b.r == 3 && b.last) ob[lp + 1] = 0;
+      } else if (b.last) {
+        ob[lp] = (uint8_t)(b.r - 3);
+      }
+      pos += b.e;
     }
-    pos += b.e;
   }
   if (bits0) atomicOr(&cb[w0 - (t0 >> 5)], bits0);
   if (bits1) atomicOr(&cb[w0 + 1 - (t0 >> 5)], bits1);
@@ -576,13 +683,61 @@ __global__ void __launch_bounds__(kT) k_period(const uint8_t* __restrict__ blk, 
       for (uint32_t i = i0 + threadIdx.x; i < n - p && i < i0 + kT * 16; i += kT)
         if (blk[lo + i] != blk[lo + i + p]) bad = 1;
       __syncthreads();
-      if (bad) break;
+      const bool stop = bad;
+      __syncthreads();  // every thread has read the flag before the next chunk may set it
+      if (stop) break;
     }
     __syncthreads();
     if (!bad) { result = p; break; }
     __syncthreads();
   }
   if (threadIdx.x == 0) period[b] = result;
+}
+
+// Quasi-periodic blocks (qsa.h): the smallest period p <= kQsaMaxPeriod, 2p <= n, of a block
+// that is not a power of a shorter word, when p does not divide n (else 0).  Thread t tests
+// p = t + 1 on the block's first 64 positions; the candidates left are verified in ascending
+// order by the whole workgroup (text blocks rarely leave any).
+__global__ void __launch_bounds__(kT) k_qperiod(const uint8_t* __restrict__ blk, const uint32_t* __restrict__ boff,
+                                                const uint32_t* __restrict__ period, uint32_t* __restrict__ qper) {
+  static_assert(kQsaMaxPeriod <= (uint32_t)kT, "one candidate period per thread");
+  __shared__ uint64_t cand[kT / 64];
+  __shared__ int bad;
+  const uint32_t b = blockIdx.x, lo = boff[b], n = boff[b + 1] - lo;
+  const uint8_t* t = blk + lo;
+  const uint32_t pmax = min(kQsaMaxPeriod, n / 2);
+  if (period[b] != n || n < 4) {  // periodic blocks go to A5
+    if (threadIdx.x == 0) qper[b] = 0;
+    return;
+  }
+  const uint32_t p = threadIdx.x + 1;
+  bool ok = p <= pmax;
+  for (uint32_t i = 0; ok && i < min(64u, n - p); i++) ok = t[i] == t[i + p];
+  const uint64_t m = __ballot(ok);
+  if (__lane_id() == 0) cand[threadIdx.x >> 6] = m;
+  __syncthreads();
+  uint32_t found = 0;
+  for (uint32_t w = 0; w < kT / 64 && !found; w++) {
+    uint64_t mw = cand[w];
+    while (mw && !found) {
+      const uint32_t q = w * 64 + (uint32_t)__builtin_ctzll(mw) + 1;
+      mw &= mw - 1;
+      if (threadIdx.x == 0) bad = 0;
+      __syncthreads();
+      for (uint32_t i0 = 0; i0 < n - q; i0 += kT * 16) {
+        for (uint32_t i = i0 + threadIdx.x; i < n - q && i < i0 + kT * 16; i += kT)
+          if (t[i] != t[i + q]) bad = 1;
+        __syncthreads();
+        const bool stop = bad;
+        __syncthreads();  // every thread has read the flag before the next chunk may set it
+        if (stop) break;
+      }
+      __syncthreads();
+      if (!bad) found = q;  // the smallest period of the block
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) qper[b] = (found && n % found != 0) ? found : 0u;
 }
 
 }  // namespace
@@ -599,6 +754,7 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   const uint64_t mcap = n + n / 4 + 64;
   uint32_t* tmax = ws.u32("rle_tmax", tiles + 64);
   uint32_t* tsum = ws.u32("rle_tsum", tiles + 64);
+  uint32_t* tinfo = ws.u32("rle_tinfo", tiles + 64);
   uint32_t* scratch = ws.u32("rle_scan", scan_scratch_words(tiles) + 64);
   uint32_t* mtot = ws.u32("rle_m", 16);
   uint8_t* blk = ws.u8("blk", mcap + 64);
@@ -608,10 +764,10 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   uint32_t* binst = ws.u32("binst", max_blocks + 2);
   uint32_t* nbl = mtot + 4;
 
-  k_run_starts<<<tiles, kT, 0, st>>>(d_in, n, tmax);
+  k_rle_count<<<tiles, kT, 0, st>>>(d_in, n, tmax, tinfo);
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Max, true, tmax, tmax, tiles, nullptr, scratch, st);
-  k_emit_count<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum);
+  k_rle_fix<<<ceil_div64(tiles, kT), kT, 0, st>>>(tmax, tinfo, tiles, tsum);
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
   HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
@@ -680,13 +836,14 @@ void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t s
   const uint64_t mcap = n + n / 4 + 64;
   uint32_t* tmax = ws.u32("seg_tmax", tiles + 64);
   uint32_t* tsum = ws.u32("seg_tsum", tiles + 64);
+  uint32_t* tinfo = ws.u32("seg_tinfo", tiles + 64);
   uint32_t* scratch = ws.u32("seg_scan", scan_scratch_words(tiles) + 64);
   uint32_t* mtot = ws.u32("seg_m", 16);
   uint32_t* cbits = ws.u32("seg_cbits", mcap / 32 + 64);
-  k_run_starts<<<tiles, kT, 0, st>>>(d_in, n, tmax);
+  k_rle_count<<<tiles, kT, 0, st>>>(d_in, n, tmax, tinfo);
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Max, true, tmax, tmax, tiles, nullptr, scratch, st);
-  k_emit_count<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum);
+  k_rle_fix<<<ceil_div64(tiles, kT), kT, 0, st>>>(tmax, tinfo, tiles, tsum);
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
   HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
@@ -742,6 +899,9 @@ void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st) {
   k_ninuse<<<ceil_div(B, kT), kT, 0, st>>>(res.inuse, B, res.ninuse);
   HIP_OK(hipGetLastError());
   k_period<<<B, kT, 0, st>>>(res.blk, res.boff, res.period);
+  HIP_OK(hipGetLastError());
+  res.qper = ws.u32("qper", B + 2);
+  k_qperiod<<<B, kT, 0, st>>>(res.blk, res.boff, res.period, res.qper);
   HIP_OK(hipGetLastError());
   copyrank_count_stage(res, ws, st);
 }

@@ -3,8 +3,8 @@
 // Replaces the reference's divsufsort (blocksort.c:1503-1545).  For an aperiodic block all
 // rotations are distinct, so any correct sort yields the reference's last column and
 // origPtr (parity fact 3).  Periodic blocks (w^k) are reduced to their
-// primitive root w; the tie rank among the k identical copies of rotation 0 is resolved on
-// the host (resolver.cpp, A5).
+// primitive root w; the rank of rotation 0 among the k identical copies is the copy rank of
+// A5 (origptr.hip on the device, copyrank.cpp on the host).
 //
 // The sort is a string sort keyed directly by the block text (read through L2: a block is
 // <= 900 kB and the workgroups of an XCD walk the blocks in order), not by rank arrays that
@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <string>
 
+#include "qsa.h"
 #include "scan.h"
 #include "sort_common.h"
 
@@ -32,7 +33,11 @@ namespace bzg {
 namespace {
 
 constexpr int kT = 256;
-constexpr uint32_t kBig = 256;        // buckets larger than this are split by S1 byte passes
+#ifndef BZG_BIG
+#define BZG_BIG 256
+#endif
+constexpr uint32_t kBig = BZG_BIG;    // buckets larger than this are split by S1 byte passes
+static_assert(kBig == 128 || kBig == 256, "S2 classes cover up to 128 or 256 rotations");
 #ifndef BZG_DTILE
 #define BZG_DTILE 2048
 #endif
@@ -46,7 +51,7 @@ constexpr uint32_t kSG = BZG_SG;      // S1 groups up to this size are packed in
 // size classes: 0..5 go to S2 (2-8 .. 129-256), 6 / 7 to the next S1 pass (packed / tiled),
 // 8 (still big after kDBig characters) to the doubling fallback
 constexpr int kNCls = 8;
-constexpr uint32_t kClsMax[7] = {8, 16, 32, 64, 128, 256, kSG};
+constexpr uint32_t kClsMax[7] = {8, 16, 32, 64, 128, kBig, kSG};
 constexpr uint32_t kClsDeep = 8;
 // S2 workgroups walk the (block-ordered) group lists XCD by XCD: each XCD's L2 then holds the
 // text and slots of its own few blocks instead of every block's
@@ -56,7 +61,7 @@ constexpr uint32_t kClsDeep = 8;
 __device__ __forceinline__ uint32_t s2_wg() { return BZG_S2_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; }
 
 __host__ __device__ __forceinline__ uint32_t size_cls(uint32_t n) {
-  return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= 256 ? 5u : n <= kSG ? 6u : 7u;
+  return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= kBig ? 5u : n <= kSG ? 6u : 7u;
 }
 
 struct SortOut {
@@ -1851,26 +1856,100 @@ __global__ void k_rank0_isa(const uint32_t* __restrict__ ulist, uint32_t n, cons
 
 }  // namespace
 
+// ---- quasi-periodic blocks (qsa.h): the analytic order of qsa_plan, written out.  The block's
+// unit is a single rotation for the sort (k_init_units finishes it at once); this kernel then
+// writes the block's last column and origPtr.  Table of block q at tab + Q.tab: cum (p + 1),
+// ord (p), lo (nspec), srot (nspec).
+struct QBlock {
+  uint32_t toff, n, p, desc, nspec, tab, unit, pad;
+};
+__global__ void __launch_bounds__(kT) k_qsa(const QBlock* __restrict__ qb, const uint32_t* __restrict__ tab,
+                                            const uint8_t* __restrict__ text, uint8_t* __restrict__ bwt,
+                                            uint32_t* __restrict__ rank0) {
+  const QBlock Q = qb[blockIdx.y];
+  const uint32_t* cum = tab + Q.tab;
+  const uint32_t* ord = cum + Q.p + 1;
+  const uint32_t* lo = ord + Q.p;
+  const uint32_t* srot = lo + Q.nspec;
+  const uint8_t* t = text + Q.toff;
+  const uint32_t nn = Q.n - Q.p + 1;  // normal rotations 0 .. n - p
+  for (uint32_t y = blockIdx.x * kT + threadIdx.x; y < nn + Q.nspec; y += gridDim.x * kT) {
+    uint32_t rot, fin;
+    if (y < nn) {
+      const uint32_t k = upper_idx(cum, Q.p, y);
+      const uint32_t o = y - cum[k], cnt = cum[k + 1] - cum[k];
+      rot = ord[k] + (Q.desc ? cnt - 1 - o : o) * Q.p;
+      uint32_t a = 0, b = Q.nspec;  // specials placed before normal y: lo[j] <= y
+      while (a < b) {
+        const uint32_t m = (a + b) >> 1;
+        if (lo[m] <= y) a = m + 1;
+        else b = m;
+      }
+      fin = y + a;
+    } else {
+      const uint32_t j = y - nn;
+      rot = srot[j];
+      fin = lo[j] + j;
+    }
+    bwt[Q.toff + fin] = t[rot == 0 ? Q.n - 1 : rot - 1];
+    if (rot == 0) rank0[Q.unit] = fin;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& h_boff,
                const std::vector<uint32_t>& h_period, uint8_t* bwt, uint32_t* rank0, SortStats* stats,
-               hipStream_t st) {
+               hipStream_t st, const uint32_t* h_qper) {
   const uint32_t nb = r.nblocks;
   if (nb == 0) return;
   if (nb > 0xffffu) throw HipFailure(hipErrorInvalidValue);  // S2 keys carry 16-bit unit ids
   std::vector<Unit> hu(nb);
   uint64_t S = 0;
   uint32_t maxlen = 0;
-  std::vector<uint32_t> periodic;
+  std::vector<uint32_t> periodic, quasi;
   for (uint32_t b = 0; b < nb; b++) {
     const uint32_t n_b = h_boff[b + 1] - h_boff[b];
+    maxlen = std::max(maxlen, n_b);
+    if (h_qper && h_qper[b]) {  // ordered analytically (k_qsa): one slot for the sort
+      hu[b] = Unit{(uint32_t)S, 1u, h_boff[b], 1u};
+      quasi.push_back(b);
+      S += 1;
+      continue;
+    }
     hu[b] = Unit{(uint32_t)S, h_period[b], h_boff[b], n_b / h_period[b]};
     if (hu[b].k > 1) periodic.push_back(b);
     S += h_period[b];
-    maxlen = std::max(maxlen, n_b);
   }
   Unit* units = ws.typed<Unit>("sort_units", nb);
   HIP_OK(hipMemcpyAsync(units, hu.data(), sizeof(Unit) * nb, hipMemcpyHostToDevice, st));
+  // plans of the quasi-periodic blocks from their first period (host, qsa.cpp)
+  std::vector<QBlock> hq;
+  std::vector<uint32_t> hqt;
+  QBlock* dq = nullptr;
+  uint32_t* dqt = nullptr;
+  uint32_t qmax = 0;
+  if (!quasi.empty()) {
+    std::vector<uint8_t> wbuf(quasi.size() * kQsaMaxPeriod);
+    for (size_t j = 0; j < quasi.size(); j++)
+      HIP_OK(hipMemcpyAsync(wbuf.data() + j * kQsaMaxPeriod, r.blk + h_boff[quasi[j]], h_qper[quasi[j]],
+                            hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (size_t j = 0; j < quasi.size(); j++) {
+      const uint32_t b = quasi[j], n_b = h_boff[b + 1] - h_boff[b], p = h_qper[b];
+      QsaPlan plan;
+      qsa_plan(wbuf.data() + j * kQsaMaxPeriod, p, n_b, plan);
+      hq.push_back(QBlock{h_boff[b], n_b, p, plan.desc ? 1u : 0u, p - 1, (uint32_t)hqt.size(), b, 0u});
+      hqt.insert(hqt.end(), plan.cum.begin(), plan.cum.end());
+      hqt.insert(hqt.end(), plan.ord.begin(), plan.ord.end());
+      hqt.insert(hqt.end(), plan.lo.begin(), plan.lo.end());
+      hqt.insert(hqt.end(), plan.srot.begin(), plan.srot.end());
+      qmax = std::max(qmax, n_b);
+    }
+    dq = ws.typed<QBlock>("sort_qblk", hq.size());
+    dqt = ws.u32("sort_qtab", hqt.size() + 16);
+    HIP_OK(hipMemcpyAsync(dq, hq.data(), sizeof(QBlock) * hq.size(), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(dqt, hqt.data(), 4 * hqt.size(), hipMemcpyHostToDevice, st));
+  }
 
   SortBufs B{};
   B.sa = ws.u32("sort_sa", S + 16);
@@ -2208,6 +2287,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     HIP_OK(hipGetLastError());
     k_rank0_isa<<<grid(fb_units.size()), kT, 0, st>>>(ulist, (uint32_t)fb_units.size(), units, B.isa, rank0);
     HIP_OK(hipGetLastError());
+  }
+  if (!quasi.empty()) {
+    k_qsa<<<dim3(std::min<uint32_t>(ceil_div(qmax, kT), 1024u), (unsigned)hq.size()), kT, 0, st>>>(dq, dqt, r.blk, bwt,
+                                                                                                 rank0);
+    HIP_OK(hipGetLastError());  // (the plan tables were copied before the first counter read-back)
   }
   if (!periodic.empty()) {  // periodic roots: the root's last column repeated k times
     uint32_t* plist = ws.u32("sort_plist", periodic.size() + 16);

@@ -66,6 +66,7 @@ struct Rle1Result {
   uint32_t* ninuse = nullptr;
   uint32_t* period = nullptr;   // primitive period of each block
   uint32_t* bq = nullptr;       // B* offsets of each periodic block's root (origptr.hip)
+  uint32_t* qper = nullptr;     // smallest period of a quasi-periodic block (qsa.h), else 0
 };
 void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool final_batch,
                 bool tail_merge, Rle1Result& res, hipStream_t st);
@@ -106,9 +107,10 @@ struct SortStats {
   uint64_t unsorted_elems = 0;  // sum over iterations of elements in unsorted groups
   int s2_iters = 0;             // S2 rounds of run emission
 };
+// h_qper (optional): r.qper on the host; those blocks are ordered analytically (qsa.h).
 void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& h_boff,
                const std::vector<uint32_t>& h_period, uint8_t* bwt, uint32_t* rank0,
-               SortStats* stats, hipStream_t st);
+               SortStats* stats, hipStream_t st, const uint32_t* h_qper = nullptr);
 
 // ---- stage A6 ------------------------------------------------------------------------
 struct MtfResult {

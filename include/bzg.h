@@ -64,6 +64,8 @@ uint64_t bzg_bound(uint64_t n);
 int bzg_stage_rle1(const void *src, uint64_t n, int level, int tail_merge, uint8_t *blocks, uint64_t blocks_cap,
                    uint32_t *offsets, uint32_t *crcs, uint32_t *nblocks, uint32_t max_blocks);
 int bzg_stage_bwt(const uint8_t *blocks, const uint32_t *offsets, uint32_t nblocks, uint8_t *bwt, int32_t *origptr);
+/* bzg_stage_mtf: block b's nmtf[b] values at mtfv[mtf_offsets[b]] (offsets 8-aligned); mtfv
+ * holds offsets[nblocks] + 8 * nblocks + 16 values. */
 int bzg_stage_mtf(const uint8_t *bwt, const uint32_t *offsets, uint32_t nblocks, uint16_t *mtfv,
                   uint32_t *mtf_offsets, uint32_t *nmtf, uint32_t *freq);
 /* BZ2_hbMakeCodeLengths (reference huffman.c:63-148) on the GPU for ntables tables: freq holds
@@ -71,9 +73,16 @@ int bzg_stage_mtf(const uint8_t *bwt, const uint32_t *offsets, uint32_t nblocks,
 int bzg_stage_code_lengths(const uint32_t *freq, const int32_t *alpha, uint32_t ntables, int max_len, uint8_t *lens);
 
 /* origPtr the reference assigns to one exactly periodic block w^k (SURVEY.md 8a row A5;
- * host-side replay of the reference's divsufsort tie order, bzip2_amd/csrc/resolver.cpp).
+ * the copy-rank model of bzip2_amd/csrc/copyrank.cpp: closed form when the root has one B*
+ * suffix, else a replay of the reference's divsufsort passes on the root).
  * Returns -1 on failure.  Needs no GPU. */
 int32_t bzg_periodic_origptr(const uint8_t *block, int32_t n);
+
+/* BWT and origPtr of a quasi-periodic block (smallest period p <= 256 with 2p <= n not
+ * dividing n, e.g. the last block of a single-repeated-byte input), computed on the host by the
+ * analytic order of bzip2_amd/csrc/qsa.cpp that the GPU sort uses for such blocks (k_qsa).
+ * Returns p, or 0 (nothing written) when the block is not quasi-periodic.  Needs no GPU. */
+uint32_t bzg_qperiodic_bwt(const uint8_t *block, uint32_t n, uint8_t *bwt, uint32_t *origptr);
 
 /* Timing of the last bzg_compress_device call, per stage, from HIP events (ms). */
 typedef struct {

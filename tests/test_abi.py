@@ -185,6 +185,38 @@ def test_periodic_origptr_fuzz_wide(lib):
         assert B.periodic_origptr(blk) == O.ref_blocksort(blk)[1], (len(w), w[:24], len(blk) // len(w))
 
 
+def test_qperiodic_bwt_host_matches_oracle(lib):
+    """Analytic order of quasi-periodic blocks (qsa.cpp, the plan the GPU sort writes out with
+    k_qsa) against the oracle's BWT, and against the reference build when present: RLE1 shapes
+    of a repeated byte, random roots of 2..256 bytes with every tail length class."""
+    from tests import oracles as O
+    import random
+    rng = random.Random(2718)
+    cases = [bytes([c] * 4 + [0xFB]) * k + bytes([c]) * r for c in (0, 0x61, 0xFF) for k in (2, 9, 4000)
+             for r in (1, 2, 3)]
+    for _ in range(200):
+        w = bytes(rng.randrange(rng.choice([2, 3, 4, 256])) for _ in range(rng.randint(2, 256)))
+        k = rng.randint(2, max(2, 12_000 // len(w)))
+        cases.append(w * k + w[: rng.randint(1, len(w) - 1)])
+    seen = 0
+    for blk in cases:
+        q = B.qperiodic_bwt(blk)
+        if q is None:
+            continue
+        seen += 1
+        L, o, per = O.orc_bwt(blk)
+        assert per == len(blk)
+        assert q[1:] == (L, o), (q[0], len(blk), blk[:12])
+        if O.has_ref():
+            assert q[1:] == O.ref_blocksort(blk), (q[0], len(blk))
+    assert seen >= 200
+    # not quasi-periodic: text, exact powers, periods above 256 or without two copies
+    assert B.qperiodic_bwt(b"abcab" * 3) is None  # exact power
+    assert B.qperiodic_bwt(bytes(range(200)) * 3 + b"\x00") is not None
+    assert B.qperiodic_bwt(bytes(range(256)) + bytes([7]) + bytes(range(256)) + bytes([7]) + b"\x00") is None
+    assert B.qperiodic_bwt(b"abcdefgh" + b"abc") is None
+
+
 def _libc():
     c = ctypes.CDLL(None)
     c.fopen.restype = ctypes.c_void_p

@@ -57,7 +57,7 @@ def gpu_bwt(blocks: bytes, offs):
 def gpu_mtf(bwt: bytes, offs):
     nb = len(offs) - 1
     total = offs[-1]
-    mtfv = (ctypes.c_uint16 * (total + nb + 16))()
+    mtfv = (ctypes.c_uint16 * (total + 8 * nb + 16))()
     moff = (ctypes.c_uint32 * (nb + 1))()
     nmtf = (ctypes.c_uint32 * nb)()
     freq = (ctypes.c_uint32 * (nb * 258))()
@@ -292,6 +292,40 @@ def test_mtf_matches_oracle(case):
         assert np.array_equal(freq[b][: nu + 2].astype(np.int64), fr[: nu + 2].astype(np.int64)), (case, b)
 
 
+def test_mtf_mixed_entropy_chunks():
+    """Chunks on both MTF paths in one block (k_mtf_run: few distinct symbols; k_mtf_row: many)
+    with zero runs crossing slice and chunk boundaries on the row path: text and random
+    segments of a few kB, random bytes repeated 1..5 times, a 70-symbol alphabet."""
+    rng = np.random.default_rng(77)
+    parts = []
+    for i in range(60):
+        k = int(rng.integers(500, 6000))
+        if i % 3 == 0:
+            parts.append(datagen.text(k, 1000 + i))
+        elif i % 3 == 1:
+            v = rng.integers(0, 256, k // 3, dtype=np.uint8)
+            parts.append(np.repeat(v, rng.integers(1, 6, v.size)).tobytes())
+        else:
+            parts.append(rng.integers(0, 70, k, dtype=np.uint8).tobytes())
+    data = b"".join(parts)
+    blocks, offs = _blocks_of(data, 1)
+    bwt = b"".join(O.orc_bwt(blocks[offs[b]:offs[b + 1]])[0] for b in range(len(offs) - 1))
+    got, freq = gpu_mtf(bwt, offs)
+    for b in range(len(offs) - 1):
+        mv, fr, nu = O.orc_mtf(bwt[offs[b]:offs[b + 1]])
+        assert np.array_equal(got[b], mv), b
+        assert np.array_equal(freq[b][: nu + 2].astype(np.int64), fr[: nu + 2].astype(np.int64)), b
+    # raw random-ish columns straight into the MTF stage (not a BWT: every chunk high-entropy)
+    raw = rng.integers(0, 256, 300_000, dtype=np.uint8)
+    raw[1000:5000] = 7  # one long zero run across slices and chunks
+    raw = raw.tobytes()
+    offs2 = [0, 100_000, 100_001, 300_000]
+    got, _ = gpu_mtf(raw, offs2)
+    for b in range(3):
+        mv, _, _ = O.orc_mtf(raw[offs2[b]:offs2[b + 1]])
+        assert np.array_equal(got[b], mv), b
+
+
 def test_mtf_long_zero_runs():
     # runs of identical BWT symbols spanning many MTF chunks (RUNA/RUNB carry across chunks)
     bwt = b"a" * 5000 + b"b" + b"a" * 3000 + b"c" * 70000 + b"ab" * 10
@@ -331,6 +365,49 @@ def test_periodic_text_blocks():
     w = datagen.text(3_001, 99)
     for data in (w * 300, b"abcabcabd" * 120_000, b"ab" * 500_000):
         assert B.buff_to_buff_compress(data, 2) == expected(data, 2)
+
+
+def _quasi_periodic_blocks(seed):
+    """Blocks w^k w' (w' a proper prefix of w): the analytic path of qsa.h, beside ordinary
+    blocks in the same batch."""
+    rng = random.Random(seed)
+    parts = [bytes([0x61] * 4 + [0xFB]) * 20_000 + b"a", bytes([0] * 4 + [0xFB]) * 7 + b"\0\0\0",
+             datagen.text(30_000, 3)]
+    for _ in range(24):
+        w = bytes(rng.randrange(rng.choice([2, 3, 4, 256])) for _ in range(rng.randint(2, 256)))
+        k = rng.randint(2, max(2, 150_000 // len(w)))
+        parts.append(w * k + w[: rng.randint(1, len(w) - 1)])
+    offs = [0]
+    for p_ in parts:
+        offs.append(offs[-1] + len(p_))
+    return b"".join(parts), offs
+
+
+def test_bwt_quasi_periodic_blocks():
+    """Quasi-periodic blocks through the stage ABI (device detection k_qperiod, host plan,
+    k_qsa) against the oracle, and the host analytic path (bzg_qperiodic_bwt) agrees."""
+    blocks, offs = _quasi_periodic_blocks(9)
+    bwt, orig = gpu_bwt(blocks, offs)
+    nq = 0
+    for b in range(len(offs) - 1):
+        blk = blocks[offs[b]:offs[b + 1]]
+        L, o, per = O.orc_bwt(blk)
+        assert bwt[offs[b]:offs[b + 1]] == L, b
+        assert orig[b] == o, b
+        q = B.qperiodic_bwt(blk)
+        if q is not None:
+            nq += 1
+            assert q[1:] == (L, o), b
+    assert nq >= 20
+
+
+@pytest.mark.parametrize("level", [1, 9])
+def test_single_byte_quasi_periodic_tail(level):
+    """Config 4 shape: a repeated byte whose last RLE1 chunk holds 1..3 bytes makes the last
+    block (c c c c 0xFB)^k c.. quasi-periodic (k_qsa); full blocks stay exactly periodic (A5)."""
+    for c, r in ((0x61, 1), (0xFB, 3), (0x00, 2)):
+        data = bytes([c]) * (255 * 9_000 + r)
+        assert B.buff_to_buff_compress(data, level) == expected(data, level), (c, r)
 
 
 def test_single_byte_aperiodic_tail():
