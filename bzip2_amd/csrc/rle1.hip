@@ -74,7 +74,7 @@ __device__ __forceinline__ RunBits run_bits(const uint8_t* __restrict__ x, uint6
 // tile's first run start on, h = the bytes before it (they continue the run that starts at the
 // carried run start), ends = that run ends at the tile's byte h - 1.  k_rle_fix adds the h
 // bytes' output once the carries are known (closed form).  tinfo = S | h << 16 | ends << 31.
-__global__ void __launch_bounds__(kT) k_rle_count(const uint8_t* __restrict__ x, uint64_t n,
+__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_rle_count(const uint8_t* __restrict__ x, uint64_t n,
                                                   uint32_t* __restrict__ tmax, uint32_t* __restrict__ tinfo) {
   __shared__ uint32_t sh[kT / 64];
   __shared__ uint32_t thr[kT];
@@ -201,7 +201,7 @@ __device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_
 }
 
 // Pass 3: write block bytes, chunk-start bitmap and chunk-start -> input position map.
-__global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint64_t n,
+__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict__ x, uint64_t n,
                                              const uint32_t* __restrict__ carry,
                                              const uint32_t* __restrict__ out_base,
                                              uint8_t* __restrict__ out, uint32_t* __restrict__ cbits,
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(kT) k_emit(const uint8_t* __restrict__ x, uint
 
 // Input offset of the chunk whose first output byte is p (p a chunk start), by re-deriving
 // the byte info of the one RLE tile that produced p.  One workgroup per queried boundary.
-__global__ void __launch_bounds__(kT) k_chunk_inpos(const uint8_t* __restrict__ x, uint64_t n,
+__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_chunk_inpos(const uint8_t* __restrict__ x, uint64_t n,
                                                     const uint32_t* __restrict__ carry,
                                                     const uint32_t* __restrict__ out_base, uint32_t ntiles,
                                                     const uint32_t* __restrict__ qpos, uint32_t nq,

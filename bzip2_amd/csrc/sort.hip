@@ -44,6 +44,12 @@ static_assert(kBig == 128 || kBig == 256, "S2 classes cover up to 128 or 256 rot
 constexpr uint32_t kDTile = BZG_DTILE;  // rotations per workgroup in an S1 pass
 constexpr uint32_t kPerT = kDTile / kT;
 constexpr uint32_t kDBig = 16;        // S1 byte passes stop at this depth (then doubling)
+// 1: tiled S1 passes keep a 4-character key cache beside the slots (sk / sk2); 0: every tiled
+// pass gathers its character from the text (L2: the tiles of an XCD walk one or two blocks)
+#ifndef BZG_S1_TCACHE
+#define BZG_S1_TCACHE 1
+#endif
+constexpr bool kTCache = BZG_S1_TCACHE != 0;
 #ifndef BZG_SG
 #define BZG_SG 2048
 #endif
@@ -244,7 +250,7 @@ __device__ __forceinline__ void s1_load(const SortBufs& B, const Grp& gr, const 
   uint32_t* srck = alt ? B.sk2 : B.sk;
   const bool ident = gr.flags & kGrpIdent;
   const uint32_t depth = grp_depth(gr);
-  const bool fresh = ident || (kCounting && grp_cache(gr) == 0);
+  const bool fresh = ident || ((kCounting || !kTCache) && grp_cache(gr) == 0);
   const uint8_t* ut = B.text + U.toff;
   // (whole-loop uniform branches keep vv / kk in registers)
   if (ident) {
@@ -266,7 +272,7 @@ __device__ __forceinline__ void s1_load(const SortBufs& B, const Grp& gr, const 
       const uint32_t q = cyc_pos(vv[i], depth, U.len);
       kk[i] = q + 4 <= U.len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(ut, U.len, q);
     }
-    if (kCounting && !ident) {
+    if (kCounting && !ident && kTCache) {
 #pragma unroll
       for (int i = 0; i < (int)kPerT; i++) {
         const uint32_t e = lo + i * kT + threadIdx.x;
@@ -281,6 +287,8 @@ __device__ __forceinline__ uint32_t s1_next_cache(const Grp& gr) {
   const uint32_t c = (gr.flags & kGrpIdent) ? 0u : grp_cache(gr);
   return c ? c - 1 : 3u;
 }
+// the same for the buckets of a tiled pass
+__device__ __forceinline__ uint32_t tiled_next_cache(const Grp& gr) { return kTCache ? s1_next_cache(gr) : 0u; }
 
 __global__ void __launch_bounds__(kT) k_s1_hist(const TileRec* __restrict__ TR, SortBufs B, uint32_t* __restrict__ hist) {
   // 4 copies of every bin in consecutive words (lane & 3 picks one): lanes of a wave that
@@ -344,7 +352,7 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
   }
   if (cl == kClsDeep) {  // rare: a bucket still larger than kBig after kDBig characters
     const uint32_t dst_alt = (gr.flags & kGrpIdent) ? 0u : ((gr.flags & kGrpAlt) ^ 1u);
-    deep[wave_append(n_deep, true)] = Grp{base, total, gr.unit, grp_flags(dst_alt, depth, s1_next_cache(gr))};
+    deep[wave_append(n_deep, true)] = Grp{base, total, gr.unit, grp_flags(dst_alt, depth, tiled_next_cache(gr))};
   }
   __syncthreads();
   if (d < (uint32_t)kNCls) ccnt[(size_t)d * nTot + g] = cc[d];
@@ -419,7 +427,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
       kk[i] = Lk[x];
       pos[i] = base[kk[i] >> 24] + x;
       dst[pos[i]] = vv[i];
-      if (single[kk[i] >> 24] & 2u) dstk[pos[i]] = kk[i] << 8;
+      if (kTCache && (single[kk[i] >> 24] & 2u)) dstk[pos[i]] = kk[i] << 8;
     }
   }
   // a bucket of one: this rotation is ordered (its primary-SA copy is made by k_s1_single,
@@ -443,7 +451,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   if (cl < (uint32_t)kNCls) {
     for (uint32_t x = 0; x < w; x++) rank += wc[x][cl];
     const uint32_t p = C.base[cl] + cscan[(size_t)cl * nTot + g] - cscan[(size_t)cl * nTot] + rank;
-    C.l[cl][p] = Grp{gbase, total, gr.unit, grp_flags(dst_alt ? kGrpAlt : 0u, depth, s1_next_cache(gr))};
+    C.l[cl][p] = Grp{gbase, total, gr.unit, grp_flags(dst_alt ? kGrpAlt : 0u, depth, tiled_next_cache(gr))};
   }
 }
 
@@ -560,7 +568,7 @@ __device__ __forceinline__ uint32_t rec_pack(uint32_t j, uint32_t start, uint32_
   return (j << 28) | (start << 14) | size;
 }
 
-__global__ void __launch_bounds__(kTS) k_s1s_pass(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+__global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
                                                  const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
                                                  SortBufs B, SortOut O, uint32_t* __restrict__ rec,
                                                  uint32_t* __restrict__ nrec, uint32_t* __restrict__ ccnt, uint32_t nTot,
@@ -1083,7 +1091,7 @@ __device__ __forceinline__ uint32_t g8_xor(uint32_t v, uint32_t hm) {
 // workgroup's range, so both outputs keep the list order) and one atomic per output per
 // workgroup: single-address device atomics cost ~10 ns each, one per wave was 5 ms per GB.
 constexpr uint32_t kSplitPer = 16;
-__global__ void __launch_bounds__(kT) k_split_pairs(const Grp* __restrict__ L, uint32_t n, Grp* __restrict__ pairs,
+__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_split_pairs(const Grp* __restrict__ L, uint32_t n, Grp* __restrict__ pairs,
                                                     Grp* __restrict__ rest, uint32_t* __restrict__ cnt) {
   __shared__ uint32_t sh[kT / 64];
   __shared__ uint32_t base[2];
@@ -1244,6 +1252,9 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
 // padded segment has fewer than 256 elements); later rounds give valid run starts < 0xff
 // there as well, and a run start 0xff would be a singleton, whose key is (position, 0).
 using BsortKey = uint64_t;
+#ifndef BZG_S2_COMPACT
+#define BZG_S2_COMPACT 0
+#endif
 constexpr BsortKey kPadKey = ~0ull;
 
 __device__ __forceinline__ BsortKey make_key1(uint32_t hi, uint32_t lo, uint32_t idx) {
@@ -1432,6 +1443,109 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
 }
 
 
+// Compacted tail of the one-group-per-wave classes: after the first bitonic round most
+// rotations are final (text: about 80%) and the tied ones form short runs.  When at most 64
+// are tied, they are packed into one lane each (LDS, in sorted order, so every run is a range
+// of lanes) and ranked inside their run on 16 characters per step, as in bsort_tail, instead
+// of re-sorting the whole segment.  Returns false (nothing done) when more than 64 are tied.
+struct S2Compact {
+  uint32_t v[64], p[64], rl[64];
+  uint4 key[64];
+  uint32_t cls[64];
+  uint8_t c[64];
+};
+template <int kPer>
+__device__ bool bsort_compact_tail(const SortBufs& B, const SortOut& O, const Grp& g, const Unit& U, uint32_t depth,
+                                   const BsortKey (&K)[kPer], const bool (&done)[kPer], const bool (&tn)[kPer],
+                                   const uint32_t (&rsn)[kPer], const uint32_t* Lv, const uint8_t* Lc,
+                                   S2Compact& C) {
+  const uint32_t lane = __lane_id();
+  bool tied[kPer];
+  uint32_t mine = 0;
+#pragma unroll
+  for (int r = 0; r < kPer; r++) {
+    tied[r] = key_valid(K[r]) && !done[r];
+    mine += tied[r] ? 1u : 0u;
+  }
+  const uint32_t incl = wave_incl_sum(mine);
+  const uint32_t nt = (uint32_t)__shfl((int)incl, 63, 64);
+  if (nt > 64) return false;
+  uint32_t ci = incl - mine;
+#pragma unroll
+  for (int r = 0; r < kPer; r++) {
+    if (!tied[r]) continue;
+    const uint32_t p = lane * kPer + r, idx = key_idx(K[r]);
+    C.v[ci] = Lv[idx];
+    C.c[ci] = Lc[idx];
+    C.p[ci] = (rsn[r] << 16) | p;
+    if (!tn[r]) C.rl[ci - (p - rsn[r])] = p - rsn[r] + 1;  // run length at the run's first lane
+    ci++;
+  }
+  wave_sync();
+  const uint8_t* t = B.text + U.toff;
+  bool live = lane < nt;
+  uint32_t v = 0, pos = 0, cls = 0xffffffffu, cst = 0, rl = 0;
+  uint8_t lastc = 0;
+  if (live) {
+    v = C.v[lane];
+    lastc = C.c[lane];
+    const uint32_t pp = C.p[lane], rs = pp >> 16;
+    cst = lane - ((pp & 0xffffu) - rs);
+    rl = C.rl[cst];
+    pos = rs;
+    cls = cst;
+  }
+  for (;;) {
+    if (__ballot(live) == 0) break;
+    const bool deep = depth >= B.dwave;
+    uint32_t k[4] = {0u, 0u, 0u, 0u};
+    if (live && !deep) text_key16(t, U.len, cyc_pos(v, depth, U.len), k);
+    C.key[lane] = make_uint4(k[0], k[1], k[2], k[3]);
+    C.cls[lane] = live ? cls : 0xffffffffu;
+    wave_sync();
+    if (deep) {  // still tied after B.dwave characters: leave to the doubling fallback
+      uint32_t rank = 0, cnt = 0;
+      if (live)
+        for (uint32_t q = cst; q < cst + rl; q++)
+          if (C.cls[q] == cls) {
+            cnt++;
+            rank += q < lane;
+          }
+      if (live) B.sa[g.start + pos + rank] = v;
+      const uint32_t ds = wave_append(O.n_deep, live && rank == 0);
+      if (live && rank == 0) O.deep[ds] = Grp{g.start + pos, cnt, g.unit, grp_flags(0u, depth, 2u)};
+      break;
+    }
+    if (live) {
+      const uint64_t mh = ((uint64_t)k[0] << 32) | k[1], ml = ((uint64_t)k[2] << 32) | k[3];
+      uint32_t lt = 0, eq = 0, rep = 0xffffffffu;
+      for (uint32_t q = cst; q < cst + rl; q++) {
+        if (C.cls[q] != cls) continue;
+        const uint4 o = C.key[q];
+        const uint64_t oh = ((uint64_t)o.x << 32) | o.y, ol = ((uint64_t)o.z << 32) | o.w;
+        lt += (oh < mh) || (oh == mh && ol < ml);
+        if (oh == mh && ol == ml) {
+          if (rep == 0xffffffffu) rep = q;
+          eq++;
+        }
+      }
+      pos += lt;
+      cls = rep;
+      if (eq == 1) {
+        live = false;
+        const uint32_t slot = g.start + pos;
+        B.sa[slot] = v;
+        const uint32_t rr = slot - U.sbase;
+        if (U.k == 1) O.bwt[U.toff + rr] = lastc;
+        if (v == 0) O.rank0[g.unit] = rr;
+      }
+    }
+    wave_sync();
+    depth += 16;
+  }
+  return true;
+}
+
 // S2 run emission (classes with one group per wave): after kRounds rounds the runs still tied
 // are left as new groups.  Their rotations are stored at their slots (primary SA) and each run
 // becomes a record (depth:15 | run start:8 | size:9) in the group's own part of `rec` (from
@@ -1444,7 +1558,7 @@ struct S2Emit {
 };
 
 template <int kSeg, int kPer, int kRounds, bool kBatch, bool kEmit = false>
-__global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_t nL, SortBufs B, SortOut O,
+__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restrict__ L, uint32_t nL, SortBufs B, SortOut O,
                                               S2Emit E = S2Emit{}) {
   constexpr int kBPW = 64 / kSeg;
   constexpr int kE = 64 * kPer;  // elements per wave
@@ -1457,6 +1571,7 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
   __shared__ uint32_t Lk[kT / 64][kEmit ? 8 : kE];
   __shared__ uint4 TK[kT / 64][kTE];
   __shared__ uint32_t TC[kT / 64][kTE];
+  __shared__ S2Compact SC[kEmit && BZG_S2_COMPACT ? kT / 64 : 1];
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   const uint32_t sl = lane % kSeg;
   const uint32_t bi = (s2_wg() * (kT / 64) + w) * kBPW + lane / kSeg;
@@ -1588,6 +1703,9 @@ __global__ void __launch_bounds__(kT) k_bsort(const Grp* __restrict__ L, uint32_
     }
     if (__ballot(any_tied) == 0) break;
     depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
+    if constexpr (kEmit && BZG_S2_COMPACT) {
+      if (depth < B.dwave && bsort_compact_tail<kPer>(B, O, g, U, depth, K, done, tn, rsn, Lv[w], Lc[w], SC[w])) break;
+    }
     if (++round >= kRounds || depth >= B.dwave) {
       if constexpr (kEmit) {
         static_assert(kSeg == 64, "one group per wave");

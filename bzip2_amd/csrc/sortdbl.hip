@@ -283,7 +283,7 @@ __device__ void lds_radix_sort(TileLds& S, uint32_t n, uint32_t nbits, uint32_t*
   }
 
 template <bool kStamp>
-__global__ void __launch_bounds__(kT) k_tile_sort(const Grp* __restrict__ small, uint32_t n_small,
+__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_tile_sort(const Grp* __restrict__ small, uint32_t n_small,
                                                   const uint32_t* __restrict__ first, const uint32_t* __restrict__ last,
                                                   uint32_t key_bits, SortBufs B, Grp* __restrict__ next,
                                                   uint32_t* __restrict__ n_next, bool isa_valid,
