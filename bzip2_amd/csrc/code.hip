@@ -22,65 +22,96 @@ constexpr int kT = 256;
 // max(freq,1) << 8 | 0, merge = sum of weights | (1 + max depth); heap moves use strict '<' on
 // weights only; rescale with w = 1 + w/2 while any length exceeds max_len.
 // The heap itself is sequential and runs on lane 0.  Heap entries carry their weight
-// (weight << 32 | node), so a sift step is one LDS round trip; both children are loaded
-// together.  Lengths (parent-chain walks) and the rescale run on all lanes.
+// (weight << 32 | node).  The chain of dependent LDS round trips is the cost, so a sift-down
+// loads the three levels below its node at once (2 + 4 + 8 entries, 16-byte reads) and walks
+// them in registers, and a sift-up loads three ancestors at once.  Lengths (parent-chain
+// walks) and the rescale run on all lanes.
+constexpr int kHeapCap = kMaxAlpha + 14;  // 272: the lookahead reads below a live node stay inside
+__device__ __forceinline__ int32_t hb_wt(uint64_t e) { return (int32_t)(e >> 32); }
+
+__device__ __forceinline__ void hb_sift_up(uint64_t* heap, int z, uint64_t item) {
+  while (z > 1) {  // heap[0] is the weight-0 sentinel above the root
+    const uint64_t p1 = heap[z >> 1], p2 = heap[z >> 2], p3 = heap[z >> 3];
+    if (!(hb_wt(item) < hb_wt(p1))) break;
+    heap[z] = p1;
+    z >>= 1;
+    if (!(hb_wt(item) < hb_wt(p2))) break;
+    heap[z] = p2;
+    z >>= 1;
+    if (!(hb_wt(item) < hb_wt(p3))) break;
+    heap[z] = p3;
+    z >>= 1;
+  }
+  heap[z] = item;
+}
+
+// One level of the reference's DOWNHEAP (huffman.c:46-59) with the node's two children in
+// registers: returns false (stop) when item stays at z; otherwise moves the smaller child up
+// (the right one only when strictly smaller) and returns its side in k.
+__device__ __forceinline__ bool hb_down_step(uint64_t* heap, int& z, int nheap, uint64_t item, uint64_t l, uint64_t r,
+                                             int& k) {
+  const int y = 2 * z;
+  if (y > nheap) return false;
+  uint64_t c = l;
+  k = 0;
+  if (y < nheap && hb_wt(r) < hb_wt(l)) {
+    c = r;
+    k = 1;
+  }
+  if (hb_wt(item) < hb_wt(c)) return false;
+  heap[z] = c;
+  z = y + k;
+  return true;
+}
+
+__device__ __forceinline__ void hb_sift_down(uint64_t* heap, int nheap, uint64_t item) {
+  const uint4* h4 = reinterpret_cast<const uint4*>(heap);
+  constexpr int kQ = kHeapCap / 2;  // 16-byte words in the heap
+  auto lo = [](uint4 q) { return ((uint64_t)q.y << 32) | q.x; };
+  auto hi = [](uint4 q) { return ((uint64_t)q.w << 32) | q.z; };
+  int z = 1;
+  for (;;) {
+    if (2 * z > nheap) break;
+    // heap[2z..2z+1], heap[4z..4z+3], heap[8z..8z+7]; past the live heap the words are clamped
+    // inside the array and never used
+    const uint4 a = h4[z];
+    const uint4 b0 = h4[min(2 * z, kQ - 2)], b1 = h4[min(2 * z, kQ - 2) + 1];
+    const int ci = min(4 * z, kQ - 4);
+    const uint4 c0 = h4[ci], c1 = h4[ci + 1], c2 = h4[ci + 2], c3 = h4[ci + 3];
+    int k1, k2, k3;
+    if (!hb_down_step(heap, z, nheap, item, lo(a), hi(a), k1)) break;
+    const uint4 b = k1 ? b1 : b0;
+    if (!hb_down_step(heap, z, nheap, item, lo(b), hi(b), k2)) break;
+    const uint4 c = k1 ? (k2 ? c3 : c2) : (k2 ? c1 : c0);
+    if (!hb_down_step(heap, z, nheap, item, lo(c), hi(c), k3)) break;
+  }
+  heap[z] = item;
+}
+
 __device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, int max_len, uint64_t* heap,
                                 int32_t* weight, int32_t* parent) {
   const int lane = (int)__lane_id();
   for (int i = lane; i < alpha; i += 64) weight[i + 1] = (int32_t)((freq[i] == 0 ? 1u : freq[i]) << 8);
-  auto wt = [](uint64_t e) { return (int32_t)(e >> 32); };
   for (int round = 0; round < 64; round++) {  // converges in a few rounds for valid tables
     for (int i = lane; i < 2 * alpha; i += 64) parent[i] = -1;
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
       int nodes = alpha, nheap = 0;
       heap[0] = 0;  // weight 0 sentinel above the root
-      for (int i = 1; i <= alpha; i++) {
-        const uint64_t item = ((uint64_t)(uint32_t)weight[i] << 32) | (uint32_t)i;
-        int z = ++nheap;
-        for (;;) {
-          const uint64_t up = heap[z >> 1];
-          if (!(wt(item) < wt(up))) break;
-          heap[z] = up;
-          z >>= 1;
-        }
-        heap[z] = item;
-      }
+      for (int i = 1; i <= alpha; i++) hb_sift_up(heap, ++nheap, ((uint64_t)(uint32_t)weight[i] << 32) | (uint32_t)i);
       while (nheap > 1) {
         uint64_t pick[2];
         for (int k = 0; k < 2; k++) {
           pick[k] = heap[1];
           const uint64_t item = heap[nheap--];
-          int z = 1;
-          for (;;) {
-            int y = z << 1;
-            if (y > nheap) break;
-            uint64_t c = heap[y];
-            const uint64_t c2 = heap[y + 1];  // in bounds: the array has kMaxAlpha + 4 entries
-            if (y < nheap && wt(c2) < wt(c)) {
-              c = c2;
-              y++;
-            }
-            if (wt(item) < wt(c)) break;
-            heap[z] = c;
-            z = y;
-          }
-          heap[z] = item;
+          hb_sift_down(heap, nheap, item);
         }
         nodes++;
         parent[(uint32_t)pick[0]] = parent[(uint32_t)pick[1]] = nodes;
-        const int32_t w0 = wt(pick[0]), w1 = wt(pick[1]);
+        const int32_t w0 = hb_wt(pick[0]), w1 = hb_wt(pick[1]);
         const int32_t d0 = w0 & 0xff, d1 = w1 & 0xff;
         const int32_t wn = (int32_t)(((uint32_t)w0 & 0xffffff00u) + ((uint32_t)w1 & 0xffffff00u)) | (1 + (d0 > d1 ? d0 : d1));
-        const uint64_t item = ((uint64_t)(uint32_t)wn << 32) | (uint32_t)nodes;
-        int z = ++nheap;
-        for (;;) {
-          const uint64_t up = heap[z >> 1];
-          if (!(wt(item) < wt(up))) break;
-          heap[z] = up;
-          z >>= 1;
-        }
-        heap[z] = item;
+        hb_sift_up(heap, ++nheap, ((uint64_t)(uint32_t)wn << 32) | (uint32_t)nodes);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -265,7 +296,7 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
 // BZ2_hbMakeCodeLengths for table t of block b (one wave; the heap work is sequential).
 __global__ void __launch_bounds__(64) k_huff(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
                                              uint32_t* __restrict__ rf_g, uint8_t* __restrict__ lens_g) {
-  __shared__ uint64_t heap[kMaxAlpha + 4];
+  __shared__ alignas(16) uint64_t heap[kHeapCap];
   __shared__ int32_t weight[kMaxAlpha + 2];
   __shared__ int32_t parent[kMaxAlpha * 2];
   __shared__ uint32_t fq[kMaxAlpha];
@@ -291,7 +322,7 @@ __global__ void __launch_bounds__(64) k_huff(const uint32_t* __restrict__ nmtf_g
 __global__ void __launch_bounds__(64) k_code_lengths_test(const uint32_t* __restrict__ freq_g,
                                                           const int32_t* __restrict__ alpha_g, int max_len,
                                                           uint8_t* __restrict__ lens_g) {
-  __shared__ uint64_t heap[kMaxAlpha + 4];
+  __shared__ alignas(16) uint64_t heap[kHeapCap];
   __shared__ int32_t weight[kMaxAlpha + 2];
   __shared__ int32_t parent[kMaxAlpha * 2];
   __shared__ uint32_t fq[kMaxAlpha];

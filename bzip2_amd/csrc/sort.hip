@@ -365,13 +365,16 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
                                                    SortBufs B, SortOut O, const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ tot, const uint32_t* __restrict__ cscan,
                                                    uint32_t nTot, ClsLists C) {
-  __shared__ uint32_t cnt[256 * 4];  // 4 bank-spread copies per bucket (see k_s1_hist)
-  __shared__ uint32_t base[256];   // global slot of the bucket's first element - its LDS start
-  __shared__ uint32_t single[256];
-  __shared__ uint32_t wc[kT / 64][kNCls + 1];
-  __shared__ uint32_t sh[kT / 64];
+  // 20 KB of LDS, so that 8 workgroups fit a CU: the bucket counters (4 bank-spread copies per
+  // bucket, see k_s1_hist) and the reordered tile.  Once the tile is reordered the counter
+  // space holds each bucket's store base and flags (and the emission's wave counts); the scan
+  // scratch lives in the tile space before the tile is.
+  __shared__ uint32_t cnt[256 * 4];
   __shared__ uint32_t Lv[kDTile], Lk[kDTile];
   static_assert(kDTile == kPerT * kT, "one element per thread and round");
+  uint32_t* const base = cnt;          // after the reorder: global slot of the bucket's first element - its LDS start
+  uint32_t* const flag = cnt + 256;    // bit 0: a bucket of one; bit 1: the bucket stays in S1 (needs its key caches)
+  uint32_t* const wcnt = cnt + 512;    // [wave][class] counts of the bucket emission
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const TileRec tr = TR[t];
   const uint32_t g = tr.gi;
@@ -386,10 +389,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   const uint32_t gbase = off[(size_t)t * 256 + d];
 #pragma unroll
   for (int q = 0; q < 4; q++) cnt[q * kT + d] = 0;
-  {  // bit 0: a bucket of one; bit 1: the bucket stays in S1 (needs its key caches)
-    const uint32_t cl = bucket_cls(total, grp_depth(gr) + 1);
-    single[d] = (total == 1 ? 1u : 0u) | (cl == 6 || cl == 7 ? 2u : 0u);
-  }
+  const uint32_t myflag = (total == 1 ? 1u : 0u) | ((bucket_cls(total, grp_depth(gr) + 1) & ~1u) == 6u ? 2u : 0u);
   uint32_t vv[kPerT], kk[kPerT];
   s1_load<false>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
@@ -399,13 +399,14 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   for (int i = 0; i < (int)kPerT; i++)
     if (lo + i * kT + threadIdx.x < hi) rk[i] = atomicAdd(&cnt[(kk[i] >> 24) * 4 + cp], 1u);
   __syncthreads();
+  uint32_t mybase;
   {  // bucket d's LDS start, and the start of each of its copies (any order within a bucket)
     const uint4 c4 = reinterpret_cast<const uint4*>(cnt)[d];
     const uint32_t c = c4.x + c4.y + c4.z + c4.w;
-    const uint32_t lstart = block_incl_sum(c, sh, (uint32_t*)nullptr) - c;
+    const uint32_t lstart = block_incl_sum(c, Lv, (uint32_t*)nullptr) - c;
     reinterpret_cast<uint4*>(cnt)[d] =
         make_uint4(lstart, lstart + c4.x, lstart + c4.x + c4.y, lstart + c4.x + c4.y + c4.z);
-    base[d] = gbase - lstart;
+    mybase = gbase - lstart;
   }
   __syncthreads();
 #pragma unroll
@@ -417,6 +418,9 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
     }
   }
   __syncthreads();
+  base[d] = mybase;
+  flag[d] = myflag;
+  __syncthreads();
   const uint32_t m = hi - lo;
   uint32_t pos[kPerT];
 #pragma unroll
@@ -427,14 +431,14 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
       kk[i] = Lk[x];
       pos[i] = base[kk[i] >> 24] + x;
       dst[pos[i]] = vv[i];
-      if (kTCache && (single[kk[i] >> 24] & 2u)) dstk[pos[i]] = kk[i] << 8;
+      if (kTCache && (flag[kk[i] >> 24] & 2u)) dstk[pos[i]] = kk[i] << 8;
     }
   }
   // a bucket of one: this rotation is ordered (its primary-SA copy is made by k_s1_single,
   // since other workgroups may still read the primary SA in this pass)
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    if (i * kT + threadIdx.x < m && (single[kk[i] >> 24] & 1u)) emit_final(B, O, U, gr.unit, pos[i], vv[i], !dst_alt);
+    if (i * kT + threadIdx.x < m && (flag[kk[i] >> 24] & 1u)) emit_final(B, O, U, gr.unit, pos[i], vv[i], !dst_alt);
   if (tr.k != 0) return;
   // ---- bucket emission (digit order within the group)
   const uint32_t depth = grp_depth(gr) + 1;
@@ -443,13 +447,13 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   uint32_t rank = 0;
 #pragma unroll
   for (int k = 0; k < kNCls; k++) {
-    const uint64_t m = __ballot(cl == (uint32_t)k);
-    if (cl == (uint32_t)k) rank = (uint32_t)__popcll(m & lanemask_lt());
-    if (__lane_id() == 0) wc[w][k] = (uint32_t)__popcll(m);
+    const uint64_t mk = __ballot(cl == (uint32_t)k);
+    if (cl == (uint32_t)k) rank = (uint32_t)__popcll(mk & lanemask_lt());
+    if (__lane_id() == 0) wcnt[w * kNCls + k] = (uint32_t)__popcll(mk);
   }
   __syncthreads();
   if (cl < (uint32_t)kNCls) {
-    for (uint32_t x = 0; x < w; x++) rank += wc[x][cl];
+    for (uint32_t x = 0; x < w; x++) rank += wcnt[x * kNCls + cl];
     const uint32_t p = C.base[cl] + cscan[(size_t)cl * nTot + g] - cscan[(size_t)cl * nTot] + rank;
     C.l[cl][p] = Grp{gbase, total, gr.unit, grp_flags(dst_alt ? kGrpAlt : 0u, depth, tiled_next_cache(gr))};
   }
@@ -1252,6 +1256,7 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
 // padded segment has fewer than 256 elements); later rounds give valid run starts < 0xff
 // there as well, and a run start 0xff would be a singleton, whose key is (position, 0).
 using BsortKey = uint64_t;
+// bit c (3..5): class c uses the compacted tail after its first round
 #ifndef BZG_S2_COMPACT
 #define BZG_S2_COMPACT 0
 #endif
@@ -1571,7 +1576,8 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   __shared__ uint32_t Lk[kT / 64][kEmit ? 8 : kE];
   __shared__ uint4 TK[kT / 64][kTE];
   __shared__ uint32_t TC[kT / 64][kTE];
-  __shared__ S2Compact SC[kEmit && BZG_S2_COMPACT ? kT / 64 : 1];
+  constexpr bool kCompact = kEmit && ((BZG_S2_COMPACT >> (kPer == 1 ? 3 : kPer == 2 ? 4 : 5)) & 1);
+  __shared__ S2Compact SC[kCompact ? kT / 64 : 1];
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   const uint32_t sl = lane % kSeg;
   const uint32_t bi = (s2_wg() * (kT / 64) + w) * kBPW + lane / kSeg;
@@ -1703,7 +1709,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
     }
     if (__ballot(any_tied) == 0) break;
     depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
-    if constexpr (kEmit && BZG_S2_COMPACT) {
+    if constexpr (kCompact) {
       if (depth < B.dwave && bsort_compact_tail<kPer>(B, O, g, U, depth, K, done, tn, rsn, Lv[w], Lc[w], SC[w])) break;
     }
     if (++round >= kRounds || depth >= B.dwave) {
