@@ -1335,6 +1335,53 @@ __device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
 }
 
 
+// Later rounds of the one-group-per-wave classes only reorder inside the tied runs (keys
+// of different runs already differ in their run-start byte), and those runs are short: an
+// odd-even transposition sort over the whole segment needs as many steps as the longest run,
+// a handful of compare-exchanges with the neighbouring position each, against a full bitonic
+// network (21..36 stages).  Positions p = lane * kPer + r; kSeg = 64 (no segment edges).
+#ifndef BZG_OETS_MAX
+#define BZG_OETS_MAX 16
+#endif
+__device__ __forceinline__ void key_ce(BsortKey& a, BsortKey& b) {
+  const bool sw = key_less(b, a);
+  const BsortKey x = a, y = b;
+  a = sw ? y : x;
+  b = sw ? x : y;
+}
+__device__ __forceinline__ BsortKey key_shfl_down1(BsortKey k) {
+  return ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(k >> 32), 1, 64) << 32) | (uint32_t)__shfl_down((int)(uint32_t)k, 1, 64);
+}
+__device__ __forceinline__ BsortKey key_shfl_up1(BsortKey k) {
+  return ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(k >> 32), 1, 64) << 32) | (uint32_t)__shfl_up((int)(uint32_t)k, 1, 64);
+}
+template <int kPer>
+__device__ __forceinline__ void oets(BsortKey (&K)[kPer], uint32_t steps) {
+  const uint32_t lane = __lane_id();
+  for (uint32_t s = 0; s < steps; s++) {
+    const uint32_t par = s & 1u;
+    if constexpr (kPer == 1) {
+      // pairs (lane, lane + 1) with lane % 2 == par
+      const BsortKey nx = key_shfl_down1(K[0]), pv = key_shfl_up1(K[0]);
+      const bool left = (lane & 1u) == par;
+      if (left && lane < 63) K[0] = key_less(nx, K[0]) ? nx : K[0];
+      if (!left && lane > 0) K[0] = key_less(K[0], pv) ? pv : K[0];
+    } else {
+      static_assert((kPer & 1) == 0, "even registers per lane");
+      if (par == 0) {
+#pragma unroll
+        for (int r = 0; r + 1 < kPer; r += 2) key_ce(K[r], K[r + 1]);
+      } else {
+#pragma unroll
+        for (int r = 1; r + 1 < kPer; r += 2) key_ce(K[r], K[r + 1]);
+        const BsortKey nx = key_shfl_down1(K[0]), pv = key_shfl_up1(K[kPer - 1]);
+        if (lane < 63 && key_less(nx, K[kPer - 1])) K[kPer - 1] = nx;
+        if (lane > 0 && key_less(K[0], pv)) K[0] = pv;
+      }
+    }
+  }
+}
+
 // Runs still tied after kRounds bitonic rounds (few rotations, often long repeats) are
 // finished in place: every tied rotation ranks itself among the members of its run that are
 // still tied with it (same class, named by the lowest position of the class) on the next 16
@@ -1640,12 +1687,16 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
 #pragma unroll
   for (int r = 0; r < kPer; r++) done[r] = false;
   int round = 0;
+  uint32_t maxrun = 0;  // longest tied run of the previous round (kSeg = 64)
   // BZG_DEBUG: waves entering each round, per class (dbg[8 + 8 * class + round]; round 7:
   // the rank-counting tail)
   constexpr int kDbgCls = kSeg * kPer == 16 ? 1 : kSeg * kPer == 32 ? 2 : kSeg * kPer == 64 ? 3 : kSeg * kPer == 128 ? 4 : 5;
   for (;;) {
     if (O.dbg && lane == 0) atomicAdd(&O.dbg[8 + 8 * kDbgCls + min(round, 6)], 1ull);
-    bitonic<kSeg, kPer>(K);
+    if (kSeg == 64 && BZG_OETS_MAX > 0 && round > 0 && maxrun <= BZG_OETS_MAX)
+      oets<kPer>(K, maxrun);
+    else
+      bitonic<kSeg, kPer>(K);
     // ties with the previous / next position of the segment (same run start and key)
     bool tp[kPer], tn[kPer];
 #pragma unroll
@@ -1743,6 +1794,13 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         bsort_tail<kSeg, kPer, kBatch>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       }
       break;
+    }
+    if constexpr (kSeg == 64) {
+      uint32_t ml = 0;
+#pragma unroll
+      for (int r = 0; r < kPer; r++)
+        if (key_valid(K[r]) && !done[r] && !tn[r]) ml = max(ml, sl * kPer + r - rsn[r] + 1);
+      maxrun = (uint32_t)__shfl((int)wave_incl_max(ml), 63, 64);
     }
     // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
 #pragma unroll
