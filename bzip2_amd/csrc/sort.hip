@@ -1340,6 +1340,11 @@ __device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
 // odd-even transposition sort over the whole segment needs as many steps as the longest run,
 // a handful of compare-exchanges with the neighbouring position each, against a full bitonic
 // network (21..36 stages).  Positions p = lane * kPer + r; kSeg = 64 (no segment edges).
+// 1: the one-group-per-wave classes gather 16 characters in their first round (the second
+// round's keys come from LDS instead of a second dependent gather)
+#ifndef BZG_S2_PRE
+#define BZG_S2_PRE 1
+#endif
 #ifndef BZG_OETS_MAX
 #define BZG_OETS_MAX 16
 #endif
@@ -1625,6 +1630,8 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   __shared__ uint32_t TC[kT / 64][kTE];
   constexpr bool kCompact = kEmit && ((BZG_S2_COMPACT >> (kPer == 1 ? 3 : kPer == 2 ? 4 : 5)) & 1);
   __shared__ S2Compact SC[kCompact ? kT / 64 : 1];
+  constexpr bool kPre = kEmit && BZG_S2_PRE;
+  __shared__ uint64_t Lx[kT / 64][kPre ? kE : 1];  // characters depth + 7 .. + 14 (second-round keys)
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   const uint32_t sl = lane % kSeg;
   const uint32_t bi = (s2_wg() * (kT / 64) + w) * kBPW + lane / kSeg;
@@ -1645,7 +1652,30 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
     const uint32_t p = sl * kPer + r;
     vq[r] = p < m ? ((g.flags & kGrpIdent) ? p : src[g.start + p]) : 0u;
   }
-  if constexpr (kBatch) {
+  if constexpr (kPre) {
+    // one round trip for two rounds: 16 characters per rotation, the 8 after the first 7
+    // kept in LDS for the second round's keys (almost every wave of these classes has one)
+    uint32_t raw[kPer][5], cq[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      cq[r] = cyc_pos(vq[r], depth, U.len);
+      text_raw<4>(t + cq[r], raw[r]);
+      cq[r] |= (uint32_t)t[vq[r] == 0 ? U.len - 1 : vq[r] - 1] << 24;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const uint32_t p = sl * kPer + r, idx = lane * kPer + r;
+      const bool valid = p < m;
+      const uint32_t q = cq[r] & 0xffffffu;
+      uint32_t k4[4];
+      text_words_of<4>(t + q, raw[r], k4);
+      if (valid && q + 16 > U.len) text_words_wrap<4>(t, U.len, q, k4);
+      Lv[w][idx] = vq[r];
+      Lc[w][idx] = (uint8_t)(cq[r] >> 24);
+      Lx[w][idx] = ((uint64_t)((k4[1] << 24) | (k4[2] >> 8)) << 32) | ((k4[2] << 24) | (k4[3] >> 8));
+      K[r] = valid ? make_key1(k4[0], k4[1], idx) : kPadKey;
+    }
+  } else if constexpr (kBatch) {
     // all loads issued before any is used (3 aligned words and the BWT byte per rotation);
     // keys that wrap past the unit end are rebuilt afterwards
     uint32_t raw[kPer][3], cq[kPer];
@@ -1812,7 +1842,13 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         K[r] = make_key2(p, 0, 0, idx);
       } else {
         uint32_t hi, lo;
-        text_key8(t, U.len, cyc_pos(Lv[w][idx], depth, U.len), hi, lo);
+        if (kPre && round == 1) {
+          const uint64_t x = Lx[w][kPre ? idx : 0];
+          hi = (uint32_t)(x >> 32);
+          lo = (uint32_t)x;
+        } else {
+          text_key8(t, U.len, cyc_pos(Lv[w][idx], depth, U.len), hi, lo);
+        }
         K[r] = make_key2(rsn[r], hi, lo, idx);
       }
     }
