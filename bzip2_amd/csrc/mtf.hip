@@ -246,12 +246,93 @@ constexpr int kRegW = BZG_MTF_REGW;  // list words (4 positions each) held in re
 #define BZG_MTF_ROWMIN 64
 #endif
 constexpr uint32_t kRowMin = BZG_MTF_ROWMIN;  // chunks with more distinct symbols go to k_mtf_row
-__global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
+// BZG_MTF_FIRST (default): a chunk handled here has at most kRowMin (64) distinct symbols, and
+// the symbols it has moved always precede the ones it has not touched, which keep the order of
+// the chunk's initial list.  So the lane keeps only the recency list of the moved symbols (64
+// positions: 8 register words and 8 LDS words instead of 56), and the rank of a symbol's first
+// occurrence, which depends on the initial list only, comes precomputed from k_mtf_first.
+// The LDS footprint drops from 74 KB to 25 KB per workgroup (2 -> 6 waves per SIMD).
+#ifndef BZG_MTF_FIRST
+#define BZG_MTF_FIRST 0
+#endif
+constexpr bool kFirst = BZG_MTF_FIRST != 0;
+constexpr int kListW = kFirst ? 16 : 64;  // list words a lane holds (registers + LDS)
+
+// k-th distinct symbol of the chunk by first occurrence, s_k: its rank there is
+// k + pos0(s_k) - #{i < k : pos0(s_i) < pos0(s_k)} (pos0: position in the chunk's initial
+// list; the k moved symbols precede the untouched rest).  One wave per chunk; frank[g * 64 + k].
+__global__ void __launch_bounds__(kT) k_mtf_first(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
+                                                  const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ siglen,
+                                                  const uint32_t* __restrict__ init, uint8_t* __restrict__ frank) {
+  __shared__ uint32_t fp[kT / 64][256];  // first offset of each symbol in the chunk
+  __shared__ uint32_t p0[kT / 64][256];  // its position in the chunk's initial list
+  __shared__ uint32_t cs[kT / 64][64];   // distinct symbols: first offset << 8 | symbol
+  __shared__ uint32_t ord[kT / 64][64];  // distinct symbols by first occurrence
+  const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
+  const uint32_t b = blockIdx.y, c = blockIdx.x * (kT / 64) + w;
+  const uint32_t n = boff[b + 1] - boff[b];
+  if (c * kChunk >= n) return;  // (uniform in the wave)
+  const uint32_t g = cbase[b] + c;
+  const uint32_t sl = siglen[g];
+  if (sl > kRowMin) return;
+  const uint32_t lo = boff[b] + c * kChunk, len = min(n - c * kChunk, kChunk);
+  for (uint32_t k = lane; k < 256; k += 64) {
+    fp[w][k] = 0xffffffffu;
+    p0[w][k] = 0xffffffffu;
+  }
+  wave_sync();
+  // (the list past nInUse is unspecified: the smallest position of a byte is its own)
+  const uint32_t iw = init[(size_t)g * 64 + lane];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) atomicMin(&p0[w][(iw >> (8 * k)) & 0xffu], lane * 4 + k);
+  uint4 q;
+  __builtin_memcpy(&q, L + lo + 16 * lane, 16);  // unaligned; the column is padded
+  const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++)
+    if (16 * lane + k < len) atomicMin(&fp[w][(wd[k >> 2] >> (8 * (k & 3))) & 0xffu], 16 * lane + k);
+  wave_sync();
+  uint32_t have = 0, e[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    e[k] = fp[w][lane * 4 + k];
+    have += e[k] != 0xffffffffu ? 1u : 0u;
+  }
+  uint32_t p = wave_incl_sum(have) - have;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++)
+    if (e[k] != 0xffffffffu) cs[w][p++] = (e[k] << 8) | (lane * 4 + k);
+  wave_sync();
+  if (lane < sl) {
+    const uint32_t me = cs[w][lane];
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < sl; i++) k += cs[w][i] < me ? 1u : 0u;
+    ord[w][k] = me & 0xffu;
+  }
+  wave_sync();
+  if (lane < sl) {
+    const uint32_t ps = p0[w][ord[w][lane]];
+    uint32_t before = 0;
+    for (uint32_t i = 0; i < lane; i++) before += p0[w][ord[w][i]] < ps ? 1u : 0u;
+    frank[(size_t)g * 64 + lane] = (uint8_t)(lane + ps - before);
+  }
+}
+
+#ifndef BZG_MTF_LB
+#define BZG_MTF_LB 0
+#endif
+#if BZG_MTF_LB > 0
+#define BZG_MTF_BOUNDS __launch_bounds__(kT, BZG_MTF_LB)
+#else
+#define BZG_MTF_BOUNDS __launch_bounds__(kT)
+#endif
+__global__ void BZG_MTF_BOUNDS k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                                 const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ siglen,
-                                                const uint32_t* __restrict__ init,
+                                                const uint32_t* __restrict__ init, const uint8_t* __restrict__ frank,
                                                 uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
                                                 uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
-  __shared__ uint32_t lst[64 - kRegW][kT];
+  __shared__ uint32_t lst[kListW - kRegW][kT];
+  __shared__ uint32_t frl[kFirst ? 16 : 1][kT];  // kFirst: the chunk's first-occurrence ranks, 4 per word
   // rank words of the wave's 64 chunks for one 64-symbol window, [chunk][word] (17: no bank
   // conflicts on the per-lane writes); flushed as 16-byte stores, 4 lanes per chunk
   __shared__ uint32_t stg[kT / 64][64 * 17];
@@ -264,9 +345,26 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
   const uint32_t len = mine ? r.hi - r.lo : 0u;
   const uint32_t* src = init + (size_t)(r.valid ? r.gidx : 0u) * 64;
   uint32_t W[kRegW];
+  uint32_t m = 0;  // kFirst: symbols moved so far (list positions in use)
+  const uint32_t* fr = reinterpret_cast<const uint32_t*>(frank + (size_t)(r.valid ? r.gidx : 0u) * 64);
+  uint32_t fcur = 0, fi = 0;  // kFirst: first-occurrence ranks (current word of frl)
+  if constexpr (kFirst) {
 #pragma unroll
-  for (int w = 0; w < kRegW; w++) W[w] = src[w];
-  for (int w = kRegW; w < 64; w++) lst[w - kRegW][t] = src[w];
+    for (int w = 0; w < kRegW; w++) W[w] = 0;
+    for (int w = kRegW; w < kListW; w++) lst[w - kRegW][t] = 0;
+    if (mine) {
+      uint32_t x[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) x[k] = fr[k];
+#pragma unroll
+      for (int k = 0; k < 16; k++) frl[k][t] = x[k];
+    }
+    fcur = frl[0][t];
+  } else {
+#pragma unroll
+    for (int w = 0; w < kRegW; w++) W[w] = src[w];
+    for (int w = kRegW; w < kListW; w++) lst[w - kRegW][t] = src[w];
+  }
   uint32_t racc = 0;  // 4 ranks packed
   uint32_t ld = 0, z = 0, cnt = 0;
   bool seen = false;
@@ -287,8 +385,9 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
       pos = fw * 4 + ((uint32_t)__builtin_ctz(fz) >> 3);
     } else {  // beyond the register words: LDS words, 4 loads in flight per step (every
               // block byte is in the list)
+      const uint32_t wlim = kFirst ? min((uint32_t)kListW, (m + 3) >> 2) : (uint32_t)kListW;
       uint32_t w = kRegW, x = 0;
-      for (; w < 64; w += 4) {
+      for (; w < wlim; w += 4) {
         uint32_t y[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) y[k] = lst[w + k - kRegW][t] ^ pat;
@@ -306,30 +405,43 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
           break;
         }
       }
-      if (w >= 64) {  // only a corrupt input; keeps the loop finite
-        w = 63;
-        x = 0x80000000u;
+      if (kFirst) {
+        pos = w < wlim ? w * 4 + ((uint32_t)__builtin_ctz(x) >> 3) : 0xffu;
+      } else {
+        if (w >= 64) {  // only a corrupt input; keeps the loop finite
+          w = 63;
+          x = 0x80000000u;
+        }
+        pos = w * 4 + ((uint32_t)__builtin_ctz(x) >> 3);
       }
-      pos = w * 4 + ((uint32_t)__builtin_ctz(x) >> 3);
     }
-    racc |= pos << (8 * (j & 3));
+    uint32_t rank = pos;
+    bool fresh = false;
+    if (kFirst && pos >= m) {  // first occurrence in the chunk: enters at the front
+      fresh = true;
+      pos = m++;
+      rank = (fcur >> (8 * (fi & 3))) & 0xffu;
+      if ((++fi & 3) == 0 && fi < 64) fcur = frl[fi >> 2][t];
+    }
+    racc |= rank << (8 * (j & 3));
     if ((j & 3) == 3 || j + 1 == len) {
       sw[lane * 17 + ((j >> 2) & 15)] = racc;
       racc = 0;
     }
     // zero-run summary (RUNA/RUNB symbols of inner runs are counted here)
-    if (pos == 0) {
+    if (rank == 0) {
       z++;
-      return;
-    }
-    if (!seen) {
-      ld = z;
-      seen = true;
+      if (!fresh) return;
     } else {
-      cnt += nsym(z);
+      if (!seen) {
+        ld = z;
+        seen = true;
+      } else {
+        cnt += nsym(z);
+      }
+      z = 0;
+      cnt++;
     }
-    z = 0;
-    cnt++;
     // move c to the front: positions [0, pos) shift up by one byte
     const uint32_t tw = pos >> 2, tb = pos & 3;
     // word w takes its bytes 0..min(pos - 4w, 3) from the list shifted up by one byte
@@ -343,8 +455,8 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
         const uint32_t v = W[w];
         const uint32_t shifted = __builtin_amdgcn_alignbyte(v, prev, 3);
         const uint32_t sb = (uint32_t)min(max(nbits - 32 * w, 0), 32);
-        const uint32_t m = (uint32_t)((0xffffffffull << sb) >> 32);
-        W[w] = (shifted & m) | (v & ~m);
+        const uint32_t mk = (uint32_t)((0xffffffffull << sb) >> 32);
+        W[w] = (shifted & mk) | (v & ~mk);
         prev = v;
       }
     }
@@ -820,7 +932,13 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
   HIP_OK(hipMemsetAsync(n_hi, 0, 4, st));
   k_mtf_pick<<<g2, kT, 0, st>>>(r.boff, cbase, siglen, hi_list, n_hi);
   HIP_OK(hipGetLastError());
-  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, siglen, init, ranks, lead, trail, inner);
+  uint8_t* frank = nullptr;
+  if (kFirst) {
+    frank = ws.u8("mtf_frank", (size_t)nchunks * 64 + 64);
+    k_mtf_first<<<dim3(ceil_div(maxch, kT / 64), nb), kT, 0, st>>>(bwt, r.boff, cbase, siglen, init, frank);
+    HIP_OK(hipGetLastError());
+  }
+  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, siglen, init, frank, ranks, lead, trail, inner);
   HIP_OK(hipGetLastError());
   // grid for every chunk; workgroups past the picked count exit at once
   k_mtf_row<<<ceil_div(nchunks, kRowChunks), kT, 0, st>>>(bwt, r.boff, cbase, init, hi_list, n_hi, ranks, lead, trail,

@@ -562,16 +562,16 @@ struct S1sOwner {
 };
 
 // One packed pass in one kernel: counts, LDS reorder, stores of the slots and caches, and
-// the tile's buckets of two or more rotations as records (group:4 | start:14 | size:14,
+// the tile's buckets of two or more rotations as records (group:5 | start:13 | size:14,
 // tile-relative) in the tile's own part of `rec` (it starts at half the tile's first element
 // offset: a tile of n rotations has at most n / 2 such buckets), with the per-class counts for
 // the class-major scan.  k_s1s_emit turns the records into class-list entries.
 // Element rounds past the tile's size are skipped (uniform branches); loads are issued for
 // all rounds before their values are used, from addresses selected without branches.
 __device__ __forceinline__ uint32_t rec_pack(uint32_t j, uint32_t start, uint32_t size) {
-  return (j << 28) | (start << 14) | size;
+  return (j << 27) | (start << 14) | size;  // group:5 | start:13 | size:14 (tiles < 8192 rotations)
 }
-
+static_assert(kSGrp <= 32 && 2 * kSG <= 8192, "packed bucket records");
 __global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
                                                  const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
                                                  SortBufs B, SortOut O, uint32_t* __restrict__ rec,
@@ -741,7 +741,7 @@ __global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, con
   const uint32_t m = nrec[t];
   for (uint32_t x = lane; x < m; x += 64) {
     const uint32_t r = trec[x];
-    const uint32_t j = r >> 28, start = (r >> 14) & 0x3fffu, total = r & 0x3fffu;
+    const uint32_t j = r >> 27, start = (r >> 14) & 0x1fffu, total = r & 0x3fffu;
     const uint32_t fl = gfl[j];
     const uint32_t depth = grp_depth(Grp{0, 0, 0, fl}) + 1;
     const uint32_t cl = bucket_cls(total, depth);
@@ -1345,6 +1345,13 @@ __device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
 #ifndef BZG_S2_PRE
 #define BZG_S2_PRE 1
 #endif
+// the same two for the several-groups-per-wave classes (9..32)
+#ifndef BZG_S2_PRE_SEG
+#define BZG_S2_PRE_SEG 1
+#endif
+#ifndef BZG_OETS_SEG
+#define BZG_OETS_SEG 1
+#endif
 #ifndef BZG_OETS_MAX
 #define BZG_OETS_MAX 16
 #endif
@@ -1360,17 +1367,17 @@ __device__ __forceinline__ BsortKey key_shfl_down1(BsortKey k) {
 __device__ __forceinline__ BsortKey key_shfl_up1(BsortKey k) {
   return ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(k >> 32), 1, 64) << 32) | (uint32_t)__shfl_up((int)(uint32_t)k, 1, 64);
 }
-template <int kPer>
+template <int kSeg, int kPer>
 __device__ __forceinline__ void oets(BsortKey (&K)[kPer], uint32_t steps) {
-  const uint32_t lane = __lane_id();
+  const uint32_t lane = __lane_id(), sl = lane % kSeg;
   for (uint32_t s = 0; s < steps; s++) {
     const uint32_t par = s & 1u;
     if constexpr (kPer == 1) {
       // pairs (lane, lane + 1) with lane % 2 == par
       const BsortKey nx = key_shfl_down1(K[0]), pv = key_shfl_up1(K[0]);
       const bool left = (lane & 1u) == par;
-      if (left && lane < 63) K[0] = key_less(nx, K[0]) ? nx : K[0];
-      if (!left && lane > 0) K[0] = key_less(K[0], pv) ? pv : K[0];
+      if (left && sl < kSeg - 1) K[0] = key_less(nx, K[0]) ? nx : K[0];
+      if (!left && sl > 0) K[0] = key_less(K[0], pv) ? pv : K[0];
     } else {
       static_assert((kPer & 1) == 0, "even registers per lane");
       if (par == 0) {
@@ -1380,8 +1387,8 @@ __device__ __forceinline__ void oets(BsortKey (&K)[kPer], uint32_t steps) {
 #pragma unroll
         for (int r = 1; r + 1 < kPer; r += 2) key_ce(K[r], K[r + 1]);
         const BsortKey nx = key_shfl_down1(K[0]), pv = key_shfl_up1(K[kPer - 1]);
-        if (lane < 63 && key_less(nx, K[kPer - 1])) K[kPer - 1] = nx;
-        if (lane > 0 && key_less(K[0], pv)) K[0] = pv;
+        if (sl < kSeg - 1 && key_less(nx, K[kPer - 1])) K[kPer - 1] = nx;
+        if (sl > 0 && key_less(K[0], pv)) K[0] = pv;
       }
     }
   }
@@ -1630,7 +1637,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   __shared__ uint32_t TC[kT / 64][kTE];
   constexpr bool kCompact = kEmit && ((BZG_S2_COMPACT >> (kPer == 1 ? 3 : kPer == 2 ? 4 : 5)) & 1);
   __shared__ S2Compact SC[kCompact ? kT / 64 : 1];
-  constexpr bool kPre = kEmit && BZG_S2_PRE;
+  constexpr bool kPre = (kEmit || BZG_S2_PRE_SEG) && BZG_S2_PRE;
   __shared__ uint64_t Lx[kT / 64][kPre ? kE : 1];  // characters depth + 7 .. + 14 (second-round keys)
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   const uint32_t sl = lane % kSeg;
@@ -1723,8 +1730,8 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   constexpr int kDbgCls = kSeg * kPer == 16 ? 1 : kSeg * kPer == 32 ? 2 : kSeg * kPer == 64 ? 3 : kSeg * kPer == 128 ? 4 : 5;
   for (;;) {
     if (O.dbg && lane == 0) atomicAdd(&O.dbg[8 + 8 * kDbgCls + min(round, 6)], 1ull);
-    if (kSeg == 64 && BZG_OETS_MAX > 0 && round > 0 && maxrun <= BZG_OETS_MAX)
-      oets<kPer>(K, maxrun);
+    if ((kSeg == 64 || BZG_OETS_SEG) && BZG_OETS_MAX > 0 && round > 0 && maxrun <= BZG_OETS_MAX)
+      oets<kSeg, kPer>(K, maxrun);
     else
       bitonic<kSeg, kPer>(K);
     // ties with the previous / next position of the segment (same run start and key)
@@ -1825,7 +1832,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       }
       break;
     }
-    if constexpr (kSeg == 64) {
+    if constexpr (kSeg == 64 || BZG_OETS_SEG) {
       uint32_t ml = 0;
 #pragma unroll
       for (int r = 0; r < kPer; r++)
