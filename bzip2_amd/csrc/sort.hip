@@ -2022,6 +2022,161 @@ __global__ void __launch_bounds__(kT) k_fb_isa_all(const uint32_t* __restrict__ 
   B.isa[U.sbase + v] = U.sbase + q;
 }
 
+// ---------------------------------------------------------------- S3 pairs
+// Most deep groups are pairs, made by long repeated passages: rotations a and b = a + d tied
+// for >= h0 characters.  Their order is decided at the first position p >= a where
+// t[p] != t[p + d].  Consecutive pairs (a, a + d), (a + 1, a + d + 1), ... of one passage
+// share that position, so it is looked up once, after the pair at the end of the run:
+//   pm[x] = partner of x when x is in a deep pair (~0 otherwise); x links to x + 1 when
+//   pm[x + 1] = pm[x] + 1 (both in the unit); E(x) = the first unlinked position >= x;
+//   the order of (a, b) is the order of (E, pm[E]), tied for >= h0 characters: compare
+//   from E + h0 on (usually one character: the pair after E is tied for < h0).
+// Pairs whose comparison runs past kPairScan characters (the run continues into a larger
+// group) stay for the doubling.  Positions are unit-local; slots sbase + x.
+constexpr uint32_t kRunTile = 4096;  // positions per run-end tile (16 per thread)
+constexpr uint32_t kPairScan = 4096;
+
+__global__ void __launch_bounds__(kT) k_pm_init(const uint32_t* __restrict__ ulist, uint32_t nu, uint32_t chunks,
+                                                const Unit* __restrict__ units, uint32_t* __restrict__ pm) {
+  const uint32_t ui = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  if (ui >= nu) return;
+  const Unit U = units[ulist[ui]];
+  for (uint32_t q = ch * kT * 16 + threadIdx.x; q < min(U.len, (ch + 1) * kT * 16); q += kT) pm[U.sbase + q] = 0xffffffffu;
+}
+
+__global__ void __launch_bounds__(kT) k_pair_mark(const Grp* __restrict__ L, uint32_t n, SortBufs B,
+                                                  uint32_t* __restrict__ pm) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const Grp gr = L[g];
+  if (gr.size != 2) return;
+  const uint32_t sb = B.units[gr.unit].sbase;
+  const uint32_t a = B.sa[gr.start], b = B.sa[gr.start + 1];
+  pm[sb + a] = b;
+  pm[sb + b] = a;
+}
+
+// Run ends inside each tile of kRunTile positions of the listed units: E[x] (unit-local),
+// or ~0 when the run goes on past the tile; tsum[tile] = the tile's first unlinked position
+// (~0: none).  Tile (ui, c) has index tbase[ui] + c.
+__global__ void __launch_bounds__(kT) k_runend_tile(const uint32_t* __restrict__ ulist, const uint32_t* __restrict__ tbase,
+                                                    uint32_t nu, const Unit* __restrict__ units,
+                                                    const uint32_t* __restrict__ pm, uint32_t* __restrict__ E,
+                                                    uint32_t* __restrict__ tsum) {
+  __shared__ uint32_t fb[kT];
+  const uint32_t ui = blockIdx.y, c = blockIdx.x;
+  if (ui >= nu) return;
+  const Unit U = units[ulist[ui]];
+  const uint32_t t0 = c * kRunTile;
+  if (t0 >= U.len) return;  // (uniform)
+  const uint32_t* p = pm + U.sbase;
+  const uint32_t x0 = t0 + threadIdx.x * 16;
+  uint32_t v[17];
+#pragma unroll
+  for (int k = 0; k < 17; k++) v[k] = x0 + k < U.len ? p[x0 + k] : 0xffffffffu;
+  // x links to x + 1: both in the unit, x paired, and pm[x + 1] = pm[x] + 1 without wrapping
+  uint32_t lk = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t x = x0 + k;
+    const bool l = x + 1 < U.len && v[k] != 0xffffffffu && v[k] + 1 < U.len && v[k + 1] == v[k] + 1;
+    lk |= (l ? 1u : 0u) << k;
+  }
+  // first unlinked position of this thread's slice (every position past the unit end is one)
+  const uint32_t nl = ~lk & 0xffffu;
+  fb[threadIdx.x] = nl ? x0 + (uint32_t)__builtin_ctz(nl) : 0xffffffffu;
+  __syncthreads();
+  // suffix minimum over the threads after this one
+  for (uint32_t o = 1; o < kT; o <<= 1) {
+    const uint32_t y = threadIdx.x + o < kT ? fb[threadIdx.x + o] : 0xffffffffu;
+    __syncthreads();
+    fb[threadIdx.x] = min(fb[threadIdx.x], y);
+    __syncthreads();
+  }
+  const uint32_t after = threadIdx.x + 1 < kT ? fb[threadIdx.x + 1] : 0xffffffffu;
+  if (threadIdx.x == 0) tsum[tbase[ui] + c] = fb[0];
+  uint32_t e = after;
+#pragma unroll
+  for (int k = 15; k >= 0; k--) {
+    const uint32_t x = x0 + k;
+    if (!((lk >> k) & 1u)) e = x;
+    if (x < U.len && v[k] != 0xffffffffu) E[U.sbase + x] = e;
+  }
+}
+
+// F[tile] = the first unlinked position at or after the tile's start (walks the following
+// tiles of the unit; the unit's last position is always unlinked).
+__global__ void k_runend_tiles(const uint32_t* __restrict__ ulist, const uint32_t* __restrict__ tbase, uint32_t nu,
+                               const Unit* __restrict__ units, const uint32_t* __restrict__ tsum,
+                               uint32_t* __restrict__ F) {
+  const uint32_t ui = blockIdx.y, c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ui >= nu) return;
+  const uint32_t nt = ceil_div(units[ulist[ui]].len, kRunTile);
+  if (c >= nt) return;
+  const uint32_t tb = tbase[ui];
+  uint32_t k = c;
+  while (tsum[tb + k] == 0xffffffffu && k + 1 < nt) k++;
+  F[tb + c] = tsum[tb + k];
+}
+
+// Resolves the deep pairs; every other group (and a pair whose comparison runs long) goes to
+// R for the doubling.
+__global__ void __launch_bounds__(kT) k_pair_resolve(const Grp* __restrict__ L, uint32_t n, SortBufs B, SortOut O,
+                                                     const uint32_t* __restrict__ pm, const uint32_t* __restrict__ E,
+                                                     const uint32_t* __restrict__ F, const uint32_t* __restrict__ ulist_of,
+                                                     const uint32_t* __restrict__ tbase, uint32_t h0,
+                                                     Grp* __restrict__ R, uint32_t* __restrict__ nR) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  Grp gr{0, 0, 0, 0};
+  if (g < n) gr = L[g];
+  bool keep = g < n && gr.size != 2;
+  if (g < n && gr.size == 2) {
+    const Unit U = B.units[gr.unit];
+    const uint8_t* t = B.text + U.toff;
+    const uint32_t a = B.sa[gr.start], b = B.sa[gr.start + 1];
+    uint32_t e = E[U.sbase + a];
+    if (e == 0xffffffffu) e = F[tbase[ulist_of[gr.unit]] + a / kRunTile + 1];
+    const uint32_t f = pm[U.sbase + e];
+    // first mismatch of rotations e and f from character h0 on
+    uint32_t qe = cyc_pos(e, h0, U.len), qf = cyc_pos(f, h0, U.len);
+    int ord = 0;  // -1: e first, +1: f first
+    for (uint32_t k = 0; k < kPairScan && ord == 0; k += 4) {
+      uint32_t xe, xf;
+      if (qe + 4 <= U.len && qf + 4 <= U.len) {
+        xe = ld_be4(t + qe);
+        xf = ld_be4(t + qf);
+      } else {
+        xe = text_key4_wrap(t, U.len, qe);
+        xf = text_key4_wrap(t, U.len, qf);
+      }
+      if (xe != xf) ord = xe < xf ? -1 : 1;
+      qe += 4;
+      if (qe >= U.len) qe -= U.len;
+      qf += 4;
+      if (qf >= U.len) qf -= U.len;
+    }
+    if (ord == 0) {
+      keep = true;
+    } else {
+      // (a, b) orders as (e, f) = (a + j, b + j): the pairs between are tied, so their first
+      // characters agree
+      const bool a_first = ord < 0;
+      const uint32_t lo = a_first ? a : b, hi = a_first ? b : a;
+      B.sa[gr.start] = lo;
+      B.sa[gr.start + 1] = hi;
+      const uint32_t r = gr.start - U.sbase;
+      if (U.k == 1) {
+        O.bwt[U.toff + r] = t[lo == 0 ? U.len - 1 : lo - 1];
+        O.bwt[U.toff + r + 1] = t[hi == 0 ? U.len - 1 : hi - 1];
+      }
+      if (lo == 0) O.rank0[gr.unit] = r;
+      if (hi == 0) O.rank0[gr.unit] = r + 1;
+    }
+  }
+  const uint32_t p = wave_append(nR, keep);
+  if (keep) R[p] = gr;
+}
+
 // BWT bytes of the slots of the deep groups (everything else was written when its rotation
 // was ordered), for aperiodic units.
 __global__ void __launch_bounds__(kT) k_deep_out(const Grp* __restrict__ L0, uint32_t n, const Unit* __restrict__ units,
@@ -2481,16 +2636,71 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     }
     k_fb_copy<<<grid(n_deep), kT, 0, st>>>(O.deep, n_deep, L0, B);
     HIP_OK(hipGetLastError());
+    static const bool pairs = [] {
+      const char* e = getenv("BZG_S3_PAIRS");
+      return !e || atoi(e) != 0;
+    }();
+    uint32_t n_left = n_deep;
+    if (pairs) {  // deep pairs by their run's first mismatch (k_pair_resolve)
+      const uint32_t nu = (uint32_t)fb_units.size();
+      std::vector<uint32_t> htb(nu + 1, 0u), huo(nb, 0u);
+      uint32_t maxt = 0;
+      for (uint32_t i = 0; i < nu; i++) {
+        const uint32_t nt = ceil_div(hu[fb_units[i]].len, kRunTile);
+        htb[i + 1] = htb[i] + nt;
+        maxt = std::max(maxt, nt);
+        huo[fb_units[i]] = i;
+      }
+      uint32_t* tbase = ws.u32("sort_p_tbase", nu + 16);
+      uint32_t* uof = ws.u32("sort_p_uof", nb + 16);
+      uint32_t* tsum = ws.u32("sort_p_tsum", htb[nu] + 16);
+      uint32_t* F = ws.u32("sort_p_F", htb[nu] + 16);
+      Grp* R = ws.typed<Grp>("sort_p_R", n_deep + 16);
+      HIP_OK(hipMemcpyAsync(tbase, htb.data(), 4 * (nu + 1), hipMemcpyHostToDevice, st));
+      HIP_OK(hipMemcpyAsync(uof, huo.data(), 4 * nb, hipMemcpyHostToDevice, st));
+      uint32_t* pm = B.key;
+      uint32_t* E = B.key2;
+      const uint32_t pch = ceil_div(flen, kT * 16);
+      k_pm_init<<<nu * pch, kT, 0, st>>>(ulist, nu, pch, units, pm);
+      k_pair_mark<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, pm);
+      k_runend_tile<<<dim3(maxt, nu), kT, 0, st>>>(ulist, tbase, nu, units, pm, E, tsum);
+      k_runend_tiles<<<dim3(ceil_div(maxt, kT), nu), kT, 0, st>>>(ulist, tbase, nu, units, tsum, F);
+      HIP_OK(hipMemsetAsync(cnt + 21, 0, 4, st));
+      k_pair_resolve<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, O, pm, E, F, uof, tbase, h0, R, cnt + 21);
+      HIP_OK(hipGetLastError());
+      read_counters();
+      n_left = hc[21];
+      if (debug) fprintf(stderr, "[bzg sort S3] pairs resolved %u of %u deep groups\n", n_deep - n_left, n_deep);
+      HIP_OK(hipMemcpyAsync(L0, R, sizeof(Grp) * n_left, hipMemcpyDeviceToDevice, st));
+      // the units that still have deep groups
+      fb_units.clear();
+      flen = 0;
+      if (n_left) {
+        HIP_OK(hipMemsetAsync(uflag, 0, 4 * (size_t)nb, st));
+        HIP_OK(hipMemsetAsync(cnt + 20, 0xff, 4, st));
+        k_fb_flag<<<grid(n_left), kT, 0, st>>>(L0, n_left, uflag, cnt + 20);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpyAsync(hf.data(), uflag, 4 * (size_t)nb, hipMemcpyDeviceToHost, st));
+        read_counters();  // (L0's flags are reset: h0 stays the minimum depth of the deep list)
+        for (uint32_t b = 0; b < nb; b++)
+          if (hf[b]) {
+            fb_units.push_back(b);
+            flen = std::max(flen, hu[b].len * hu[b].k);
+          }
+        HIP_OK(hipMemcpyAsync(ulist, fb_units.data(), 4 * fb_units.size(), hipMemcpyHostToDevice, st));
+      }
+    }
+    if (n_left > 0) {
     {
       const uint32_t nu = (uint32_t)fb_units.size(), chunks = ceil_div(flen, kT);
       k_fb_isa_all<<<kNumXcd * ceil_div(nu, kNumXcd) * chunks, kT, 0, st>>>(ulist, nu, chunks, units, B);
     }
     HIP_OK(hipGetLastError());
-    k_fb_group_isa<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B);
+    k_fb_group_isa<<<grid(n_left), kT, 0, st>>>(L0, n_left, B);
     HIP_OK(hipGetLastError());
     if (debug) {
-      std::vector<Grp> hd(n_deep);
-      HIP_OK(hipMemcpyAsync(hd.data(), L0, sizeof(Grp) * n_deep, hipMemcpyDeviceToHost, st));
+      std::vector<Grp> hd(n_left);
+      HIP_OK(hipMemcpyAsync(hd.data(), L0, sizeof(Grp) * n_left, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
       uint64_t tot = 0, mx = 0, hist[5] = {0, 0, 0, 0, 0};
       for (const Grp& g : hd) {
@@ -2499,19 +2709,20 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         hist[std::min<uint32_t>(g.size, 4)]++;
       }
       fprintf(stderr, "[bzg sort S3] deep groups=%u elems=%llu max=%llu sizes 0:%llu 1:%llu 2:%llu 3:%llu 4+:%llu units=%zu h0=%u\n",
-              n_deep, (unsigned long long)tot, (unsigned long long)mx, (unsigned long long)hist[0],
+              n_left, (unsigned long long)tot, (unsigned long long)mx, (unsigned long long)hist[0],
               (unsigned long long)hist[1], (unsigned long long)hist[2], (unsigned long long)hist[3],
               (unsigned long long)hist[4], fb_units.size(), h0);
     }
-    doubling_sort(ws, B, L0, n_deep, h0, &dbl_iters, &dbl_elems, st);
+    doubling_sort(ws, B, L0, n_left, h0, &dbl_iters, &dbl_elems, st);
     if (getenv("BZG_FULL_UNIT_OUT")) {
       k_unit_out<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B.sa, r.blk, bwt);
     } else {
-      k_deep_out<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, units, B.sa, r.blk, bwt);
+      k_deep_out<<<grid(n_left), kT, 0, st>>>(L0, n_left, units, B.sa, r.blk, bwt);
     }
     HIP_OK(hipGetLastError());
     k_rank0_isa<<<grid(fb_units.size()), kT, 0, st>>>(ulist, (uint32_t)fb_units.size(), units, B.isa, rank0);
     HIP_OK(hipGetLastError());
+    }
   }
   if (!quasi.empty()) {
     k_qsa<<<dim3(std::min<uint32_t>(ceil_div(qmax, kT), 1024u), (unsigned)hq.size()), kT, 0, st>>>(dq, dqt, r.blk, bwt,
