@@ -2034,7 +2034,7 @@ __global__ void __launch_bounds__(kT) k_fb_isa_all(const uint32_t* __restrict__ 
 // Pairs whose comparison runs past kPairScan characters (the run continues into a larger
 // group) stay for the doubling.  Positions are unit-local; slots sbase + x.
 constexpr uint32_t kRunTile = 4096;  // positions per run-end tile (16 per thread)
-constexpr uint32_t kPairScan = 4096;
+constexpr uint32_t kPairScan = 1u << 20;  // characters a run-end pair compares at most
 
 __global__ void __launch_bounds__(kT) k_pm_init(const uint32_t* __restrict__ ulist, uint32_t nu, uint32_t chunks,
                                                 const Unit* __restrict__ units, uint32_t* __restrict__ pm) {
@@ -2119,58 +2119,86 @@ __global__ void k_runend_tiles(const uint32_t* __restrict__ ulist, const uint32_
   F[tb + c] = tsum[tb + k];
 }
 
-// Resolves the deep pairs; every other group (and a pair whose comparison runs long) goes to
-// R for the doubling.
+// First mismatch of rotations e and f (tied for >= h0 characters) within `limit` characters
+// from character h0: -1 (e first), +1 (f first) or 0 (none found).  16 characters per step.
+__device__ int pair_order(const uint8_t* t, uint32_t len, uint32_t e, uint32_t f, uint32_t h0, uint32_t limit) {
+  uint32_t qe = cyc_pos(e, h0, len), qf = cyc_pos(f, h0, len);
+  for (uint32_t k = 0; k < limit; k += 16) {
+    uint32_t xe[4], xf[4];
+    if (qe + 16 <= len && qf + 16 <= len) {
+      text_key16(t, len, qe, xe);
+      text_key16(t, len, qf, xf);
+    } else {
+      text_words_wrap<4>(t, len, qe, xe);
+      text_words_wrap<4>(t, len, qf, xf);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+      if (xe[w] != xf[w]) return xe[w] < xf[w] ? -1 : 1;
+    qe += 16;
+    if (qe >= len) qe -= len;
+    qf += 16;
+    if (qf >= len) qf -= len;
+  }
+  return 0;
+}
+
+// Orders the pair in slots (start, start + 1): lo first.
+__device__ __forceinline__ void pair_write(const SortBufs& B, const SortOut& O, const Grp& gr, const Unit& U,
+                                           const uint8_t* t, uint32_t lo, uint32_t hi) {
+  B.sa[gr.start] = lo;
+  B.sa[gr.start + 1] = hi;
+  const uint32_t r = gr.start - U.sbase;
+  if (U.k == 1) {
+    O.bwt[U.toff + r] = t[lo == 0 ? U.len - 1 : lo - 1];
+    O.bwt[U.toff + r + 1] = t[hi == 0 ? U.len - 1 : hi - 1];
+  }
+  if (lo == 0) O.rank0[gr.unit] = r;
+  if (hi == 0) O.rank0[gr.unit] = r + 1;
+}
+
+// Run-end pairs (a unlinked: the pair that ends its run) compare their rotations directly, up
+// to kPairScan characters, and publish the result for both members (ordat: 1 = this
+// rotation first, 2 = the partner first, 0 = undecided) for the rest of the run.
+__global__ void __launch_bounds__(kT) k_pair_end(const Grp* __restrict__ L, uint32_t n, SortBufs B, SortOut O,
+                                                 const uint32_t* __restrict__ E, uint32_t h0, uint32_t* __restrict__ ordat) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const Grp gr = L[g];
+  if (gr.size != 2) return;
+  const Unit U = B.units[gr.unit];
+  const uint32_t a = B.sa[gr.start], b = B.sa[gr.start + 1];
+  if (E[U.sbase + a] != a) return;
+  const uint8_t* t = B.text + U.toff;
+  const int ord = pair_order(t, U.len, a, b, h0, kPairScan);
+  ordat[U.sbase + a] = ord == 0 ? 0u : ord < 0 ? 1u : 2u;
+  ordat[U.sbase + b] = ord == 0 ? 0u : ord < 0 ? 2u : 1u;
+}
+
+// Every pair takes the order of its run's end pair (a, b) ~ (a + j, b + j): the pairs
+// between are tied, so their first characters agree.  Other groups, and pairs left
+// undecided, go to R for the doubling.
 __global__ void __launch_bounds__(kT) k_pair_resolve(const Grp* __restrict__ L, uint32_t n, SortBufs B, SortOut O,
-                                                     const uint32_t* __restrict__ pm, const uint32_t* __restrict__ E,
-                                                     const uint32_t* __restrict__ F, const uint32_t* __restrict__ ulist_of,
-                                                     const uint32_t* __restrict__ tbase, uint32_t h0,
-                                                     Grp* __restrict__ R, uint32_t* __restrict__ nR) {
+                                                     const uint32_t* __restrict__ E, const uint32_t* __restrict__ F,
+                                                     const uint32_t* __restrict__ ulist_of,
+                                                     const uint32_t* __restrict__ tbase,
+                                                     const uint32_t* __restrict__ ordat, Grp* __restrict__ R,
+                                                     uint32_t* __restrict__ nR) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   Grp gr{0, 0, 0, 0};
   if (g < n) gr = L[g];
   bool keep = g < n && gr.size != 2;
   if (g < n && gr.size == 2) {
     const Unit U = B.units[gr.unit];
-    const uint8_t* t = B.text + U.toff;
     const uint32_t a = B.sa[gr.start], b = B.sa[gr.start + 1];
     uint32_t e = E[U.sbase + a];
     if (e == 0xffffffffu) e = F[tbase[ulist_of[gr.unit]] + a / kRunTile + 1];
-    const uint32_t f = pm[U.sbase + e];
-    // first mismatch of rotations e and f from character h0 on
-    uint32_t qe = cyc_pos(e, h0, U.len), qf = cyc_pos(f, h0, U.len);
-    int ord = 0;  // -1: e first, +1: f first
-    for (uint32_t k = 0; k < kPairScan && ord == 0; k += 4) {
-      uint32_t xe, xf;
-      if (qe + 4 <= U.len && qf + 4 <= U.len) {
-        xe = ld_be4(t + qe);
-        xf = ld_be4(t + qf);
-      } else {
-        xe = text_key4_wrap(t, U.len, qe);
-        xf = text_key4_wrap(t, U.len, qf);
-      }
-      if (xe != xf) ord = xe < xf ? -1 : 1;
-      qe += 4;
-      if (qe >= U.len) qe -= U.len;
-      qf += 4;
-      if (qf >= U.len) qf -= U.len;
-    }
-    if (ord == 0) {
+    const uint32_t o = ordat[U.sbase + e];
+    if (o == 0) {
       keep = true;
     } else {
-      // (a, b) orders as (e, f) = (a + j, b + j): the pairs between are tied, so their first
-      // characters agree
-      const bool a_first = ord < 0;
-      const uint32_t lo = a_first ? a : b, hi = a_first ? b : a;
-      B.sa[gr.start] = lo;
-      B.sa[gr.start + 1] = hi;
-      const uint32_t r = gr.start - U.sbase;
-      if (U.k == 1) {
-        O.bwt[U.toff + r] = t[lo == 0 ? U.len - 1 : lo - 1];
-        O.bwt[U.toff + r + 1] = t[hi == 0 ? U.len - 1 : hi - 1];
-      }
-      if (lo == 0) O.rank0[gr.unit] = r;
-      if (hi == 0) O.rank0[gr.unit] = r + 1;
+      const bool a_first = o == 1;
+      pair_write(B, O, gr, U, B.text + U.toff, a_first ? a : b, a_first ? b : a);
     }
   }
   const uint32_t p = wave_append(nR, keep);
@@ -2666,7 +2694,9 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_runend_tile<<<dim3(maxt, nu), kT, 0, st>>>(ulist, tbase, nu, units, pm, E, tsum);
       k_runend_tiles<<<dim3(ceil_div(maxt, kT), nu), kT, 0, st>>>(ulist, tbase, nu, units, tsum, F);
       HIP_OK(hipMemsetAsync(cnt + 21, 0, 4, st));
-      k_pair_resolve<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, O, pm, E, F, uof, tbase, h0, R, cnt + 21);
+      uint32_t* ordat = B.isa;  // (the ISA is built afterwards, for the groups left)
+      k_pair_end<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, O, E, h0, ordat);
+      k_pair_resolve<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, O, E, F, uof, tbase, ordat, R, cnt + 21);
       HIP_OK(hipGetLastError());
       read_counters();
       n_left = hc[21];
