@@ -2034,7 +2034,8 @@ __global__ void __launch_bounds__(kT) k_fb_isa_all(const uint32_t* __restrict__ 
 // Pairs whose comparison runs past kPairScan characters (the run continues into a larger
 // group) stay for the doubling.  Positions are unit-local; slots sbase + x.
 constexpr uint32_t kRunTile = 4096;  // positions per run-end tile (16 per thread)
-constexpr uint32_t kPairScan = 1u << 20;  // characters a run-end pair compares at most
+constexpr uint32_t kPairShort = 2048;    // characters a run-end pair compares on its own lane
+constexpr uint32_t kPairScan = 1u << 20;  // and on a whole wave (k_pair_long), at most
 
 __global__ void __launch_bounds__(kT) k_pm_init(const uint32_t* __restrict__ ulist, uint32_t nu, uint32_t chunks,
                                                 const Unit* __restrict__ units, uint32_t* __restrict__ pm) {
@@ -2160,19 +2161,59 @@ __device__ __forceinline__ void pair_write(const SortBufs& B, const SortOut& O, 
 // Run-end pairs (a unlinked: the pair that ends its run) compare their rotations directly, up
 // to kPairScan characters, and publish the result for both members (ordat: 1 = this
 // rotation first, 2 = the partner first, 0 = undecided) for the rest of the run.
-__global__ void __launch_bounds__(kT) k_pair_end(const Grp* __restrict__ L, uint32_t n, SortBufs B, SortOut O,
-                                                 const uint32_t* __restrict__ E, uint32_t h0, uint32_t* __restrict__ ordat) {
+__global__ void __launch_bounds__(kT) k_pair_end(const Grp* __restrict__ L, uint32_t n, SortBufs B,
+                                                 const uint32_t* __restrict__ E, uint32_t h0, uint32_t* __restrict__ ordat,
+                                                 Grp* __restrict__ lng, uint32_t* __restrict__ nlong) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n) return;
-  const Grp gr = L[g];
-  if (gr.size != 2) return;
-  const Unit U = B.units[gr.unit];
-  const uint32_t a = B.sa[gr.start], b = B.sa[gr.start + 1];
-  if (E[U.sbase + a] != a) return;
+  Grp gr{0, 0, 0, 0};
+  if (g < n) gr = L[g];
+  const bool pair = g < n && gr.size == 2;
+  Unit U{0, 1, 0, 1};
+  uint32_t a = 0, b = 0;
+  if (pair) {
+    U = B.units[gr.unit];
+    a = B.sa[gr.start];
+    b = B.sa[gr.start + 1];
+  }
+  const bool end = pair && E[U.sbase + a] == a;
   const uint8_t* t = B.text + U.toff;
-  const int ord = pair_order(t, U.len, a, b, h0, kPairScan);
-  ordat[U.sbase + a] = ord == 0 ? 0u : ord < 0 ? 1u : 2u;
-  ordat[U.sbase + b] = ord == 0 ? 0u : ord < 0 ? 2u : 1u;
+  const int ord = end ? pair_order(t, U.len, a, b, h0, kPairShort) : 0;
+  if (end) {
+    ordat[U.sbase + a] = ord == 0 ? 0u : ord < 0 ? 1u : 2u;
+    ordat[U.sbase + b] = ord == 0 ? 0u : ord < 0 ? 2u : 1u;
+  }
+  const uint32_t p = wave_append(nlong, end && ord == 0);  // longer comparisons: k_pair_long
+  if (end && ord == 0) lng[p] = gr;
+}
+
+// Run-end pairs still tied after kPairShort characters (the run ends inside a larger group),
+// one wave each: the lanes compare consecutive 16-character pieces, 1024 characters per step.
+__global__ void __launch_bounds__(kT) k_pair_long(const Grp* __restrict__ lng, const uint32_t* __restrict__ nlong,
+                                                  SortBufs B, uint32_t h0, uint32_t* __restrict__ ordat) {
+  const uint32_t wv = blockIdx.x * (kT / 64) + (threadIdx.x >> 6), lane = __lane_id();
+  if (wv >= *nlong) return;
+  const Grp gr = lng[wv];
+  const Unit U = B.units[gr.unit];
+  const uint8_t* t = B.text + U.toff;
+  const uint32_t a = B.sa[gr.start], b = B.sa[gr.start + 1];
+  const uint32_t base = h0 + kPairShort;
+  int ord = 0;
+  for (uint32_t k = 0; k < kPairScan && ord == 0; k += 64 * 16) {
+    const uint32_t off = base + k + 16 * lane;
+    uint32_t xe[4], xf[4];
+    text_key16(t, U.len, cyc_pos(a, off % U.len, U.len), xe);
+    text_key16(t, U.len, cyc_pos(b, off % U.len, U.len), xf);
+    int o = 0;
+#pragma unroll
+    for (int w = 3; w >= 0; w--)
+      if (xe[w] != xf[w]) o = xe[w] < xf[w] ? -1 : 1;
+    const uint64_t m = __ballot(o != 0);
+    if (m) ord = __shfl(o, __ffsll((unsigned long long)m) - 1, 64);
+  }
+  if (lane == 0) {
+    ordat[U.sbase + a] = ord == 0 ? 0u : ord < 0 ? 1u : 2u;
+    ordat[U.sbase + b] = ord == 0 ? 0u : ord < 0 ? 2u : 1u;
+  }
 }
 
 // Every pair takes the order of its run's end pair (a, b) ~ (a + j, b + j): the pairs
@@ -2695,7 +2736,14 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_runend_tiles<<<dim3(ceil_div(maxt, kT), nu), kT, 0, st>>>(ulist, tbase, nu, units, tsum, F);
       HIP_OK(hipMemsetAsync(cnt + 21, 0, 4, st));
       uint32_t* ordat = B.isa;  // (the ISA is built afterwards, for the groups left)
-      k_pair_end<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, O, E, h0, ordat);
+      HIP_OK(hipMemsetAsync(cnt + 22, 0, 4, st));
+      k_pair_end<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, E, h0, ordat, R, cnt + 22);
+      {  // (R holds the long ones until k_pair_resolve refills it; waves past the count exit)
+        uint32_t nlong = 0;
+        HIP_OK(hipMemcpyAsync(&nlong, cnt + 22, 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (nlong) k_pair_long<<<ceil_div(nlong, kT / 64), kT, 0, st>>>(R, cnt + 22, B, h0, ordat);
+      }
       k_pair_resolve<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, O, E, F, uof, tbase, ordat, R, cnt + 21);
       HIP_OK(hipGetLastError());
       read_counters();
