@@ -75,6 +75,7 @@ struct SortOut {
   uint32_t* rank0;   // slot of rotation 0 relative to its unit
   Grp* deep;         // groups left for the doubling fallback
   uint32_t* n_deep;
+  Grp* tdeep;        // k_tiny<2>: the deep pair of bucket i at [i] (zeroed before; k_deep_compact appends them)
   unsigned long long* dbg;  // BZG_DEBUG counters (null otherwise)
 };
 
@@ -1181,10 +1182,12 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
         member(lane ^ 6u, g8_xor<6>(cls, hc));
         member(lane ^ 7u, g8_xor<7>(cls, hc));
       }
-      if (deep_now && !done) {
-        B.sa[s0 + pos + r] = v;
-        const uint32_t ds = wave_append(O.n_deep, r == 0);  // one atomic per wave
-        if (r == 0) O.deep[ds] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
+      if (deep_now && !done) B.sa[s0 + pos + r] = v;
+      if constexpr (kW == 2) {  // a pair bucket is one deep group: its own slot, no atomics
+        if (deep_now && !done && r == 0) O.tdeep[bi] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
+      } else {
+        const uint32_t ds = wave_append(O.n_deep, deep_now && !done && r == 0);  // one atomic per wave
+        if (deep_now && !done && r == 0) O.deep[ds] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
       }
       if (deep_now) break;
     }
@@ -1240,6 +1243,32 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
     }
     d += 16;
   }
+}
+
+// The deep pairs of a k_tiny<2> launch (entries of size 0: none) appended to the deep list,
+// one atomic per workgroup of 4096 entries (a single-address atomic per wave, 1.5 M of them
+// for long repeats, serialised to tens of ms).
+constexpr uint32_t kCompactPer = 16;
+__global__ void __launch_bounds__(kT) k_deep_compact(const Grp* __restrict__ in, uint32_t n, Grp* __restrict__ out,
+                                                     uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t base;
+  const uint32_t i0 = (blockIdx.x * kT + threadIdx.x) * kCompactPer;
+  Grp g[kCompactPer];
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kCompactPer; j++) {
+    g[j] = i0 + j < n ? in[i0 + j] : Grp{0, 0, 0, 0};
+    k += g[j].size ? 1u : 0u;
+  }
+  uint32_t tot;
+  const uint32_t ex = block_incl_sum(k, sh, &tot) - k;
+  if (threadIdx.x == 0) base = tot ? atomicAdd(cnt, tot) : 0u;
+  __syncthreads();
+  uint32_t p = base + ex;
+#pragma unroll
+  for (uint32_t j = 0; j < kCompactPer; j++)
+    if (g[j].size) out[p++] = g[j];
 }
 
 // ---- buckets of 9..256 rotations: one segment of kSeg lanes x kPer registers per bucket
@@ -2433,6 +2462,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   O.bwt = bwt;
   O.rank0 = rank0;
   O.deep = ws.typed<Grp>("sort_deep", S / 2 + nb + 16);
+  O.tdeep = ws.typed<Grp>("sort_tdeep", ccap[0]);
   O.dbg = nullptr;
   if (getenv("BZG_DEBUG")) {
     O.dbg = reinterpret_cast<unsigned long long*>(ws.u32("sort_dbg", 128));
@@ -2621,7 +2651,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         uint32_t hn[2];
         HIP_OK(hipMemcpyAsync(hn, cnt + 32, 8, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
-        if (hn[0]) k_tiny<2><<<ceil_div(hn[0], 32 * (kT / 64)), kT, 0, st>>>(tiny2, hn[0], B, O);
+        if (hn[0]) {
+          HIP_OK(hipMemsetAsync(O.tdeep, 0, sizeof(Grp) * hn[0], st));
+          k_tiny<2><<<ceil_div(hn[0], 32 * (kT / 64)), kT, 0, st>>>(tiny2, hn[0], B, O);
+          k_deep_compact<<<ceil_div(hn[0], kT * kCompactPer), kT, 0, st>>>(O.tdeep, hn[0], O.deep, O.n_deep);
+        }
         if (hn[1]) k_tiny<8><<<ceil_div(hn[1], 8 * (kT / 64)), kT, 0, st>>>(tiny8, hn[1], B, O);
       }
       if (ncls[1]) k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
