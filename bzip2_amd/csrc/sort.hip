@@ -76,6 +76,9 @@ struct SortOut {
   Grp* deep;         // groups left for the doubling fallback
   uint32_t* n_deep;
   Grp* tdeep;        // k_tiny<2>: the deep pair of bucket i at [i] (zeroed before; k_deep_compact appends them)
+  Grp* dslot;        // classes 9..32: group i's deep groups at [i * dm, + dnum[i]) (k_deep_compact2 appends them)
+  uint32_t* dnum;
+  uint32_t dm;
   unsigned long long* dbg;  // BZG_DEBUG counters (null otherwise)
 };
 
@@ -1149,6 +1152,9 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
     }
   }
   if (!__ballot(act)) return;
+  if constexpr (kW == 8) {
+    if (bi < n_tiny && el == 0) O.dnum[bi] = 0;  // (the deep branch counts the bucket's deep groups)
+  }
   Unit U{0, 1, 0, 1};
   if (act) U = B.units[unit];
   const uint8_t* t = B.text + U.toff;
@@ -1185,9 +1191,11 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
       if (deep_now && !done) B.sa[s0 + pos + r] = v;
       if constexpr (kW == 2) {  // a pair bucket is one deep group: its own slot, no atomics
         if (deep_now && !done && r == 0) O.tdeep[bi] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
-      } else {
-        const uint32_t ds = wave_append(O.n_deep, deep_now && !done && r == 0);  // one atomic per wave
-        if (deep_now && !done && r == 0) O.deep[ds] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
+      } else {  // at most 4 deep groups per bucket: the bucket's own slots
+        const bool lead = deep_now && !done && r == 0;
+        const uint64_t bl = __ballot(lead) & (0xffull << (lane & ~7u));
+        if (lead) O.dslot[(size_t)bi * 4 + __popcll(bl & lanemask_lt())] = Grp{s0 + pos, cnt, unit, grp_flags(0u, d, 1u)};
+        if (deep_now && el == 0 && bi < n_tiny) O.dnum[bi] = (uint32_t)__popcll(bl);
       }
       if (deep_now) break;
     }
@@ -1269,6 +1277,29 @@ __global__ void __launch_bounds__(kT) k_deep_compact(const Grp* __restrict__ in,
 #pragma unroll
   for (uint32_t j = 0; j < kCompactPer; j++)
     if (g[j].size) out[p++] = g[j];
+}
+
+// Deep groups in per-item slots ([i * m, i * m + num[i])) appended to the deep list, one
+// atomic per workgroup.
+__global__ void __launch_bounds__(kT) k_deep_compact2(const Grp* __restrict__ slot, const uint32_t* __restrict__ num,
+                                                      uint32_t n, uint32_t m, Grp* __restrict__ out,
+                                                      uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t base;
+  const uint32_t i0 = (blockIdx.x * kT + threadIdx.x) * kCompactPer;
+  uint32_t c[kCompactPer], k = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kCompactPer; j++) {
+    c[j] = i0 + j < n ? num[i0 + j] : 0u;
+    k += c[j];
+  }
+  uint32_t tot;
+  const uint32_t ex = block_incl_sum(k, sh, &tot) - k;
+  if (threadIdx.x == 0) base = tot ? atomicAdd(cnt, tot) : 0u;
+  __syncthreads();
+  uint32_t p = base + ex;
+  for (uint32_t j = 0; j < kCompactPer; j++)
+    for (uint32_t x = 0; x < c[j]; x++) out[p++] = slot[(size_t)(i0 + j) * m + x];
 }
 
 // ---- buckets of 9..256 rotations: one segment of kSeg lanes x kPer registers per bucket
@@ -1430,7 +1461,7 @@ __device__ __forceinline__ void oets(BsortKey (&K)[kPer], uint32_t steps) {
 
 
 template <int kSeg, int kPer, bool kBatch>
-__device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, const Unit& U, uint32_t depth,
+__device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, uint32_t bi, const Unit& U, uint32_t depth,
                            const BsortKey (&K)[kPer], const bool (&done)[kPer], const uint32_t (&rsn)[kPer],
                            const uint32_t* Lv, uint32_t* Lk, uint4* TK, uint32_t* TC) {
   constexpr int kN = kSeg * kPer;
@@ -1487,20 +1518,25 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, co
     }
     wave_sync();
     if (deep) {  // still tied after B.dwave characters: leave to the doubling fallback
-#pragma unroll
-      for (int r = 0; r < kPer; r++)
-        if (live[r]) {
-          const uint32_t p = sl * kPer + r;
-          uint32_t rank = 0, cnt = 0;
-          for (uint32_t q = rsn[r]; q < rsn[r] + rlen[r]; q++)
-            if (TC[sb + q] == cls[r]) {
-              cnt++;
-              rank += q < p;
-            }
-          B.sa[g.start + pos[r] + rank] = v[r];
-          const uint32_t ds = wave_append(O.n_deep, rank == 0);  // one atomic per wave
-          if (rank == 0) O.deep[ds] = Grp{g.start + pos[r], cnt, g.unit, grp_flags(0u, depth, 2u)};
-        }
+      static_assert(kPer == 1, "one rotation per lane: a segment's deep groups are counted by ballot");
+      // (all lanes of a segment take this branch together: depth is the segment's)
+      const uint32_t p = sl;
+      uint32_t rank = 0, cnt = 0;
+      if (live[0]) {
+        for (uint32_t q = rsn[0]; q < rsn[0] + rlen[0]; q++)
+          if (TC[sb + q] == cls[0]) {
+            cnt++;
+            rank += q < p;
+          }
+        B.sa[g.start + pos[0] + rank] = v[0];
+      }
+      // the segment's deep groups go to its own slots (a single-address atomic per wave
+      // serialises when long repeats make millions of them)
+      const bool lead = live[0] && rank == 0;
+      const uint64_t seg = (kSeg == 64 ? ~0ull : ((1ull << kSeg) - 1ull)) << (lane - sl);
+      const uint64_t bl = __ballot(lead) & seg;
+      if (lead) O.dslot[(size_t)bi * O.dm + __popcll(bl & lanemask_lt())] = Grp{g.start + pos[0], cnt, g.unit, grp_flags(0u, depth, 2u)};
+      if (sl == 0) O.dnum[bi] = (uint32_t)__popcll(bl);
       break;
     }
 #pragma unroll
@@ -1675,6 +1711,9 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   if (__ballot(has) == 0) return;
   Grp g{0, 0, 0, 0};
   if (has) g = L[bi];
+  if constexpr (!kEmit) {
+    if (has && sl == 0) O.dnum[bi] = 0;  // (bsort_tail counts the group's deep groups here)
+  }
   Unit U{0, 1, 0, 1};
   if (has) U = B.units[g.unit];
   const uint8_t* t = B.text + U.toff;
@@ -1857,7 +1896,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         }
       } else {
         if (O.dbg && lane == 0) atomicAdd(&O.dbg[8 + 8 * kDbgCls + 7], 1ull);
-        bsort_tail<kSeg, kPer, kBatch>(B, O, g, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
+        bsort_tail<kSeg, kPer, kBatch>(B, O, g, bi, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       }
       break;
     }
@@ -2656,10 +2695,34 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
           k_tiny<2><<<ceil_div(hn[0], 32 * (kT / 64)), kT, 0, st>>>(tiny2, hn[0], B, O);
           k_deep_compact<<<ceil_div(hn[0], kT * kCompactPer), kT, 0, st>>>(O.tdeep, hn[0], O.deep, O.n_deep);
         }
-        if (hn[1]) k_tiny<8><<<ceil_div(hn[1], 8 * (kT / 64)), kT, 0, st>>>(tiny8, hn[1], B, O);
+        if (hn[1]) {
+          SortOut O8 = O;
+          O8.dm = 4;
+          O8.dslot = ws.typed<Grp>("sort_dslot8", (size_t)hn[1] * 4);
+          O8.dnum = ws.u32("sort_dnum8", hn[1]);
+          k_tiny<8><<<ceil_div(hn[1], 8 * (kT / 64)), kT, 0, st>>>(tiny8, hn[1], B, O8);
+          k_deep_compact2<<<ceil_div(hn[1], kT * kCompactPer), kT, 0, st>>>(O8.dslot, O8.dnum, hn[1], 4u, O.deep,
+                                                                           O.n_deep);
+        }
       }
-      if (ncls[1]) k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O);
-      if (ncls[2]) k_bsort<32, 1, 2, false><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O);
+      if (ncls[1]) {
+        SortOut O1 = O;
+        O1.dm = 8;  // a segment of 16 has at most 8 deep groups
+        O1.dslot = ws.typed<Grp>("sort_dslot1", (size_t)ncls[1] * O1.dm);
+        O1.dnum = ws.u32("sort_dnum1", ncls[1]);
+        k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O1);
+        k_deep_compact2<<<ceil_div(ncls[1], kT * kCompactPer), kT, 0, st>>>(O1.dslot, O1.dnum, ncls[1], O1.dm, O.deep,
+                                                                             O.n_deep);
+      }
+      if (ncls[2]) {
+        SortOut O2 = O;
+        O2.dm = 16;
+        O2.dslot = ws.typed<Grp>("sort_dslot2", (size_t)ncls[2] * O2.dm);
+        O2.dnum = ws.u32("sort_dnum2", ncls[2]);
+        k_bsort<32, 1, 2, false><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O2);
+        k_deep_compact2<<<ceil_div(ncls[2], kT * kCompactPer), kT, 0, st>>>(O2.dslot, O2.dnum, ncls[2], O2.dm, O.deep,
+                                                                             O.n_deep);
+      }
       HIP_OK(hipGetLastError());
       const uint32_t total = ncls[3] + ncls[4] + ncls[5];
       if (total == 0) break;
