@@ -201,7 +201,15 @@ __device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_
 }
 
 // Pass 3: write block bytes, chunk-start bitmap and chunk-start -> input position map.
-__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict__ x, uint64_t n,
+#ifndef BZG_EMIT_WAVES
+#define BZG_EMIT_WAVES 0  // 6 or 8: VGPR spills, measured slower (+0.3 / +0.7 ms)
+#endif
+#if BZG_EMIT_WAVES > 0
+#define BZG_EMIT_BOUNDS __launch_bounds__(kT, BZG_EMIT_WAVES)
+#else
+#define BZG_EMIT_BOUNDS __launch_bounds__(kT)
+#endif
+__global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict__ x, uint64_t n,
                                              const uint32_t* __restrict__ carry,
                                              const uint32_t* __restrict__ out_base,
                                              uint8_t* __restrict__ out, uint32_t* __restrict__ cbits,
