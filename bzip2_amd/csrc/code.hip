@@ -147,10 +147,10 @@ __device__ __forceinline__ int n_groups(uint32_t nmtf) {  // compress.c:266-270
 #endif
 constexpr uint32_t kCfSlices = BZG_CF_SLICES;  // workgroups per block in k_cf
 
-__global__ void k_init_tables(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ freq_g,
+__global__ void k_init_tables(uint32_t b0, const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ freq_g,
                               const uint32_t* __restrict__ ninuse, uint8_t* __restrict__ lens_g,
                               uint32_t* __restrict__ rf_g) {
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = b0 + blockIdx.x;
   uint8_t* L = lens_g + (size_t)b * kNGroups * kMaxAlpha;
   for (int i = threadIdx.x; i < kNGroups * kMaxAlpha; i += blockDim.x) {
     L[i] = 0;
@@ -187,12 +187,12 @@ struct CfLds {
 
 // final == 0: select tables and count frequencies (into rf_g); final == 1: payload bits of
 // every group under its (already chosen) table into gbits_g, their sum into info_g[b*8+6].
-__global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, const uint32_t* __restrict__ mtf_off,
+__global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restrict__ mtfv, const uint32_t* __restrict__ mtf_off,
                                            const uint32_t* __restrict__ nmtf_g, const uint8_t* __restrict__ lens_g,
                                            uint8_t* __restrict__ sel_g, uint32_t* __restrict__ rf_g,
                                            uint16_t* __restrict__ gbits_g, uint32_t* __restrict__ info_g, int final) {
   __shared__ CfLds S;
-  const uint32_t b = blockIdx.y;
+  const uint32_t b = b0 + blockIdx.y;
   const uint32_t nmtf = nmtf_g[b];
   const uint32_t nsel = ceil_div(nmtf, kGroupSize);
   const uint32_t nch = ceil_div(nsel, kT);
@@ -294,14 +294,14 @@ __global__ void __launch_bounds__(kT) k_cf(const uint16_t* __restrict__ mtfv, co
 }
 
 // BZ2_hbMakeCodeLengths for table t of block b (one wave; the heap work is sequential).
-__global__ void __launch_bounds__(64) k_huff(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
+__global__ void __launch_bounds__(64) k_huff(uint32_t b0, const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
                                              uint32_t* __restrict__ rf_g, uint8_t* __restrict__ lens_g) {
   __shared__ alignas(16) uint64_t heap[kHeapCap];
   __shared__ int32_t weight[kMaxAlpha + 2];
   __shared__ int32_t parent[kMaxAlpha * 2];
   __shared__ uint32_t fq[kMaxAlpha];
   __shared__ uint8_t len[kMaxAlpha + 2];
-  const uint32_t b = blockIdx.x / kNGroups, t = blockIdx.x % kNGroups;
+  const uint32_t b = b0 + blockIdx.x / kNGroups, t = blockIdx.x % kNGroups;
   const int ng = n_groups(nmtf_g[b]);
   if ((int)t >= ng) return;
   const int alpha = (int)ninuse[b] + 2;
@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(64) k_code_lengths_test(const uint32_t* __rest
 
 // Canonical codes (huffman.c:152-166), selector MTF (compress.c:573-631), table bits
 // (compress.c:694-706) and the block's total bit count.  info_g[b*8+6] holds the payload bits.
-__global__ void __launch_bounds__(kT) k_final(const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
+__global__ void __launch_bounds__(kT) k_final(uint32_t b0, const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
                                               const uint32_t* __restrict__ inuse, const uint8_t* __restrict__ lens_g,
                                               uint32_t* __restrict__ codes_g, const uint8_t* __restrict__ sel_g,
                                               uint8_t* __restrict__ selmtf_g, uint32_t* __restrict__ info_g) {
@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(kT) k_final(const uint32_t* __restrict__ nmtf_
   __shared__ uint8_t sel[kMaxSelectors + 4];
   __shared__ uint32_t sh[8];
   __shared__ uint32_t misc[16];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = b0 + blockIdx.x;
   const uint32_t nmtf = nmtf_g[b];
   const int alpha = (int)ninuse[b] + 2;
   const int ng = n_groups(nmtf);
@@ -717,7 +717,8 @@ __global__ void k_frame(uint32_t* __restrict__ out, int header, uint64_t hdr_bit
 
 }  // namespace
 
-void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_t nb, CodeTables& t, hipStream_t st) {
+void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_t nb, CodeTables& t, hipStream_t st,
+                 hipStream_t st2) {
   const size_t nbx = std::max<uint32_t>(nb, 1);
   t.lens = ws.u8("code_lens", nbx * kNGroups * kMaxAlpha);
   t.codes = ws.u32("code_codes", nbx * kNGroups * kMaxAlpha);
@@ -729,18 +730,40 @@ void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_
   uint32_t* rf = ws.u32("code_rf", nbx * kNGroups * kMaxAlpha);
   if (nb == 0) return;
   HIP_OK(hipMemsetAsync(t.info, 0, nbx * 8 * 4, st));
-  k_init_tables<<<nb, 64, 0, st>>>(m.nmtf, m.freq, r.ninuse, t.lens, rf);
-  HIP_OK(hipGetLastError());
-  for (int it = 0; it < kIters; it++) {
-    k_cf<<<dim3(kCfSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 0);
+  // Blocks are independent, and k_huff is a latency chain with a small grid that leaves the
+  // device mostly idle: with a second stream the blocks run as two halves whose k_cf and
+  // k_huff launches interleave (one half's selection beside the other half's Huffman).
+  const bool split = st2 != nullptr && nb >= 64;
+  hipEvent_t e_in = nullptr, e_out = nullptr;
+  if (split) {
+    HIP_OK(hipEventCreateWithFlags(&e_in, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&e_out, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(e_in, st));
+    HIP_OK(hipStreamWaitEvent(st2, e_in, 0));
+  }
+  const uint32_t half = split ? nb / 2 : nb;
+  for (int h = 0; h < (split ? 2 : 1); h++) {
+    const uint32_t b0 = h ? half : 0, n = h ? nb - half : half;
+    hipStream_t s = h ? st2 : st;
+    k_init_tables<<<n, 64, 0, s>>>(b0, m.nmtf, m.freq, r.ninuse, t.lens, rf);
     HIP_OK(hipGetLastError());
-    k_huff<<<nb * kNGroups, 64, 0, st>>>(m.nmtf, r.ninuse, rf, t.lens);
+    for (int it = 0; it < kIters; it++) {
+      k_cf<<<dim3(kCfSlices, n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 0);
+      HIP_OK(hipGetLastError());
+      k_huff<<<n * kNGroups, 64, 0, s>>>(b0, m.nmtf, r.ninuse, rf, t.lens);
+      HIP_OK(hipGetLastError());
+    }
+    k_cf<<<dim3(kCfSlices, n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 1);
+    HIP_OK(hipGetLastError());
+    k_final<<<n, kT, 0, s>>>(b0, m.nmtf, r.ninuse, r.inuse, t.lens, t.codes, t.sel, t.selmtf, t.info);
     HIP_OK(hipGetLastError());
   }
-  k_cf<<<dim3(kCfSlices, nb), kT, 0, st>>>(m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 1);
-  HIP_OK(hipGetLastError());
-  k_final<<<nb, kT, 0, st>>>(m.nmtf, r.ninuse, r.inuse, t.lens, t.codes, t.sel, t.selmtf, t.info);
-  HIP_OK(hipGetLastError());
+  if (split) {
+    HIP_OK(hipEventRecord(e_out, st2));
+    HIP_OK(hipStreamWaitEvent(st, e_out, 0));
+    HIP_OK(hipEventDestroy(e_in));
+    HIP_OK(hipEventDestroy(e_out));
+  }
 }
 
 uint64_t code_emit(Workspace& ws, const std::vector<CodePart>& parts, int level, bool final_batch, StreamCarry& carry,

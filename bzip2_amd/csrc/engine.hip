@@ -178,6 +178,10 @@ struct Engine {
 
   // Parts per batch and concurrent sort streams (BZG_PARTS / BZG_SORT_STREAMS).  Batches of
   // fewer than 64 blocks are one part on one stream.
+  static bool split_tables() {  // BZG_SPLIT_TABLES=0: one stream for the table optimisation
+    static const bool v = cfg("BZG_SPLIT_TABLES", 1, 0, 1) != 0;
+    return v;
+  }
   static int cfg(const char* name, int dflt, int lo, int hi) {
     const char* e = getenv(name);
     return std::min(hi, std::max(lo, e ? atoi(e) : dflt));
@@ -316,7 +320,7 @@ struct Engine {
           P.w = &ws;
           mtf_stage(ws, r, bwt, nb, hboff[nb], P.m, s, &hboff);
           HIP_OK(hipEventRecord(e1, s));
-          code_tables(ws, r, P.m, nb, P.t, s);
+          code_tables(ws, r, P.m, nb, P.t, s, split_tables() ? sstream[0] : nullptr);
           HIP_OK(hipEventRecord(e2, s));
           HIP_OK(hipEventSynchronize(e2));
           (void)hipEventElapsedTime(&mtf_ms, e0, e1);

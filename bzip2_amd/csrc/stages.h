@@ -144,7 +144,8 @@ struct CodeTables {
   uint32_t* info = nullptr;
   uint64_t* bbits = nullptr;
 };
-void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_t nb, CodeTables& t, hipStream_t st);
+void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_t nb, CodeTables& t, hipStream_t st,
+                 hipStream_t st2 = nullptr);
 // One part of a batch (consecutive blocks, in stream order) ready to be packed.
 struct CodePart {
   const Rle1Result* r;
