@@ -687,9 +687,27 @@ __global__ void __launch_bounds__(kT) k_period(const uint8_t* __restrict__ blk, 
     if (p >= n) break;
     if (threadIdx.x == 0) bad = 0;
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < n - p; i0 += kT * 16) {
-      for (uint32_t i = i0 + threadIdx.x; i < n - p && i < i0 + kT * 16; i += kT)
-        if (blk[lo + i] != blk[lo + i + p]) bad = 1;
+    // 16 bytes per thread and step (unaligned loads; the block buffer is padded), 64 KB per
+    // step: the period that holds reads the whole block (single-byte runs: 900 kB)
+    for (uint32_t i0 = 0; i0 < n - p; i0 += kT * 16 * 16) {
+      bool diff = false;
+#pragma unroll 4
+      for (uint32_t k = 0; k < 16; k++) {
+        const uint32_t i = i0 + (k * kT + threadIdx.x) * 16;
+        if (i >= n - p) break;
+        uint4 x, y;
+        __builtin_memcpy(&x, blk + lo + i, 16);
+        __builtin_memcpy(&y, blk + lo + i + p, 16);
+        const uint32_t m = n - p - i;  // bytes of this piece that count
+        if (m >= 16) {
+          diff |= (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
+        } else {
+          const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+          for (uint32_t c = 0; c < m; c++)
+            diff |= ((xs[c >> 2] ^ ys[c >> 2]) >> (8 * (c & 3))) & 0xffu;
+        }
+      }
+      if (diff) bad = 1;
       __syncthreads();
       const bool stop = bad;
       __syncthreads();  // every thread has read the flag before the next chunk may set it
