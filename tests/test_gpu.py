@@ -246,6 +246,50 @@ def test_bwt_long_repeats_fallback():
         assert orig[b] == o, b
 
 
+def _deep_pair_blocks():
+    """Blocks whose deep tied groups are mostly pairs, for the S3 pair resolver (sort.hip
+    k_pair_end / k_pair_long / k_pair_resolve): twice-copied passages (run ends compare a few
+    characters), pairs whose run ends inside a three-copy group (a run-end scan past
+    kPairShort, the k_pair_long path), self-overlapping copies (a pair's partner run crosses its
+    own run), and copies that wrap round the block end (cyclic comparison)."""
+    rng = random.Random(23)
+
+    def rnd(k):
+        return bytes(rng.randrange(256) for _ in range(k))
+
+    out = []
+    p = rnd(5000)  # twice-copied passage, random continuations
+    out.append(rnd(3000) + p + rnd(2000) + p + rnd(4000))
+    s = rnd(6000)  # "x"+S twice, "y"+S once: the x-pairs share 6001 chars, their successors are triples
+    out.append(rnd(1000) + b"x" + s + rnd(500) + b"x" + s + rnd(700) + b"y" + s + rnd(900))
+    u = rnd(6000)  # u u u[:3000]: pairs (i, i+6000) overlap themselves
+    out.append(rnd(800) + u + u + u[:3000] + b"\x00" + rnd(1200))
+    w = rnd(4000)  # one copy at the end, one at the start: comparisons wrap round
+    out.append(w[2000:] + rnd(3000) + w + rnd(1500) + w[:2000])
+    t = datagen.text(30_000, 77)  # text passage twice inside text
+    out.append(datagen.text(50_000, 78) + t + datagen.text(20_000, 79) + t + datagen.text(10_000, 80))
+    offs = [0]
+    for p_ in out:
+        offs.append(offs[-1] + len(p_))
+    return b"".join(out), offs
+
+
+def test_bwt_deep_pairs():
+    blocks, offs = _deep_pair_blocks()
+    bwt, orig = gpu_bwt(blocks, offs)
+    for b in range(len(offs) - 1):
+        blk = blocks[offs[b]:offs[b + 1]]
+        L, o, per = O.orc_bwt(blk)
+        assert per == len(blk), b
+        assert bwt[offs[b]:offs[b + 1]] == L, b
+        assert orig[b] == o, b
+
+
+def test_deep_pairs_stream():
+    blocks, _ = _deep_pair_blocks()
+    assert B.buff_to_buff_compress(blocks, 9) == expected(blocks, 9)
+
+
 def test_many_deep_groups_repeats():
     """Enwik-like long repeats at scale: 400 MB of text with a quarter overwritten by copies of
     earlier passages (2-200 kB) gives tens of millions of groups still tied after the string
