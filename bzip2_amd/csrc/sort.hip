@@ -393,7 +393,9 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   const uint32_t gbase = off[(size_t)t * 256 + d];
 #pragma unroll
   for (int q = 0; q < 4; q++) cnt[q * kT + d] = 0;
-  const uint32_t myflag = (total == 1 ? 1u : 0u) | ((bucket_cls(total, grp_depth(gr) + 1) & ~1u) == 6u ? 2u : 0u);
+  // (a cache that this pass empties is not stored: the next pass refills it from the text)
+  const uint32_t myflag = (total == 1 ? 1u : 0u) |
+                          ((bucket_cls(total, grp_depth(gr) + 1) & ~1u) == 6u && tiled_next_cache(gr) ? 2u : 0u);
   uint32_t vv[kPerT], kk[kPerT];
   s1_load<false>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
@@ -686,8 +688,10 @@ __global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __re
       Lv[x] = v;
       const uint32_t slot = S.gstart[j] + x - S.goff[j];
       const bool dst_alt = !(fl & kGrpIdent) && !(fl & kGrpAlt);
-      // key caches only for buckets that stay in S1 (S2 and S3 read the text)
-      if (bucket_cls(total, grp_depth(Grp{0, 0, 0, fl}) + 1) == 6u) (dst_alt ? B.sk2 : B.sk)[slot] = kk[i] << 8;
+      // key caches only for buckets that stay in S1 (S2 and S3 read the text), and only when
+      // this pass leaves a byte in them
+      if (bucket_cls(total, grp_depth(Grp{0, 0, 0, fl}) + 1) == 6u && s1_next_cache(Grp{0, 0, 0, fl}))
+        (dst_alt ? B.sk2 : B.sk)[slot] = kk[i] << 8;
       if (total == 1) {
         if (dst_alt) B.sa[slot] = v;
         const uint32_t r = slot - S.gsb[j];
