@@ -497,9 +497,21 @@ struct BitWriter {
 #endif
 constexpr uint32_t kPackSlices = BZG_PACK_SLICES;  // workgroups per block in k_pack
 
+// The step's bit buffer holds either the whole step (default) or a window of it: a smaller
+// buffer lets more workgroups share a CU, and a step with more bits (high-entropy input) is
+// encoded in several windows, each taking the groups that start inside it.
+constexpr uint32_t kPackFull = (kT * kGroupSize * kMaxCodeLen + 31) / 32 + 2;
+#ifndef BZG_PACK_BITSW
+#define BZG_PACK_BITSW 3328  // 13 KB: 3 workgroups per CU (the whole step, kPackFull words, gives 2)
+#endif
+constexpr uint32_t kPackBitsW = BZG_PACK_BITSW;             // words of the bit buffer
+constexpr uint32_t kPackOv = (kGroupSize * kMaxCodeLen + 31) / 32 + 1;  // words a group can reach past its window
+static_assert(kPackBitsW >= kPackFull || kPackBitsW >= 4 * kPackOv, "bit window too small");
+constexpr uint32_t kPackWS = kPackBitsW >= kPackFull ? kPackBitsW * 32 : (kPackBitsW - kPackOv) * 32;  // bits per window
+
 struct PackLds {
   alignas(16) uint16_t chunk[kT * kGroupSize + 8];
-  uint32_t bits[(kT * kGroupSize * kMaxCodeLen + 31) / 32 + 2];  // one step's payload
+  uint32_t bits[kPackBitsW];  // one window of the step's payload
 };
 
 __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, const uint32_t* __restrict__ mtf_off,
@@ -652,41 +664,51 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
       const uint32_t gx = block_incl_sum(mybits, sh, &stepbits) - mybits;
       const uint32_t w0 = (uint32_t)(pos & 31);          // bit offset of the step in its first word
       const uint32_t nwords = (w0 + stepbits + 31) >> 5;  // words the step touches
-      for (uint32_t i = threadIdx.x; i < nwords; i += kT) P.bits[i] = 0;
-      __syncthreads();
-      if (g < nsel) {
-        const int t = selo[g];
-        const uint16_t* c = P.chunk + threadIdx.x * kGroupSize;
-        const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
-        uint32_t bp = w0 + gx;                    // bit position in P.bits
-        uint64_t acc = 0;                         // left-aligned pending bits
-        uint32_t na = bp & 31;                    // bits in acc, counted from the word start
-        uint32_t wi = bp >> 5;
-        for (uint32_t i = 0; i < n; i++) {
-          const uint32_t cl = code[t][c[i]];
-          const uint32_t l = cl >> 24;
-          acc |= ((uint64_t)(cl & 0xffffffu) << (64 - l)) >> na;
-          na += l;
-          if (na >= 32) {
-            atomicOr(&P.bits[wi++], (uint32_t)(acc >> 32));
-            acc <<= 32;
-            na -= 32;
+      const uint32_t nwin = (w0 + stepbits + kPackWS - 1) / kPackWS;
+      const uint32_t mywin = (w0 + gx) / kPackWS;
+      uint32_t* ow = out + (pos >> 5);
+      for (uint32_t r = 0; r < nwin; r++) {
+        const uint32_t wbw = r * (kPackWS / 32);  // first word of the window
+        const uint32_t nw = min(kPackBitsW, nwords - wbw);
+        for (uint32_t i = threadIdx.x; i < nw; i += kT) P.bits[i] = 0;
+        __syncthreads();
+        if (g < nsel && mywin == r) {
+          const int t = selo[g];
+          const uint16_t* c = P.chunk + threadIdx.x * kGroupSize;
+          const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
+          uint32_t bp = w0 + gx - wbw * 32;         // bit position in P.bits
+          uint64_t acc = 0;                         // left-aligned pending bits
+          uint32_t na = bp & 31;                    // bits in acc, counted from the word start
+          uint32_t wi = bp >> 5;
+          for (uint32_t i = 0; i < n; i++) {
+            const uint32_t cl = code[t][c[i]];
+            const uint32_t l = cl >> 24;
+            acc |= ((uint64_t)(cl & 0xffffffu) << (64 - l)) >> na;
+            na += l;
+            if (na >= 32) {
+              atomicOr(&P.bits[wi++], (uint32_t)(acc >> 32));
+              acc <<= 32;
+              na -= 32;
+            }
+          }
+          if (na) atomicOr(&P.bits[wi], (uint32_t)(acc >> 32));
+        }
+        __syncthreads();
+        // words shared with the neighbouring steps, or with the previous / next window, are ORed
+        for (uint32_t i = threadIdx.x; i < nw; i += kT) {
+          const uint32_t v = bswap32(P.bits[i]);
+          const uint32_t gi = wbw + i;
+          const bool shared = gi == 0 || gi + 1 == nwords || (r > 0 && i < kPackOv) ||
+                              (r + 1 < nwin && i >= kPackWS / 32);
+          if (shared) {
+            if (v) atomicOr(&ow[gi], v);
+          } else {
+            ow[gi] = v;
           }
         }
-        if (na) atomicOr(&P.bits[wi], (uint32_t)(acc >> 32));
-      }
-      __syncthreads();
-      uint32_t* ow = out + (pos >> 5);
-      for (uint32_t i = threadIdx.x; i < nwords; i += kT) {
-        const uint32_t v = bswap32(P.bits[i]);
-        if (i == 0 || i + 1 == nwords) {
-          if (v) atomicOr(&ow[i], v);
-        } else {
-          ow[i] = v;
-        }
+        __syncthreads();
       }
       pos += stepbits;
-      __syncthreads();
     }
   }
 }

@@ -294,27 +294,43 @@ __device__ __forceinline__ uint32_t s1_next_cache(const Grp& gr) {
 // the same for the buckets of a tiled pass
 __device__ __forceinline__ uint32_t tiled_next_cache(const Grp& gr) { return kTCache ? s1_next_cache(gr) : 0u; }
 
+#ifndef BZG_HIST_CP
+#define BZG_HIST_CP 4
+#endif
+#ifndef BZG_OFF_UNROLL
+#define BZG_OFF_UNROLL 1
+#endif
+#define BZG_STR_(x) #x
+#define BZG_UNROLL(n) _Pragma(BZG_STR_(unroll n))
+constexpr uint32_t kHistCp = BZG_HIST_CP;
+static_assert(kHistCp == 4 || kHistCp == 8, "histogram copies");
+
 __global__ void __launch_bounds__(kT) k_s1_hist(const TileRec* __restrict__ TR, SortBufs B, uint32_t* __restrict__ hist) {
-  // 4 copies of every bin in consecutive words (lane & 3 picks one): lanes of a wave that
-  // count the same character (skewed text) hit 4 banks instead of queueing on one word
-  __shared__ uint32_t h[256 * 4];
+  // kHistCp copies of every bin in consecutive words (lane % kHistCp picks one): lanes of a
+  // wave that count the same character (skewed text) hit several banks instead of one word
+  __shared__ uint32_t h[256 * kHistCp];
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
   const TileRec tr = TR[t];
   const Grp gr = tr.g;
   const Unit U = tr.u;
   const uint32_t lo = tr.k * kDTile, hi = min(gr.size, lo + kDTile);
 #pragma unroll
-  for (int q = 0; q < 4; q++) h[q * kT + threadIdx.x] = 0;
+  for (int q = 0; q < (int)kHistCp; q++) h[q * kT + threadIdx.x] = 0;
   uint32_t vv[kPerT], kk[kPerT];
   s1_load<true>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
-  const uint32_t cp = threadIdx.x & 3u;
+  const uint32_t cp = threadIdx.x % kHistCp;
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
-    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[(kk[i] >> 24) * 4 + cp], 1u);
+    if (lo + i * kT + threadIdx.x < hi) atomicAdd(&h[(kk[i] >> 24) * kHistCp + cp], 1u);
   __syncthreads();
-  const uint4 c4 = reinterpret_cast<const uint4*>(h)[threadIdx.x];
-  hist[(size_t)t * 256 + threadIdx.x] = c4.x + c4.y + c4.z + c4.w;
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < (int)kHistCp; q += 4) {
+    const uint4 c4 = reinterpret_cast<const uint4*>(h)[threadIdx.x * (kHistCp / 4) + q / 4];
+    c += c4.x + c4.y + c4.z + c4.w;
+  }
+  hist[(size_t)t * 256 + threadIdx.x] = c;
 }
 
 __device__ __forceinline__ uint32_t bucket_cls(uint32_t total, uint32_t depth) {
@@ -337,11 +353,13 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
   const uint32_t d = threadIdx.x;
   if (d <= (uint32_t)kNCls) cc[d] = 0;
   uint32_t total = 0;
+  BZG_UNROLL(BZG_OFF_UNROLL)
   for (uint32_t t = t0; t < t1; t++) total += hist[(size_t)t * 256 + d];
   const uint32_t incl = block_incl_sum(total, sh, (uint32_t*)nullptr);
   const uint32_t base = gr.start + incl - total;
   tot[(size_t)g * 256 + d] = total;
   uint32_t run = base;
+  BZG_UNROLL(BZG_OFF_UNROLL)
   for (uint32_t t = t0; t < t1; t++) {
     const uint32_t c = hist[(size_t)t * 256 + d];
     hist[(size_t)t * 256 + d] = run;
