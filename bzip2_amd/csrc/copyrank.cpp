@@ -1,5 +1,37 @@
 // copyrank.cpp -- A5: origPtr of an exactly periodic block.
 //
+// DERIVED WORK NOTICE.  Sections 3a/3b below model, on class labels, the exchange sequence of
+// divsufsort as modified in the reference's blocksort.c: the B* substring sort (ss_pivot /
+// ss_median3 / ss_median5 blocksort.c:211-262, ss_fixdown / ss_heapsort 168-209,
+// ss_multikey_introsort 300-424, ss_merge_forward / ss_merge_backward / ss_merge 436-622,
+// substringsort 625-664) and the rank refinement (tr_partition / tr_copy / tr_introsort
+// 964-1122, lssort / ls_introsort 833-959, trsort 1285-1309).  For q > 1 periodic roots the
+// tie order IS those exchanges, so this model mirrors their structure; it is a derived
+// component of divsufsort, used under its licence:
+//
+//   divsufsort
+//   Copyright (c) 2003-2007 Yuta Mori All Rights Reserved.
+//
+//   Permission is hereby granted, free of charge, to any person obtaining a copy of this
+//   software and associated documentation files (the "Software"), to deal in the Software
+//   without restriction, including without limitation the rights to use, copy, modify,
+//   merge, publish, distribute, sublicense, and/or sell copies of the Software, and to
+//   permit persons to whom the Software is furnished to do so, subject to the following
+//   conditions:
+//
+//   The above copyright notice and this permission notice shall be included in all copies
+//   or substantial portions of the Software.
+//
+//   THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND, EXPRESS OR IMPLIED,
+//   INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY, FITNESS FOR A
+//   PARTICULAR PURPOSE AND NONINFRINGEMENT. IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT
+//   HOLDERS BE LIABLE FOR ANY CLAIM, DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF
+//   CONTRACT, TORT OR OTHERWISE, ARISING FROM, OUT OF OR IN CONNECTION WITH THE SOFTWARE
+//   OR THE USE OR OTHER DEALINGS IN THE SOFTWARE.
+//
+// The q = 1 closed form (section 4, evaluated on the device in origptr.hip) and the
+// quasi-periodic ordering (qsa.cpp) are not derived from divsufsort code.
+//
 // A block T = w^k (w primitive, |w| = p >= 2, k >= 2) has k identical copies of each of its p
 // distinct rotations.  The last column does not depend on how the copies are ordered, but
 // origPtr does: the reference reports the slot of rotation 0, which sits somewhere inside the

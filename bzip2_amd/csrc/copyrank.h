@@ -1,6 +1,8 @@
 // copyrank.h -- A5: which of the k identical copies of rotation 0 the reference ranks first
-// in a block w^k.  See copyrank.cpp for the
-// derivation; the one-B*-per-period closed form also runs on the device (origptr.hip).
+// in a block w^k.  copy_rank is derived from
+// divsufsort as modified in the reference's blocksort.c (MIT notice and citations at the top
+// of copyrank.cpp); the one-B*-per-period closed form is original and also runs on the device
+// (origptr.hip).
 #pragma once
 #include <cstdint>
 
