@@ -5,6 +5,9 @@ itself is not available offline), resident in HBM before the timed region; one s
 complete .bz2 stream (RLE1 -> BWT -> MTF -> Huffman -> packing, bit-exact with the reference)
 written to HBM.  N GPUs = N ranks, each compressing its own 1e9-byte stream (independent
 objects, no data-path collective): scaling "weak", value = total bytes / max-over-ranks time.
+`--gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N ranks itself (a child
+`torch.distributed.run` on 127.0.0.1, started before this process touches the GPU); under an
+outside launcher the world size must equal `--gpus`.
 
 Also reported on rank 0: the reference CPU path timed on a bounded sample of the same text
 (oracle/_ref = the reference's own blocksort.c/compress.c build, 1 thread), a bit-exactness
@@ -72,9 +75,50 @@ def rank_seed(rank: int) -> int:
     return 0x5EED0001 + rank
 
 
+def launch_cmd(argv, n: int, port: int) -> list:
+    """The child command that runs this bench as n ranks of one node (one process per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv) -> int:
+    """`--gpus N` (N > 1) without an outside launcher: run N ranks as a child process group and
+    return its exit code.  Nothing in this process has touched the GPU yet (no exec either)."""
+    import subprocess
+
+    if os.environ.get("BZG_DIST_BACKEND") != "gloo":
+        have = torch.cuda.device_count()  # does not initialise the GPU on this image
+        if have < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but {have} GPU(s) visible (BZG_DIST_BACKEND=gloo rehearses "
+                  f"several ranks on one GPU)", file=sys.stderr)
+            return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(launch_cmd(argv, a.gpus, free_port()), env=env).returncode
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench.py: world size {world} != --gpus {a.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if os.environ.get("BZG_BENCH_PROBE") == "1":  # launcher test (CPU): report the rank layout only
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world,
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1

@@ -49,3 +49,35 @@ def test_ranks_get_distinct_objects():
     a = datagen.text(100_000, bench.rank_seed(0))
     b = datagen.text(100_000, bench.rank_seed(1))
     assert len(a) == len(b) == 100_000 and a != b
+
+
+def _run_bench(args, env_extra):
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=240)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    return r.returncode, lines, r.stderr
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` with no outside launcher starts 2 ranks (torch.distributed.run on
+    127.0.0.1); the probe mode stops each rank before any GPU call."""
+    rc, lines, err = _run_bench(["--gpus", "2"], {"BZG_BENCH_PROBE": "1", "BZG_DIST_BACKEND": "gloo"})
+    assert rc == 0, err[-2000:]
+    assert sorted(x["rank"] for x in lines) == [0, 1]
+    assert all(x["world"] == 2 and x["master"] == "127.0.0.1" for x in lines)
+    assert sorted(x["local_rank"] for x in lines) == [0, 1]
+
+
+def test_bench_world_size_must_match_gpus():
+    rc, lines, err = _run_bench(["--gpus", "2"], {"BZG_BENCH_PROBE": "1", "WORLD_SIZE": "3", "RANK": "0"})
+    assert rc == 2 and not lines and "!= --gpus 2" in err
+    rc, lines, _ = _run_bench(["--gpus", "1"], {"BZG_BENCH_PROBE": "1"})
+    assert rc == 0 and lines == [{"rank": 0, "world": 1, "local_rank": 0, "master": None}]
