@@ -120,7 +120,7 @@ def lib() -> ctypes.CDLL:
         L.bzg_bound.restype = u64
         L.bzg_stage_rle1.argtypes = [vp, u64, ci, ci, vp, u64, vp, vp, ctypes.POINTER(u32), u32]
         L.bzg_stage_bwt.argtypes = [vp, vp, u32, vp, vp]
-        L.bzg_stage_mtf.argtypes = [vp, vp, u32, vp, vp, vp, vp]
+        L.bzg_stage_mtf.argtypes = [vp, vp, u32, vp, ctypes.c_uint64, vp, vp, vp]
         L.bzg_stage_code_lengths.argtypes = [vp, vp, u32, ci, vp]
         L.bzg_last_stats.argtypes = [ctypes.POINTER(bzg_stats)]
         L.bzg_periodic_origptr.argtypes = [vp, ctypes.c_int32]

@@ -27,7 +27,19 @@
 namespace bzg {
 
 // ---------------------------------------------------------------- workspace
-Workspace::~Workspace() { release_all(); }
+Workspace::~Workspace() {
+  release_all();
+  if (handoff_) (void)hipEventDestroy(handoff_);
+}
+
+void Workspace::set_stream(hipStream_t s) {
+  if (s == stream_) return;
+  // no throw: Lease's destructor hands the workspaces back to the engine's own stream
+  if (!bufs_.empty() && (handoff_ || hipEventCreateWithFlags(&handoff_, hipEventDisableTiming) == hipSuccess)) {
+    if (hipEventRecord(handoff_, stream_) == hipSuccess) (void)hipStreamWaitEvent(s, handoff_, 0);
+  }
+  stream_ = s;
+}
 
 void Workspace::drop(Buf& b) {
   if (!b.p) return;
@@ -178,10 +190,6 @@ struct Engine {
 
   // Parts per batch and concurrent sort streams (BZG_PARTS / BZG_SORT_STREAMS).  Batches of
   // fewer than 64 blocks are one part on one stream.
-  static bool post_parts() {  // BZG_POST_PARTS=1: MTF and tables per part, one stream each (measured +0.4 ms)
-    static const bool v = cfg("BZG_POST_PARTS", 0, 0, 1) != 0;
-    return v;
-  }
   static bool split_tables() {  // BZG_SPLIT_TABLES=0: one stream for the table optimisation
     static const bool v = cfg("BZG_SPLIT_TABLES", 1, 0, 1) != 0;
     return v;
@@ -195,9 +203,8 @@ struct Engine {
   //
   // The blocks are cut into parts.  Each part is sorted on one of the sort streams by its own
   // host thread (the sorter synchronises with the host between passes, so several parts keep
-  // the device busy); as soon as a part's sort is done the calling thread queues its origPtr,
-  // MTF and table optimisation on the main stream, where they overlap the sorts of the later
-  // parts.  The bit offsets and the packing of all parts follow in block order.
+  // the device busy); once every part is sorted, origPtr, MTF and the table optimisation run
+  // over the whole batch on the main stream, then the bit offsets and the packing.
   void batch(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
              uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
     const int level = st->level;
@@ -288,100 +295,48 @@ struct Engine {
           }
         }
       };
-      std::vector<std::thread> th;
-      std::exception_ptr err;
-      if (S > 1)
-        for (int t = 0; t < S; t++) th.emplace_back(sorter, t);
-      else
-        sorter(0);
-      hipEvent_t e0, e1, e2;
+      // the timing events exist before any sorter thread starts, so every exit path below
+      // joins the threads
+      hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
       HIP_OK(hipEventCreate(&e0));
       HIP_OK(hipEventCreate(&e1));
       HIP_OK(hipEventCreate(&e2));
-      static const bool overlap = getenv("BZG_OVERLAP") && atoi(getenv("BZG_OVERLAP")) != 0;
+      std::vector<std::thread> th;
+      std::exception_ptr err;
       try {
-        if (!overlap) {
-          // measured (profiles/r03_pipeline_sweep.txt): MTF and tables beside the later
-          // sorts slow both more than they overlap; the default runs them once over the
-          // whole batch after every part is sorted
-          for (uint32_t p = 0; p < K; p++) {
-            sorted_f[p].get();
-            HIP_OK(hipStreamWaitEvent(s, psorted[p], 0));
-          }
-          for (auto& x : th) x.join();
-          th.clear();
-          HIP_OK(hipEventRecord(e0, s));
-          for (uint32_t p = 0; p < K; p++) {
-            parts[p].w->set_stream(s);
-            copyrank_finish(*parts[p].w, parts[p].r, rank0 + parts[p].b0, origptr + parts[p].b0, parts[p].a5, s);
-          }
-          if (post_parts() && K >= 2) {
-            // every part's MTF and tables on a stream of its own, all after the sorts: the
-            // latency-bound kernels of one part (k_compose, k_huff) run beside the others'
-            std::vector<hipEvent_t> em(K), et(K);
-            hipEvent_t eg;
-            HIP_OK(hipEventCreateWithFlags(&eg, hipEventDisableTiming));
-            HIP_OK(hipEventRecord(eg, s));
-            for (uint32_t p = 0; p < K; p++) {
-              Part& P = parts[p];
-              hipStream_t ps = p == 0 ? s : sstream[(p - 1) % kSortStreams];
-              HIP_OK(hipEventCreateWithFlags(&em[p], hipEventDisableTiming));
-              HIP_OK(hipEventCreateWithFlags(&et[p], hipEventDisableTiming));
-              if (ps != s) HIP_OK(hipStreamWaitEvent(ps, eg, 0));
-              P.w->set_stream(ps);
-              mtf_stage(*P.w, P.r, bwt + hboff[P.b0], P.r.nblocks, P.hboff.back(), P.m, ps, &P.hboff);
-              HIP_OK(hipEventRecord(em[p], ps));
-              code_tables(*P.w, P.r, P.m, P.r.nblocks, P.t, ps);
-              HIP_OK(hipEventRecord(et[p], ps));
-            }
-            for (uint32_t p = 0; p < K; p++) HIP_OK(hipStreamWaitEvent(s, em[p], 0));
-            HIP_OK(hipEventRecord(e1, s));
-            for (uint32_t p = 0; p < K; p++) HIP_OK(hipStreamWaitEvent(s, et[p], 0));
-            HIP_OK(hipEventRecord(e2, s));
-            HIP_OK(hipEventSynchronize(e2));
-            for (uint32_t p = 0; p < K; p++) {
-              parts[p].w->set_stream(s);
-              HIP_OK(hipEventDestroy(em[p]));
-              HIP_OK(hipEventDestroy(et[p]));
-            }
-            HIP_OK(hipEventDestroy(eg));
-          } else {
-            K = 1;  // one part over the whole batch from here on
-            Part& P = parts[0];
-            P.b0 = 0;
-            P.b1 = nb;
-            P.r = r;
-            P.hboff = hboff;
-            P.w = &ws;
-            mtf_stage(ws, r, bwt, nb, hboff[nb], P.m, s, &hboff);
-            HIP_OK(hipEventRecord(e1, s));
-            code_tables(ws, r, P.m, nb, P.t, s, split_tables() ? sstream[0] : nullptr);
-            HIP_OK(hipEventRecord(e2, s));
-            HIP_OK(hipEventSynchronize(e2));
-          }
-          (void)hipEventElapsedTime(&mtf_ms, e0, e1);
-          (void)hipEventElapsedTime(&tab_ms, e1, e2);
-          last_post = mtf_ms + tab_ms;
-        }
-        for (uint32_t p = 0; p < K && overlap; p++) {
-          Part& P = parts[p];
+        if (S > 1)
+          for (int t = 0; t < S; t++) th.emplace_back(sorter, t);
+        else
+          sorter(0);
+        // measured (profiles/r03_pipeline_sweep.txt): MTF and tables beside the later sorts
+        // slow both more than they overlap; they run once over the whole batch after every
+        // part is sorted
+        for (uint32_t p = 0; p < K; p++) {
           sorted_f[p].get();
-          P.w->set_stream(s);
           HIP_OK(hipStreamWaitEvent(s, psorted[p], 0));
-          HIP_OK(hipEventRecord(e0, s));
-          copyrank_finish(*P.w, P.r, rank0 + P.b0, origptr + P.b0, P.a5, s);  // origPtr on the device (A5)
-          mtf_stage(*P.w, P.r, bwt + hboff[P.b0], P.r.nblocks, P.hboff.back(), P.m, s, &P.hboff);
-          HIP_OK(hipEventRecord(e1, s));
-          code_tables(*P.w, P.r, P.m, P.r.nblocks, P.t, s);
-          HIP_OK(hipEventRecord(e2, s));
-          HIP_OK(hipEventSynchronize(e2));  // timing only: the next part's sort is waited for anyway
-          float a = 0, b = 0;
-          (void)hipEventElapsedTime(&a, e0, e1);
-          (void)hipEventElapsedTime(&b, e1, e2);
-          mtf_ms += a;
-          tab_ms += b;
-          last_post = a + b;
         }
+        for (auto& x : th) x.join();
+        th.clear();
+        HIP_OK(hipEventRecord(e0, s));
+        for (uint32_t p = 0; p < K; p++) {
+          parts[p].w->set_stream(s);
+          copyrank_finish(*parts[p].w, parts[p].r, rank0 + parts[p].b0, origptr + parts[p].b0, parts[p].a5, s);
+        }
+        K = 1;  // one part over the whole batch from here on
+        Part& P = parts[0];
+        P.b0 = 0;
+        P.b1 = nb;
+        P.r = r;
+        P.hboff = hboff;
+        P.w = &ws;
+        mtf_stage(ws, r, bwt, nb, hboff[nb], P.m, s, &hboff);
+        HIP_OK(hipEventRecord(e1, s));
+        code_tables(ws, r, P.m, nb, P.t, s, split_tables() ? sstream[0] : nullptr);
+        HIP_OK(hipEventRecord(e2, s));
+        HIP_OK(hipEventSynchronize(e2));
+        (void)hipEventElapsedTime(&mtf_ms, e0, e1);
+        (void)hipEventElapsedTime(&tab_ms, e1, e2);
+        last_post = mtf_ms + tab_ms;
       } catch (...) {
         err = std::current_exception();
       }
@@ -1244,6 +1199,7 @@ void bzg_last_stats(bzg_stats* out) {
 }
 
 void bzg_release(void) {
+  bzg::copyrank_memo_clear();
   if (pool().devices() <= 0) return;
   pool().release_idle_memory();
   SegState& S = seg_state();  // the chunk-map engines' workspaces too
@@ -1276,6 +1232,12 @@ int32_t bzg_periodic_origptr(const uint8_t* block, int32_t n) {
 }
 
 // ---------------------------------------------------------------- per-stage entry points
+// The stage hooks copy on the engine's stream, where its workspace buffers are allocated and
+// freed (hipMallocAsync / hipFreeAsync), and wait for the copy.
+static void stage_copy(Engine& e, void* dst, const void* src, size_t n, hipMemcpyKind kind) {
+  HIP_OK(hipMemcpyAsync(dst, src, n, kind, e.stream));
+  HIP_OK(hipStreamSynchronize(e.stream));
+}
 int bzg_stage_rle1(const void* src, uint64_t n, int level, int tail_merge, uint8_t* blocks, uint64_t blocks_cap,
                    uint32_t* offsets, uint32_t* crcs, uint32_t* nblocks, uint32_t max_blocks) {
   if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
@@ -1289,7 +1251,7 @@ int bzg_stage_rle1(const void* src, uint64_t n, int level, int tail_merge, uint8
   Engine& e = *lease->e;
   try {
     uint8_t* din = e.ws.u8("stage_in", n + 16);
-    HIP_OK(hipMemcpy(din, src, n, hipMemcpyHostToDevice));
+    stage_copy(e, din, src, n, hipMemcpyHostToDevice);
     Rle1Result r;
     rle1_stage(e.ws, din, n, level, true, tail_merge != 0, r, e.stream);
     HIP_OK(hipStreamSynchronize(e.stream));
@@ -1299,10 +1261,10 @@ int bzg_stage_rle1(const void* src, uint64_t n, int level, int tail_merge, uint8
       offsets[0] = 0;
       return BZ_OK;
     }
-    HIP_OK(hipMemcpy(offsets, r.boff, 4 * (r.nblocks + 1), hipMemcpyDeviceToHost));
+    stage_copy(e, offsets, r.boff, 4 * (r.nblocks + 1), hipMemcpyDeviceToHost);
     if (offsets[r.nblocks] > blocks_cap) return BZ_OUTBUFF_FULL;
-    HIP_OK(hipMemcpy(blocks, r.blk, offsets[r.nblocks], hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(crcs, r.bcrc, 4 * r.nblocks, hipMemcpyDeviceToHost));
+    stage_copy(e, blocks, r.blk, offsets[r.nblocks], hipMemcpyDeviceToHost);
+    stage_copy(e, crcs, r.bcrc, 4 * r.nblocks, hipMemcpyDeviceToHost);
     return BZ_OK;
   } catch (const HipFailure&) {
     return BZ_CONFIG_ERROR;
@@ -1326,8 +1288,8 @@ int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, u
     r.nblocks = nb;
     r.blk = e.ws.u8("blk", total + 64);
     r.boff = e.ws.u32("boff", nb + 2);
-    HIP_OK(hipMemcpy(r.blk, blocks, total, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice));
+    stage_copy(e, r.blk, blocks, total, hipMemcpyHostToDevice);
+    stage_copy(e, r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice);
     block_info_stage(e.ws, r, e.stream);
     std::vector<uint32_t> hboff(offsets, offsets + nb + 1), hper(nb), hbq(nb), hqp(nb);
     HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, e.stream));
@@ -1343,15 +1305,15 @@ int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, u
     copyrank_finish(e.ws, r, rank0, d_orig, a5, e.stream);
     HIP_OK(hipMemcpyAsync(origptr, d_orig, 4 * nb, hipMemcpyDeviceToHost, e.stream));
     HIP_OK(hipStreamSynchronize(e.stream));
-    HIP_OK(hipMemcpy(bwt_out, bwt, total, hipMemcpyDeviceToHost));
+    stage_copy(e, bwt_out, bwt, total, hipMemcpyDeviceToHost);
     return BZ_OK;
   } catch (const HipFailure&) {
     return BZ_CONFIG_ERROR;
   }
 }
 
-int bzg_stage_mtf(const uint8_t* bwt_in, const uint32_t* offsets, uint32_t nb, uint16_t* mtfv, uint32_t* mtf_offsets,
-                  uint32_t* nmtf, uint32_t* freq) {
+int bzg_stage_mtf(const uint8_t* bwt_in, const uint32_t* offsets, uint32_t nb, uint16_t* mtfv, uint64_t mtfv_cap,
+                  uint32_t* mtf_offsets, uint32_t* nmtf, uint32_t* freq) {
   if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
   Lease* lp = nullptr;
   try {
@@ -1368,16 +1330,17 @@ int bzg_stage_mtf(const uint8_t* bwt_in, const uint32_t* offsets, uint32_t nb, u
     r.nblocks = nb;
     r.blk = e.ws.u8("blk", total + 64);
     r.boff = e.ws.u32("boff", nb + 2);
-    HIP_OK(hipMemcpy(r.blk, bwt_in, total, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice));
+    stage_copy(e, r.blk, bwt_in, total, hipMemcpyHostToDevice);
+    stage_copy(e, r.boff, offsets, 4 * (nb + 1), hipMemcpyHostToDevice);
     block_info_stage(e.ws, r, e.stream);
     MtfResult m;
     mtf_stage(e.ws, r, r.blk, nb, total, m, e.stream);
     HIP_OK(hipStreamSynchronize(e.stream));
-    HIP_OK(hipMemcpy(mtf_offsets, m.mtf_off, 4 * (nb + 1), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(nmtf, m.nmtf, 4 * nb, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(freq, m.freq, 4 * (size_t)nb * kMaxAlpha, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(mtfv, m.mtfv, 2 * (size_t)mtf_offsets[nb], hipMemcpyDeviceToHost));
+    stage_copy(e, mtf_offsets, m.mtf_off, 4 * (nb + 1), hipMemcpyDeviceToHost);
+    stage_copy(e, nmtf, m.nmtf, 4 * nb, hipMemcpyDeviceToHost);
+    stage_copy(e, freq, m.freq, 4 * (size_t)nb * kMaxAlpha, hipMemcpyDeviceToHost);
+    if (mtf_offsets[nb] > mtfv_cap) return BZ_OUTBUFF_FULL;
+    stage_copy(e, mtfv, m.mtfv, 2 * (size_t)mtf_offsets[nb], hipMemcpyDeviceToHost);
     return BZ_OK;
   } catch (const HipFailure&) {
     return BZ_CONFIG_ERROR;
@@ -1404,11 +1367,11 @@ int bzg_stage_code_lengths(const uint32_t* freq, const int32_t* alpha, uint32_t 
     uint32_t* d_freq = e.ws.u32("test_freq", nf);
     int32_t* d_alpha = reinterpret_cast<int32_t*>(e.ws.u32("test_alpha", ntables));
     uint8_t* d_lens = e.ws.u8("test_lens", nf);
-    HIP_OK(hipMemcpy(d_freq, freq, 4 * nf, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(d_alpha, alpha, 4 * (size_t)ntables, hipMemcpyHostToDevice));
+    stage_copy(e, d_freq, freq, 4 * nf, hipMemcpyHostToDevice);
+    stage_copy(e, d_alpha, alpha, 4 * (size_t)ntables, hipMemcpyHostToDevice);
     code_lengths_test(d_freq, d_alpha, ntables, max_len, d_lens, e.stream);
     HIP_OK(hipStreamSynchronize(e.stream));
-    HIP_OK(hipMemcpy(lens, d_lens, nf, hipMemcpyDeviceToHost));
+    stage_copy(e, lens, d_lens, nf, hipMemcpyDeviceToHost);
     return BZ_OK;
   } catch (const HipFailure&) {
     return BZ_CONFIG_ERROR;

@@ -73,9 +73,12 @@ __global__ void __launch_bounds__(kT) k_origptr(const uint32_t* __restrict__ bof
   origptr[b] = o;
 }
 
-// identical periodic roots (e.g. every block of a long constant input) resolve once
+// identical periodic roots (e.g. every block of a long constant input) resolve once; the memo
+// holds at most kMemoBytes of root keys (a root can be ~450 KB) and bzg_release clears it
+constexpr size_t kMemoBytes = 8u << 20;
 std::mutex g_memo_mu;
 std::map<std::pair<std::string, int32_t>, int32_t> g_memo;
+size_t g_memo_bytes = 0;
 
 int32_t memo_copy_rank(const uint8_t* w, int32_t p, int32_t k) {
   std::pair<std::string, int32_t> key(std::string((const char*)w, (size_t)p), k);
@@ -85,13 +88,23 @@ int32_t memo_copy_rank(const uint8_t* w, int32_t p, int32_t k) {
     if (it != g_memo.end()) return it->second;
   }
   const int32_t r = copy_rank(w, p, k);
+  if ((size_t)p > kMemoBytes / 4) return r;  // too large to keep
   std::lock_guard<std::mutex> g(g_memo_mu);
-  if (g_memo.size() > 256) g_memo.clear();
-  g_memo.emplace(std::move(key), r);
+  if (g_memo_bytes + (size_t)p > kMemoBytes || g_memo.size() >= 256) {
+    g_memo.clear();
+    g_memo_bytes = 0;
+  }
+  if (g_memo.emplace(std::move(key), r).second) g_memo_bytes += (size_t)p;
   return r;
 }
 
 }  // namespace
+
+void copyrank_memo_clear() {
+  std::lock_guard<std::mutex> g(g_memo_mu);
+  g_memo.clear();
+  g_memo_bytes = 0;
+}
 
 void copyrank_count_stage(Rle1Result& r, Workspace& ws, hipStream_t st) {
   const uint32_t B = r.nblocks;

@@ -35,8 +35,10 @@ class Workspace {
   void release_all();
   // The stream that uses the workspace from now on: growth frees and allocates in that
   // stream's order (hipFreeAsync / hipMallocAsync) instead of synchronising the device, so
-  // concurrent engines on one device never wait for each other.
-  void set_stream(hipStream_t s) { stream_ = s; }
+  // concurrent engines on one device never wait for each other.  A switch makes the new
+  // stream wait for the work queued so far on the old one, so a later free on the new stream
+  // is ordered after every earlier use of the buffers.
+  void set_stream(hipStream_t s);
 
  private:
   struct Buf {
@@ -46,6 +48,7 @@ class Workspace {
   };
   void drop(Buf& b);
   hipStream_t stream_ = nullptr;
+  hipEvent_t handoff_ = nullptr;
   std::map<std::string, Buf> bufs_;
   size_t total_ = 0;
   uint32_t* crc_ = nullptr;
@@ -93,6 +96,7 @@ struct CopyRankJob {
   ~CopyRankJob();
 };
 void copyrank_count_stage(Rle1Result& r, Workspace& ws, hipStream_t st);
+void copyrank_memo_clear();  // bzg_release: drops the memoised periodic roots
 void copyrank_begin(const Rle1Result& r, const std::vector<uint32_t>& hboff, const std::vector<uint32_t>& hper,
                     const std::vector<uint32_t>& hbq, CopyRankJob& job, hipStream_t st);
 void copyrank_finish(Workspace& ws, const Rle1Result& r, const uint32_t* rank0, uint32_t* origptr, CopyRankJob& job,

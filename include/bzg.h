@@ -65,9 +65,10 @@ int bzg_stage_rle1(const void *src, uint64_t n, int level, int tail_merge, uint8
                    uint32_t *offsets, uint32_t *crcs, uint32_t *nblocks, uint32_t max_blocks);
 int bzg_stage_bwt(const uint8_t *blocks, const uint32_t *offsets, uint32_t nblocks, uint8_t *bwt, int32_t *origptr);
 /* bzg_stage_mtf: block b's nmtf[b] values at mtfv[mtf_offsets[b]] (offsets 8-aligned); mtfv
- * holds offsets[nblocks] + 8 * nblocks + 16 values. */
+ * holds mtfv_cap values, and offsets[nblocks] + 8 * nblocks + 16 always suffice.  Returns
+ * BZ_OUTBUFF_FULL (nothing written to mtfv) when mtf_offsets[nblocks] > mtfv_cap. */
 int bzg_stage_mtf(const uint8_t *bwt, const uint32_t *offsets, uint32_t nblocks, uint16_t *mtfv,
-                  uint32_t *mtf_offsets, uint32_t *nmtf, uint32_t *freq);
+                  uint64_t mtfv_cap, uint32_t *mtf_offsets, uint32_t *nmtf, uint32_t *freq);
 /* BZ2_hbMakeCodeLengths (reference huffman.c:63-148) on the GPU for ntables tables: freq holds
  * kMaxAlpha (258) counts per table, alpha[t] in 2..258 of them used; lens the same layout. */
 int bzg_stage_code_lengths(const uint32_t *freq, const int32_t *alpha, uint32_t ntables, int max_len, uint8_t *lens);

@@ -57,13 +57,16 @@ def gpu_bwt(blocks: bytes, offs):
 def gpu_mtf(bwt: bytes, offs):
     nb = len(offs) - 1
     total = offs[-1]
-    mtfv = (ctypes.c_uint16 * (total + 8 * nb + 16))()
+    cap = total + 8 * nb + 16
+    mtfv = (ctypes.c_uint16 * cap)()
     moff = (ctypes.c_uint32 * (nb + 1))()
     nmtf = (ctypes.c_uint32 * nb)()
     freq = (ctypes.c_uint32 * (nb * 258))()
     o32 = (ctypes.c_uint32 * (nb + 1))(*offs)
-    rc = B.lib().bzg_stage_mtf(bwt, o32, nb, mtfv, moff, nmtf, freq)
+    rc = B.lib().bzg_stage_mtf(bwt, o32, nb, mtfv, cap, moff, nmtf, freq)
     assert rc == 0, rc
+    if nb and moff[nb] > 0:  # a short buffer is refused, not overrun
+        assert B.lib().bzg_stage_mtf(bwt, o32, nb, mtfv, moff[nb] - 1, moff, nmtf, freq) == B.BZ_OUTBUFF_FULL
     arr = np.frombuffer(mtfv, dtype=np.uint16)
     fr = np.frombuffer(freq, dtype=np.uint32).reshape(nb, 258)
     return [arr[moff[b]: moff[b] + nmtf[b]].copy() for b in range(nb)], fr
