@@ -20,6 +20,7 @@ namespace {
 constexpr int kT = 256;      // threads
 constexpr int kPer = 16;     // bytes per thread
 constexpr int kTile = kT * kPer;
+static_assert(kT == 256 && kPer == 16, "SWAR fast paths: 4 waves, 4 words per thread");
 
 __device__ __forceinline__ void load16(const uint8_t* __restrict__ x, uint64_t n, uint64_t base,
                                        uint8_t (&v)[kPer]) {
@@ -69,25 +70,59 @@ __device__ __forceinline__ RunBits run_bits(const uint8_t* __restrict__ x, uint6
   return r;
 }
 
+// SWAR form of run_bits for a thread of a full interior tile (base >= 16, base + 16 < n):
+// w = its 16 bytes as little-endian words, pw = the word before them.  Byte k of the thread
+// starts a run iff it differs from the byte before; a run of 4 ends at it iff it equals the 3
+// bytes before.  Per word: three byte-shifted copies (v_alignbyte), xors, zero-byte masks.
+__device__ __forceinline__ uint32_t zero_byte_mask(uint32_t x) {  // 0x80 in every zero byte of x
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t byte_hi_bits(uint32_t m) {  // bits 7, 15, 23, 31 -> bits 0..3
+  return (((m >> 7) * 0x00204081u) >> 21) & 0xfu;
+}
+struct RunBitsW {
+  uint32_t starts;  // bit k: byte k of the thread starts a run
+  bool longrun;     // some byte of the thread ends a run of 4
+};
+__device__ __forceinline__ RunBitsW run_bits_w(const uint32_t (&w)[4], uint32_t pw) {
+  uint32_t st = 0, lr = 0, prev = pw;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t p1 = __builtin_amdgcn_alignbyte(w[j], prev, 3);  // bytes i-1
+    const uint32_t p2 = __builtin_amdgcn_alignbyte(w[j], prev, 2);  // bytes i-2
+    const uint32_t p3 = __builtin_amdgcn_alignbyte(w[j], prev, 1);  // bytes i-3
+    const uint32_t d1 = w[j] ^ p1;
+    st |= byte_hi_bits(~zero_byte_mask(d1) & 0x80808080u) << (4 * j);
+    lr |= zero_byte_mask(d1 | (w[j] ^ p2) | (w[j] ^ p3));
+    prev = w[j];
+  }
+  return RunBitsW{st, lr != 0};
+}
+
 // Pass 1: per tile, its last run start (for the carry scan) and its output size up to the
 // part that depends on the run entering the tile:  S = output bytes of the bytes from the
 // tile's first run start on, h = the bytes before it (they continue the run that starts at the
 // carried run start), ends = that run ends at the tile's byte h - 1.  k_rle_fix adds the h
 // bytes' output once the carries are known (closed form).  tinfo = S | h << 16 | ends << 31.
-__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_rle_count(const uint8_t* __restrict__ x, uint64_t n,
-                                                  uint32_t* __restrict__ tmax, uint32_t* __restrict__ tinfo) {
-  __shared__ uint32_t sh[kT / 64];
-  __shared__ uint32_t thr[kT];
-  const uint64_t ts = (uint64_t)blockIdx.x * kTile, base = ts + (uint64_t)threadIdx.x * kPer;
+constexpr uint32_t kRleG = 1;  // tiles per workgroup of the two RLE1 passes (4 with all loads in flight: +0.5 ms)
+
+__device__ __forceinline__ bool rle_interior(uint64_t tile, uint64_t n) {
+  return tile > 0 && (tile + 1) * kTile < n;
+}
+
+// k_rle_count for one tile that needs the per-byte rules (first, last or run-holding tiles).
+__device__ void rle_count_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t tile, uint32_t* __restrict__ tmax,
+                               uint32_t* __restrict__ tinfo, uint32_t* sh, uint32_t* thr) {
+  const uint64_t ts = tile * kTile, base = ts + (uint64_t)threadIdx.x * kPer;
   uint8_t v[kPer];
   load16(x, n, base, v);
   const RunBits rb = run_bits(x, n, base, v);
   const uint32_t len = (uint32_t)min<uint64_t>(kTile, n - ts);
   const bool general = __syncthreads_or(rb.longrun);
   const uint32_t incl = block_incl_max(rb.last1, sh);
-  if (threadIdx.x == kT - 1) tmax[blockIdx.x] = incl ? incl - 1u : 0u;
+  if (threadIdx.x == kT - 1) tmax[tile] = incl ? incl - 1u : 0u;
   if (!general) {  // every byte emits itself
-    if (threadIdx.x == 0) tinfo[blockIdx.x] = len;
+    if (threadIdx.x == 0) tinfo[tile] = len;
     return;
   }
   thr[threadIdx.x] = incl;
@@ -117,7 +152,55 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_rle_count(const uint8_t* 
   if (threadIdx.x == 0) {
     const uint32_t H = tot >> 16;
     const uint32_t ends = (H < len) || (ts + len >= n) || (x[ts + len] != x[ts + len - 1]);
-    tinfo[blockIdx.x] = (tot & 0xffffu) | (H << 16) | (ends << 31);
+    tinfo[tile] = (tot & 0xffffu) | (H << 16) | (ends << 31);
+  }
+}
+
+__global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_rle_count(const uint8_t* __restrict__ x, uint64_t n, uint64_t tiles,
+                                                  uint32_t* __restrict__ tmax, uint32_t* __restrict__ tinfo) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t thr[kT];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kRleG;
+  uint4 q[kRleG];
+  uint32_t pw[kRleG];
+#pragma unroll
+  for (uint32_t g = 0; g < kRleG; g++) {
+    const uint64_t base = (t0 + g) * kTile + (uint64_t)threadIdx.x * kPer;
+    if (rle_interior(t0 + g, n)) {
+      q[g] = *reinterpret_cast<const uint4*>(x + base);
+      pw[g] = *reinterpret_cast<const uint32_t*>(x + base - 4);
+    }
+  }
+#pragma unroll
+  for (uint32_t g = 0; g < kRleG; g++) {
+    const uint64_t tile = t0 + g;
+    if (tile >= tiles) break;
+    bool done = false;
+    if (rle_interior(tile, n)) {  // SWAR run bits first
+      const uint32_t w[4] = {q[g].x, q[g].y, q[g].z, q[g].w};
+      const RunBitsW rw = run_bits_w(w, pw[g]);
+      if (!__syncthreads_or(rw.longrun)) {  // every byte emits itself: size kTile, last run start
+        const uint64_t m = __ballot(rw.starts != 0);
+        if (__lane_id() == 0) {
+          uint32_t last = 0;
+          if (m) {
+            const uint32_t l = 63u - (uint32_t)__builtin_clzll(m);
+            const uint32_t stl = (uint32_t)__builtin_amdgcn_readlane((int)rw.starts, (int)l);
+            last = (uint32_t)(tile * kTile) + (threadIdx.x + l) * kPer + 31u - (uint32_t)__builtin_clz(stl) + 1u;
+          }
+          sh[threadIdx.x >> 6] = last;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          const uint32_t a = max(max(sh[0], sh[1]), max(sh[2], sh[3]));
+          tmax[tile] = a ? a - 1u : 0u;
+          tinfo[tile] = kTile;
+        }
+        done = true;
+      }
+    }
+    if (!done) rle_count_tile(x, n, tile, tmax, tinfo, sh, thr);
+    __syncthreads();  // sh / thr are reused by the next tile
   }
 }
 
@@ -209,20 +292,13 @@ __device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_
 #else
 #define BZG_EMIT_BOUNDS __launch_bounds__(kT)
 #endif
-__global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict__ x, uint64_t n,
-                                             const uint32_t* __restrict__ carry,
-                                             const uint32_t* __restrict__ out_base,
-                                             uint8_t* __restrict__ out, uint32_t* __restrict__ cbits,
-                                             uint32_t* __restrict__ last_len1) {
-  __shared__ uint32_t sh[kT / 64];
-  __shared__ uint32_t thr[kT];
-  // the tile's output (<= 5/4 of its input) staged so that LDS word k is output word
-  // (tile start & ~3) / 4 + k; written back with whole-word stores
-  __shared__ uint32_t ow[kTile * 5 / 16 + 4];
-  __shared__ uint32_t cb[kTile * 5 / 128 + 4];  // chunk-start bits, word k = global word (t0 >> 5) + k
+// k_emit for one tile that needs the per-byte rules.  ow / cb: the tile's LDS staging (cb zeroed).
+__device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t tile, const uint32_t* __restrict__ carry,
+                          const uint32_t* __restrict__ out_base, uint8_t* __restrict__ out,
+                          uint32_t* __restrict__ cbits, uint32_t* __restrict__ last_len1, uint32_t* sh, uint32_t* thr,
+                          uint32_t* ow, uint32_t* cb) {
   uint8_t* ob = reinterpret_cast<uint8_t*>(ow);
-  for (uint32_t i = threadIdx.x; i < kTile * 5 / 128 + 4; i += kT) cb[i] = 0;
-  const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kPer;
+  const uint64_t base = tile * kTile + (uint64_t)threadIdx.x * kPer;
   uint8_t v[kPer];
   load16(x, n, base, v);
   const RunBits rb = run_bits(x, n, base, v);
@@ -230,7 +306,7 @@ __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict_
   // tile has one): the others emit their bytes unchanged
   ByteInfo bi[kPer];
   if (__syncthreads_or(rb.longrun)) {
-    const uint32_t before = run_before(rb.last1 ? rb.last1 - 1u : 0u, carry[blockIdx.x], sh, thr);
+    const uint32_t before = run_before(rb.last1 ? rb.last1 - 1u : 0u, carry[tile], sh, thr);
     if (rb.longrun) byte_info_from(x, n, base, v, before, bi);
   }
   uint32_t s = rb.nvalid;
@@ -241,7 +317,7 @@ __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict_
   }
   uint32_t tot;
   uint32_t incl = block_incl_sum(s, sh, &tot);
-  const uint32_t t0 = out_base[blockIdx.x];
+  const uint32_t t0 = out_base[tile];
   const uint32_t lofs = t0 & 3u;  // LDS byte of output byte p: p - t0 + lofs
   uint32_t pos = t0 + incl - s;
   // chunk-start bits of this thread's outputs span <= 2 words (<= 32 output bytes)
@@ -307,6 +383,93 @@ __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict_
     } else {
       for (uint32_t c = max(b0, lofs); c < min(b1, lofs + tot); c++) out[(t0 & ~3u) + c] = ob[c];
     }
+  }
+}
+
+__global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict__ x, uint64_t n, uint64_t tiles,
+                                             const uint32_t* __restrict__ carry,
+                                             const uint32_t* __restrict__ out_base,
+                                             uint8_t* __restrict__ out, uint32_t* __restrict__ cbits,
+                                             uint32_t* __restrict__ last_len1) {
+  __shared__ uint32_t sh[kT / 64];
+  __shared__ uint32_t thr[kT];
+  // a tile's output (<= 5/4 of its input) staged so that LDS word k is output word
+  // (tile start & ~3) / 4 + k; written back with whole-word stores
+  __shared__ uint32_t ow[kTile * 5 / 16 + 4];
+  __shared__ uint32_t cb[kTile * 5 / 128 + 4];  // chunk-start bits, word k = global word (t0 >> 5) + k
+  const uint64_t t0g = (uint64_t)blockIdx.x * kRleG;
+  uint4 qs[kRleG];
+  uint32_t pws[kRleG];
+#pragma unroll
+  for (uint32_t g = 0; g < kRleG; g++) {
+    const uint64_t base = (t0g + g) * kTile + (uint64_t)threadIdx.x * kPer;
+    if (rle_interior(t0g + g, n)) {
+      qs[g] = *reinterpret_cast<const uint4*>(x + base);
+      pws[g] = *reinterpret_cast<const uint32_t*>(x + base - 4);
+    }
+  }
+#pragma unroll
+  for (uint32_t g = 0; g < kRleG; g++) {
+    const uint64_t tile = t0g + g;
+    if (tile >= tiles) break;
+    for (uint32_t i = threadIdx.x; i < kTile * 5 / 128 + 4; i += kT) cb[i] = 0;
+    bool done = false;
+    if (rle_interior(tile, n)) {  // SWAR run bits first
+      const uint4 q = qs[g];
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+      const uint32_t pw = pws[g];
+      const RunBitsW rw = run_bits_w(w, pw);
+      if (!__syncthreads_or(rw.longrun)) {
+        // every byte emits itself and starts a chunk iff it starts a run: the tile's output is
+        // its input at t0 = out_base, stored as whole words (the first and last word of the tile
+        // are shared with the neighbouring tiles: byte stores)
+        const uint32_t t0 = out_base[tile], lofs = t0 & 3u;
+        const uint32_t pos = t0 + threadIdx.x * kPer, sh5 = pos & 31u;
+        const uint32_t c0 = t0 >> 5, wi = (pos >> 5) - c0;
+        if (rw.starts) {
+          atomicOr(&cb[wi], rw.starts << sh5);
+          if (sh5 > 16u) atomicOr(&cb[wi + 1], rw.starts >> (32u - sh5));
+        }
+        uint32_t* outw = reinterpret_cast<uint32_t*>(out) + (pos >> 2);  // word of output byte pos
+        if (out != nullptr) {
+          if (lofs == 0) {
+            *reinterpret_cast<uint4*>(outw) = q;
+          } else {
+            // output word k of the thread holds the last lofs bytes of input word k - 1 and the
+            // first 4 - lofs of word k
+            const uint32_t sft = 4u - lofs;
+            uint32_t o[5];
+            o[0] = __builtin_amdgcn_alignbyte(w[0], pw, sft);
+  #pragma unroll
+            for (int k = 1; k < 4; k++) o[k] = __builtin_amdgcn_alignbyte(w[k], w[k - 1], sft);
+            o[4] = __builtin_amdgcn_alignbyte(0u, w[3], sft);  // the thread's last lofs bytes
+            if (threadIdx.x == 0) {
+              for (uint32_t c = lofs; c < 4u; c++) out[pos - lofs + c] = (uint8_t)(o[0] >> (8 * c));
+            } else {
+              outw[0] = o[0];
+            }
+            outw[1] = o[1];
+            outw[2] = o[2];
+            outw[3] = o[3];
+            if (threadIdx.x == kT - 1)
+              for (uint32_t c = 0; c < lofs; c++) out[pos - lofs + 16 + c] = (uint8_t)(o[4] >> (8 * c));
+          }
+        }
+        __syncthreads();
+        const uint32_t c1 = (t0 + kTile - 1) >> 5;
+        for (uint32_t k = threadIdx.x; k <= c1 - c0; k += kT) {
+          const uint32_t b = cb[k];
+          if (k == 0 || k == c1 - c0) {
+            if (b) atomicOr(&cbits[c0 + k], b);
+          } else {
+            cbits[c0 + k] = b;
+          }
+        }
+        done = true;
+      }
+    }
+    if (!done) emit_tile(x, n, tile, carry, out_base, out, cbits, last_len1, sh, thr, ow, cb);
+    __syncthreads();  // the LDS staging is reused by the next tile
   }
 }
 
@@ -559,21 +722,33 @@ __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x,
   const uint32_t s0 = min(hi, lo + w * per), s1 = min(hi, s0 + per);
   const uint32_t len = s1 - s0, R = len / kCrcRound, T = len - R * kCrcRound;
   __syncthreads();
-  auto crc16 = [&](const uint8_t* p) {
-    uint4 q;
-    __builtin_memcpy(&q, p, 16);
+  auto crc16q = [&](const uint4 q) {
     const uint32_t a = bswap32(q.x), d1 = bswap32(q.y), d2 = bswap32(q.z), d3 = bswap32(q.w);
     return tab[15][a >> 24] ^ tab[14][(a >> 16) & 255u] ^ tab[13][(a >> 8) & 255u] ^ tab[12][a & 255u] ^
            tab[11][d1 >> 24] ^ tab[10][(d1 >> 16) & 255u] ^ tab[9][(d1 >> 8) & 255u] ^ tab[8][d1 & 255u] ^
            tab[7][d2 >> 24] ^ tab[6][(d2 >> 16) & 255u] ^ tab[5][(d2 >> 8) & 255u] ^ tab[4][d2 & 255u] ^
            tab[3][d3 >> 24] ^ tab[2][(d3 >> 16) & 255u] ^ tab[1][(d3 >> 8) & 255u] ^ tab[0][d3 & 255u];
   };
+  auto crc16 = [&](const uint8_t* p) {
+    uint4 q;
+    __builtin_memcpy(&q, p, 16);
+    return crc16q(q);
+  };
+  auto fold = [&](uint32_t acc, uint32_t c) {
+    return mul[0][acc >> 24] ^ mul[1][(acc >> 16) & 255u] ^ mul[2][(acc >> 8) & 255u] ^ mul[3][acc & 255u] ^ c;
+  };
   uint32_t acc = 0;
   const uint8_t* px = x + s0 + 16 * threadIdx.x;
-  for (uint32_t r = 0; r < R; r++) {
-    const uint32_t c = crc16(px + (size_t)r * kCrcRound);
-    acc = mul[0][acc >> 24] ^ mul[1][(acc >> 16) & 255u] ^ mul[2][(acc >> 8) & 255u] ^ mul[3][acc & 255u] ^ c;
+  uint32_t r = 0;
+  // 4 rounds' loads in flight before their folds
+  for (; r + 4 <= R; r += 4) {
+    uint4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) __builtin_memcpy(&q[k], px + (size_t)(r + k) * kCrcRound, 16);
+#pragma unroll
+    for (int k = 0; k < 4; k++) acc = fold(acc, crc16q(q[k]));
   }
+  for (; r < R; r++) acc = fold(acc, crc16(px + (size_t)r * kCrcRound));
   uint32_t res = R ? crc_pow_mul(acc, xp2, kCrcRound - 16 * (threadIdx.x + 1) + T) : 0u;
   // the tail: thread t takes bytes [16 t, 16 t + 16) of it
   const uint32_t tb = 16 * threadIdx.x;
@@ -596,18 +771,24 @@ __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x,
   if (threadIdx.x == 0) part[b * kCrcSplit + w] = red[0] ^ red[1] ^ red[2] ^ red[3];
 }
 
-__global__ void k_crc_combine(const uint32_t* __restrict__ binst, const uint32_t* __restrict__ part,
-                              const uint32_t* __restrict__ xp2, uint32_t nb, uint32_t* __restrict__ bcrc) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per block: lane w < kCrcSplit shifts sub-range w's CRC to the block end, lane
+// kCrcSplit shifts the initial register through the whole block; the lanes' terms are xor-ed.
+__global__ void __launch_bounds__(64) k_crc_combine(const uint32_t* __restrict__ binst, const uint32_t* __restrict__ part,
+                                                    const uint32_t* __restrict__ xp2, uint32_t nb, uint32_t* __restrict__ bcrc) {
+  const uint32_t b = blockIdx.x, w = threadIdx.x;
   if (b >= nb) return;
   const uint32_t lo = binst[b], hi = binst[b + 1];
   const uint32_t per = ceil_div(hi - lo, kCrcSplit);
-  uint32_t c = crc_pow_mul(0xffffffffu, xp2, hi - lo);  // the initial register, shifted through
-  for (uint32_t w = 0; w < kCrcSplit; w++) {
+  uint32_t c = 0;
+  if (w < kCrcSplit) {
     const uint32_t e = min(hi, min(hi, lo + w * per) + per);
-    c ^= crc_pow_mul(part[b * kCrcSplit + w], xp2, hi - e);
+    c = crc_pow_mul(part[b * kCrcSplit + w], xp2, hi - e);
+  } else if (w == kCrcSplit) {
+    c = crc_pow_mul(0xffffffffu, xp2, hi - lo);  // the initial register, shifted through
   }
-  bcrc[b] = ~c;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
+  if (w == 0) bcrc[b] = ~c;
 }
 
 // In-use bitmap (8 words) per block; blocks are boff[b]..boff[b+1] of blk.  kInUseSplit
@@ -790,14 +971,14 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   uint32_t* binst = ws.u32("binst", max_blocks + 2);
   uint32_t* nbl = mtot + 4;
 
-  k_rle_count<<<tiles, kT, 0, st>>>(d_in, n, tmax, tinfo);
+  k_rle_count<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tinfo);
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Max, true, tmax, tmax, tiles, nullptr, scratch, st);
   k_rle_fix<<<ceil_div64(tiles, kT), kT, 0, st>>>(tmax, tinfo, tiles, tsum);
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
   HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
-  k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, blk, cbits, mtot + 8);
+  k_emit<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tsum, blk, cbits, mtot + 8);
   HIP_OK(hipGetLastError());
 
   // the cut walk of k_segment_fill from fill 0 (cuts into boff[1..]), then boff/nblocks
@@ -843,7 +1024,7 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   uint32_t* cpart = ws.u32("crc_part", (size_t)(max_blocks + 2) * kCrcSplit);
   k_block_crc<<<dim3(kCrcSplit, B), kT, 0, st>>>(d_in, binst, ws.crc_table(), ws.xpow2_table(), cpart);
   HIP_OK(hipGetLastError());
-  k_crc_combine<<<ceil_div(B, 64), 64, 0, st>>>(binst, cpart, ws.xpow2_table(), B, bcrc);
+  k_crc_combine<<<B, 64, 0, st>>>(binst, cpart, ws.xpow2_table(), B, bcrc);
   HIP_OK(hipGetLastError());
   res.bcrc = bcrc;
   res.blk = blk;
@@ -866,14 +1047,14 @@ void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t s
   uint32_t* scratch = ws.u32("seg_scan", scan_scratch_words(tiles) + 64);
   uint32_t* mtot = ws.u32("seg_m", 16);
   uint32_t* cbits = ws.u32("seg_cbits", mcap / 32 + 64);
-  k_rle_count<<<tiles, kT, 0, st>>>(d_in, n, tmax, tinfo);
+  k_rle_count<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tinfo);
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Max, true, tmax, tmax, tiles, nullptr, scratch, st);
   k_rle_fix<<<ceil_div64(tiles, kT), kT, 0, st>>>(tmax, tinfo, tiles, tsum);
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
   HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
-  k_emit<<<tiles, kT, 0, st>>>(d_in, n, tmax, tsum, nullptr, cbits, mtot + 8);
+  k_emit<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tsum, nullptr, cbits, mtot + 8);
   HIP_OK(hipGetLastError());
 }
 

@@ -297,11 +297,6 @@ __device__ __forceinline__ uint32_t tiled_next_cache(const Grp& gr) { return kTC
 #ifndef BZG_HIST_CP
 #define BZG_HIST_CP 4
 #endif
-#ifndef BZG_OFF_UNROLL
-#define BZG_OFF_UNROLL 1
-#endif
-#define BZG_STR_(x) #x
-#define BZG_UNROLL(n) _Pragma(BZG_STR_(unroll n))
 constexpr uint32_t kHistCp = BZG_HIST_CP;
 static_assert(kHistCp == 4 || kHistCp == 8, "histogram copies");
 
@@ -352,18 +347,30 @@ __global__ void __launch_bounds__(kT) k_s1_off(const Grp* __restrict__ G, uint32
   const uint32_t t0 = TP[g], t1 = t0 + ceil_div(gr.size, kDTile);
   const uint32_t d = threadIdx.x;
   if (d <= (uint32_t)kNCls) cc[d] = 0;
+  // kOffBatch tiles' counts are loaded before any is used (a group of the first pass has ~440
+  // tiles: one dependent load per tile was ~0.4 ms per pass)
+  constexpr uint32_t kOffBatch = 16;
   uint32_t total = 0;
-  BZG_UNROLL(BZG_OFF_UNROLL)
-  for (uint32_t t = t0; t < t1; t++) total += hist[(size_t)t * 256 + d];
+  for (uint32_t t = t0; t < t1; t += kOffBatch) {
+    uint32_t c[kOffBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kOffBatch; k++) c[k] = t + k < t1 ? hist[(size_t)(t + k) * 256 + d] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kOffBatch; k++) total += c[k];
+  }
   const uint32_t incl = block_incl_sum(total, sh, (uint32_t*)nullptr);
   const uint32_t base = gr.start + incl - total;
   tot[(size_t)g * 256 + d] = total;
   uint32_t run = base;
-  BZG_UNROLL(BZG_OFF_UNROLL)
-  for (uint32_t t = t0; t < t1; t++) {
-    const uint32_t c = hist[(size_t)t * 256 + d];
-    hist[(size_t)t * 256 + d] = run;
-    run += c;
+  for (uint32_t t = t0; t < t1; t += kOffBatch) {
+    uint32_t c[kOffBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kOffBatch; k++) c[k] = t + k < t1 ? hist[(size_t)(t + k) * 256 + d] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kOffBatch; k++) {
+      if (t + k < t1) hist[(size_t)(t + k) * 256 + d] = run;
+      run += c[k];
+    }
   }
   const uint32_t depth = grp_depth(gr) + 1;
   const uint32_t cl = bucket_cls(total, depth);
@@ -1367,55 +1374,69 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
   else return (uint32_t)__shfl_xor((int)x, J, 64);
 }
 
-template <int kSeg, int kPer, int J>
-__device__ __forceinline__ void bitonic_xlane(BsortKey (&K)[kPer], int k, uint32_t sl) {
-  constexpr int jl = J / kPer;
-  BsortKey o[kPer];
-#pragma unroll
-  for (int r = 0; r < kPer; r++)
-    o[r] = ((uint64_t)xor_lane<jl>((uint32_t)(K[r] >> 32)) << 32) | xor_lane<jl>((uint32_t)K[r]);
-#pragma unroll
-  for (int r = 0; r < kPer; r++) {
-    const uint32_t p = sl * kPer + r;
-    const bool keep_min = ((p & J) == 0) == ((p & k) == 0);
-    if (keep_min == key_less(o[r], K[r])) K[r] = o[r];
+// Direction masks of the bitonic network.  Element r of lane l sits at segment position
+// p = (l % kSeg) * kPer + r; at merge size kK and distance kJ it keeps the smaller key of its
+// pair iff ((p & kJ) == 0) == ((p & kK) == 0).  These are compile-time wave masks, turned into
+// lane conditions by inverse ballot (the mask is the VCC operand: no per-lane arithmetic, no
+// live SGPR pairs to spill).
+template <int kSeg, int kPer>
+constexpr uint64_t keep_min_mask(int kK, int kJ, int r) {
+  uint64_t m = 0;
+  for (int l = 0; l < 64; l++) {
+    const int p = (l % kSeg) * kPer + r;
+    if (((p & kJ) == 0) == ((p & kK) == 0)) m |= 1ull << l;
   }
+  return m;
 }
+template <int kSeg, int kPer>
+constexpr uint64_t ascending_mask(int kK, int r) {  // lanes whose position p has (p & kK) == 0
+  uint64_t m = 0;
+  for (int l = 0; l < 64; l++)
+    if ((((l % kSeg) * kPer + r) & kK) == 0) m |= 1ull << l;
+  return m;
+}
+__device__ __forceinline__ bool lane_in(uint64_t mask) { return __builtin_amdgcn_inverse_ballot_w64(mask); }
 
-template <int kSeg, int kPer, int J>
-__device__ __forceinline__ void bitonic_j(BsortKey (&K)[kPer], int k, uint32_t sl) {
-  if constexpr (J >= 1) {
-    if (J <= (k >> 1)) {
-      if constexpr (J < kPer) {  // partner in another register of this lane
+template <int kSeg, int kPer, int kK, int kJ>
+__device__ __forceinline__ void bitonic_stage(BsortKey (&K)[kPer]) {
+  if constexpr (kJ < kPer) {  // partner in another register of this lane
 #pragma unroll
-        for (int r = 0; r < kPer; r++) {
-          const int r2 = r ^ J;
-          if (r2 > r) {
-            const uint32_t p = sl * kPer + r;
-            const bool asc = (p & k) == 0;
-            // keys are distinct but for pads (equal; swapping them is harmless): one compare
-            const bool sw = key_less(K[r2], K[r]) == asc;
-            const BsortKey x = K[r], y = K[r2];
-            K[r] = sw ? y : x;
-            K[r2] = sw ? x : y;
-          }
-        }
-      } else {
-        bitonic_xlane<kSeg, kPer, J>(K, k, sl);
+    for (int r = 0; r < kPer; r++) {
+      const int r2 = r ^ kJ;
+      if (r2 > r) {
+        // keys are distinct but for pads (equal; swapping them is harmless): one compare
+        const bool sw = key_less(K[r2], K[r]) == lane_in(ascending_mask<kSeg, kPer>(kK, r));
+        const BsortKey x = K[r], y = K[r2];
+        K[r] = sw ? y : x;
+        K[r2] = sw ? x : y;
       }
     }
-    bitonic_j<kSeg, kPer, J / 2>(K, k, sl);
+  } else {  // partner lane l ^ (kJ / kPer), same register
+    constexpr int jl = kJ / kPer;
+    constexpr uint64_t keep = keep_min_mask<kSeg, kPer>(kK, kJ, 0);
+    BsortKey o[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; r++)
+      o[r] = ((uint64_t)xor_lane<jl>((uint32_t)(K[r] >> 32)) << 32) | xor_lane<jl>((uint32_t)K[r]);
+#pragma unroll
+    for (int r = 0; r < kPer; r++)
+      if (lane_in(keep) == key_less(o[r], K[r])) K[r] = o[r];
   }
 }
-
-template <int kSeg, int kPer>
-__device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
-  constexpr int kN = kSeg * kPer;
-  const uint32_t sl = __lane_id() % kSeg;
-#pragma unroll
-  for (int k = 2; k <= kN; k <<= 1) bitonic_j<kSeg, kPer, kN / 2>(K, k, sl);
+template <int kSeg, int kPer, int kK, int kJ>
+__device__ __forceinline__ void bitonic_merge(BsortKey (&K)[kPer]) {
+  if constexpr (kJ >= 1) {
+    bitonic_stage<kSeg, kPer, kK, kJ>(K);
+    bitonic_merge<kSeg, kPer, kK, kJ / 2>(K);
+  }
 }
-
+template <int kSeg, int kPer, int kK = 2>
+__device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
+  if constexpr (kK <= kSeg * kPer) {
+    bitonic_merge<kSeg, kPer, kK, kK / 2>(K);
+    bitonic<kSeg, kPer, kK * 2>(K);
+  }
+}
 
 // Later rounds of the one-group-per-wave classes only reorder inside the tied runs (keys
 // of different runs already differ in their run-start byte), and those runs are short: an
@@ -1443,11 +1464,32 @@ __device__ __forceinline__ void key_ce(BsortKey& a, BsortKey& b) {
   a = sw ? y : x;
   b = sw ? x : y;
 }
+// Neighbour exchanges and segment scans by DPP (one VALU operation each, no LDS round trip):
+// wave_shr:1 / wave_shl:1 move a value one lane up / down (the lane without a source gets 0).
+__device__ __forceinline__ uint32_t dpp_up1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+__device__ __forceinline__ uint32_t dpp_down1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);  // wave_shl:1
+}
+// Inclusive max over the lanes of each kSeg-lane segment (kSeg = 16, 32, 64), up to this lane:
+// row_shr 1, 2, 4, 8 inside rows of 16, then row_bcast15 / row_bcast31 across rows.
+template <int kSeg>
+__device__ __forceinline__ uint32_t seg_incl_max(uint32_t x) {
+  static_assert(kSeg == 16 || kSeg == 32 || kSeg == 64, "segments of whole DPP rows");
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  if constexpr (kSeg >= 32) x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast15
+  if constexpr (kSeg >= 64) x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast31
+  return x;
+}
 __device__ __forceinline__ BsortKey key_shfl_down1(BsortKey k) {
-  return ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(k >> 32), 1, 64) << 32) | (uint32_t)__shfl_down((int)(uint32_t)k, 1, 64);
+  return ((uint64_t)dpp_down1((uint32_t)(k >> 32)) << 32) | dpp_down1((uint32_t)k);
 }
 __device__ __forceinline__ BsortKey key_shfl_up1(BsortKey k) {
-  return ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(k >> 32), 1, 64) << 32) | (uint32_t)__shfl_up((int)(uint32_t)k, 1, 64);
+  return ((uint64_t)dpp_up1((uint32_t)(k >> 32)) << 32) | dpp_up1((uint32_t)k);
 }
 template <int kSeg, int kPer>
 __device__ __forceinline__ void oets(BsortKey (&K)[kPer], uint32_t steps) {
@@ -1832,8 +1874,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       if (r > 0) {
         q = K[r - 1];
       } else {
-        q = ((uint64_t)(uint32_t)__shfl_up((int)(K[kPer - 1] >> 32), 1, 64) << 32) |
-            (uint32_t)__shfl_up((int)(uint32_t)K[kPer - 1], 1, 64);
+        q = key_shfl_up1(K[kPer - 1]);
         if (sl == 0) q = ~K[r];  // no previous element
       }
       tp[r] = key_valid(K[r]) && key_tied(q, K[r]);
@@ -1843,7 +1884,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       if (r + 1 < kPer) {
         tn[r] = tp[r + 1];
       } else {
-        bool x = __shfl_down((int)tp[0], 1, 64) != 0;
+        bool x = dpp_down1(tp[0] ? 1u : 0u) != 0;
         if (sl == kSeg - 1) x = false;
         tn[r] = x;
       }
@@ -1857,13 +1898,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       mx = max(mx, tp[r] ? 0u : p);
       rsn[r] = mx;
     }
-    uint32_t pre = mx;
-#pragma unroll
-    for (int o = 1; o < kSeg; o <<= 1) {
-      const uint32_t x = (uint32_t)__shfl_up((int)pre, o, 64);
-      if (sl >= (uint32_t)o) pre = max(pre, x);
-    }
-    pre = (uint32_t)__shfl_up((int)pre, 1, 64);
+    uint32_t pre = dpp_up1(seg_incl_max<kSeg>(mx));
     if (sl == 0) pre = 0;
     bool any_tied = false;
 #pragma unroll
@@ -1927,7 +1962,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
 #pragma unroll
       for (int r = 0; r < kPer; r++)
         if (key_valid(K[r]) && !done[r] && !tn[r]) ml = max(ml, sl * kPer + r - rsn[r] + 1);
-      maxrun = (uint32_t)__shfl((int)wave_incl_max(ml), 63, 64);
+      maxrun = (uint32_t)__builtin_amdgcn_readlane((int)seg_incl_max<64>(ml), 63);
     }
     // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
 #pragma unroll
@@ -2440,7 +2475,7 @@ __global__ void __launch_bounds__(kT) k_qsa(const QBlock* __restrict__ qb, const
 // ------------------------------------------------------------------------------------
 void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& h_boff,
                const std::vector<uint32_t>& h_period, uint8_t* bwt, uint32_t* rank0, SortStats* stats,
-               hipStream_t st, const uint32_t* h_qper) {
+               hipStream_t st, const uint32_t* h_qper, const std::function<void()>* s1_done) {
   const uint32_t nb = r.nblocks;
   if (nb == 0) return;
   if (nb > 0xffffu) throw HipFailure(hipErrorInvalidValue);  // S2 keys carry 16-bit unit ids
@@ -2657,6 +2692,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     std::swap(cur6, nxt6);
     std::swap(cur7, nxt7);
   }
+  if (s1_done) (*s1_done)();  // (read_counters above synchronised the stream)
   if (debug && O.dbg) {
     unsigned long long d[4];
     HIP_OK(hipMemcpyAsync(d, O.dbg, sizeof(d), hipMemcpyDeviceToHost, st));

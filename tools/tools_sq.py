@@ -1,5 +1,5 @@
 """Per-kernel SQ counter summary from a rocprofv3 --pmc counter_collection.csv:
-python tools_sq.py <counter_collection.csv> [top]
+python tools_sq.py <counter_collection.csv> [top] [--tmpl]   (--tmpl: keep template arguments)
 Prints per kernel: waves, VALU / LDS / VMEM-read instructions per wave, and the split of wave
 cycles into active-issue, issue-stall (WAIT_INST_ANY) and parked (WAIT_ANY) fractions."""
 import collections
@@ -7,14 +7,18 @@ import csv
 import sys
 
 agg = collections.defaultdict(lambda: collections.Counter())
+tmpl = "--tmpl" in sys.argv
+sys.argv = [a for a in sys.argv if a != "--tmpl"]
 for r in csv.DictReader(open(sys.argv[1])):
-    n = r["Kernel_Name"].replace("(anonymous namespace)", "").split("(")[0].split("::")[-1].split("<")[0]
+    n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("::")[-1]
+    if not tmpl:
+        n = n.split("<")[0]
     agg[n][r["Counter_Name"]] += float(r["Counter_Value"])
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 rows = sorted(agg.items(), key=lambda kv: -kv[1]["SQ_WAVE_CYCLES"])[:top]
-print(f"{'kernel':22s} {'waves':>10s} {'valu/w':>8s} {'lds/w':>7s} {'vmem/w':>7s} {'act':>5s} {'stall':>5s} {'park':>5s} {'Gcyc':>7s}")
+print(f"{'kernel':40s} {'waves':>10s} {'valu/w':>8s} {'lds/w':>7s} {'vmem/w':>7s} {'act':>5s} {'stall':>5s} {'park':>5s} {'Gcyc':>7s}")
 for n, c in rows:
     w = max(c["SQ_WAVES"], 1)
     wc = max(c["SQ_WAVE_CYCLES"], 1)
-    print(f"{n:22s} {int(w):10d} {c['SQ_INSTS_VALU']/w:8.0f} {c['SQ_INSTS_LDS']/w:7.0f} {c['SQ_INSTS_VMEM_RD']/w:7.0f} "
+    print(f"{n[:40]:40s} {int(w):10d} {c['SQ_INSTS_VALU']/w:8.0f} {c['SQ_INSTS_LDS']/w:7.0f} {c['SQ_INSTS_VMEM_RD']/w:7.0f} "
           f"{c['SQ_ACTIVE_INST_ANY']/wc:5.2f} {c['SQ_WAIT_INST_ANY']/wc:5.2f} {c['SQ_WAIT_ANY']/wc:5.2f} {wc/1e9:7.2f}")

@@ -16,6 +16,12 @@ def main():
     path = sys.argv[1]
     first = sys.argv[2] if len(sys.argv) > 2 else "k_rle_count"
     rows = list(csv.DictReader(open(path)))
+    for r in rows:  # full demangled names (no -T): "void bzg::(anonymous namespace)::k_x<...>(args)"
+        n = r["Kernel_Name"]
+        if n.startswith("void "):
+            n = n[5:]
+        n = n.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].split("::")[-1]
+        r["Kernel_Name"] = n
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     starts = [int(r["Start_Timestamp"]) for r in rows if r["Kernel_Name"].startswith(first)]
     if not starts:
