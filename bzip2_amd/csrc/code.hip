@@ -178,12 +178,22 @@ __global__ void k_init_tables(uint32_t b0, const uint32_t* __restrict__ nmtf_g, 
 }
 
 constexpr uint32_t kCfVec = (kT * kGroupSize + 8 * kT - 1) / (8 * kT);  // 16-byte words per thread per chunk
+// BZG_CF_MODE 1: one 64-bit length word per symbol (all six tables in 10-bit fields), so a
+// symbol costs one LDS read and one add; 0: two 32-bit words (tables 0-2 / 3-5)
+#ifndef BZG_CF_MODE
+#define BZG_CF_MODE 1
+#endif
 struct CfLds {
   alignas(16) uint16_t chunk[kT * kGroupSize + 8];
+#if BZG_CF_MODE == 1
+  uint64_t lenp[kMaxAlpha];
+#else
   uint32_t lenp[2][kMaxAlpha];       // lengths of tables 0-2 / 3-5 in 10-bit fields
+#endif
   uint32_t rfreq[kNGroups][kMaxAlpha * 2];  // 2 bank-spread copies per counter (thread & 1)
   uint32_t sh[8];
 };
+static_assert(kGroupSize * 17 < 1024, "a group's cost under one table fits a 10-bit field");
 
 // final == 0: select tables and count frequencies (into rf_g); final == 1: payload bits of
 // every group under its (already chosen) table into gbits_g, their sum into info_g[b*8+6].
@@ -203,8 +213,15 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
   const uint16_t* mv = mtfv + mtf_off[b];
   const uint8_t* L = lens_g + (size_t)b * kNGroups * kMaxAlpha;
   for (int v = threadIdx.x; v < kMaxAlpha; v += kT) {
+#if BZG_CF_MODE == 1
+    uint64_t x = 0;
+#pragma unroll
+    for (int t = 0; t < kNGroups; t++) x |= (uint64_t)L[t * kMaxAlpha + v] << (10 * t);
+    S.lenp[v] = x;
+#else
     S.lenp[0][v] = L[v] | ((uint32_t)L[kMaxAlpha + v] << 10) | ((uint32_t)L[2 * kMaxAlpha + v] << 20);
     S.lenp[1][v] = L[3 * kMaxAlpha + v] | ((uint32_t)L[4 * kMaxAlpha + v] << 10) | ((uint32_t)L[5 * kMaxAlpha + v] << 20);
+#endif
   }
   if (!final)
     for (int i = threadIdx.x; i < kNGroups * kMaxAlpha * 2; i += kT) (&S.rfreq[0][0])[i] = 0;
@@ -236,6 +253,15 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
     if (g < nsel) {
       const uint16_t* c = S.chunk + threadIdx.x * kGroupSize;
       const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
+      // 50 lengths <= 17: every 10-bit field sum stays below 1024
+#if BZG_CF_MODE == 1
+      uint64_t acc = 0;
+#pragma unroll 10
+      for (uint32_t i = 0; i < n; i++) acc += S.lenp[c[i]];
+      uint32_t cost[kNGroups];
+#pragma unroll
+      for (int t = 0; t < kNGroups; t++) cost[t] = (uint32_t)(acc >> (10 * t)) & 1023u;
+#else
       uint32_t a = 0, bsum = 0;
 #pragma unroll 10
       for (uint32_t i = 0; i < n; i++) {
@@ -243,9 +269,9 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
         a += S.lenp[0][v];
         bsum += S.lenp[1][v];
       }
-      // 50 lengths <= 17: every 10-bit field sum stays below 1024
       const uint32_t cost[kNGroups] = {a & 1023u, (a >> 10) & 1023u, a >> 20,
                                        bsum & 1023u, (bsum >> 10) & 1023u, bsum >> 20};
+#endif
       if (final) {
         const uint32_t bits = cost[selo[g]];
         gbits_g[(size_t)b * kMaxSelectors + g] = (uint16_t)bits;
@@ -261,16 +287,15 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
         selo[g] = (uint8_t)bt;
         // symbols 0..3 (RUNA, RUNB and the nearest ranks: most of the group on text) are
         // counted in registers first, so few lanes of a wave hit the same LDS counter
-        uint32_t f0 = 0, f1 = 0, f2 = 0, f3 = 0;
+        // (four byte counters in one word: a group has at most 50 symbols)
+        uint32_t f4 = 0;
 #pragma unroll 10
         for (uint32_t i = 0; i < n; i++) {
           const uint32_t v = c[i];
-          f0 += v == 0;
-          f1 += v == 1;
-          f2 += v == 2;
-          f3 += v == 3;
           if (v > 3) atomicAdd(&S.rfreq[bt][v * 2 + (threadIdx.x & 1u)], 1u);
+          else f4 += 1u << (8 * v);
         }
+        const uint32_t f0 = f4 & 255u, f1 = (f4 >> 8) & 255u, f2 = (f4 >> 16) & 255u, f3 = f4 >> 24;
         const uint32_t cp = threadIdx.x & 1u;
         if (f0) atomicAdd(&S.rfreq[bt][0 + cp], f0);
         if (f1) atomicAdd(&S.rfreq[bt][2 + cp], f1);

@@ -1485,6 +1485,16 @@ __device__ __forceinline__ uint32_t seg_incl_max(uint32_t x) {
   if constexpr (kSeg >= 64) x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast31
   return x;
 }
+// The same as an inclusive sum over the whole wave.
+__device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast31
+  return x;
+}
 __device__ __forceinline__ BsortKey key_shfl_down1(BsortKey k) {
   return ((uint64_t)dpp_down1((uint32_t)(k >> 32)) << 32) | dpp_down1((uint32_t)k);
 }
@@ -1516,6 +1526,42 @@ __device__ __forceinline__ void oets(BsortKey (&K)[kPer], uint32_t steps) {
       }
     }
   }
+}
+
+// Later rounds of the one-group-per-wave classes with several registers per lane, when the
+// tied runs are too long for the transposition sort: if at most 64 elements are still tied,
+// they are packed one per lane (in sorted order, through the wave's 64-key LDS scratch X),
+// sorted by a 64-key network (21 stages instead of 28 / 36) and put back.  The tied runs keep
+// their places (their keys lead with the run start), so the packed order maps back 1:1.
+// Returns false (nothing done) when more than 64 are tied.
+#ifndef BZG_S2_CSORT
+#define BZG_S2_CSORT 1
+#endif
+template <int kPer>
+__device__ __forceinline__ bool compact_sort(BsortKey (&K)[kPer], const bool (&done)[kPer], uint64_t* X) {
+  uint32_t mine = 0;
+#pragma unroll
+  for (int r = 0; r < kPer; r++) mine += (key_valid(K[r]) && !done[r]) ? 1u : 0u;
+  const uint32_t incl = wave_incl_sum_dpp(mine);
+  const uint32_t nt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  if (nt > 64) return false;
+  const uint32_t lane = __lane_id();
+  uint32_t ci = incl - mine;
+#pragma unroll
+  for (int r = 0; r < kPer; r++)
+    if (key_valid(K[r]) && !done[r]) X[ci++] = K[r];
+  wave_sync();
+  BsortKey k1[1] = {lane < nt ? X[lane] : kPadKey};
+  wave_sync();
+  bitonic<64, 1>(k1);
+  X[lane] = k1[0];
+  wave_sync();
+  ci = incl - mine;
+#pragma unroll
+  for (int r = 0; r < kPer; r++)
+    if (key_valid(K[r]) && !done[r]) K[r] = X[ci++];
+  wave_sync();
+  return true;
 }
 
 // Runs still tied after kRounds bitonic rounds (few rotations, often long repeats) are
@@ -1862,9 +1908,20 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   constexpr int kDbgCls = kSeg * kPer == 16 ? 1 : kSeg * kPer == 32 ? 2 : kSeg * kPer == 64 ? 3 : kSeg * kPer == 128 ? 4 : 5;
   for (;;) {
     if (O.dbg && lane == 0) atomicAdd(&O.dbg[8 + 8 * kDbgCls + min(round, 6)], 1ull);
+    if (O.dbg && round > 0 && kDbgCls >= 3) {  // later rounds: longest tied run and tied elements
+      uint32_t nt = 0;
+#pragma unroll
+      for (int r = 0; r < kPer; r++) nt += (key_valid(K[r]) && !done[r]) ? 1u : 0u;
+      nt = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nt), 63);
+      auto bk = [](uint32_t x) { return x <= 4 ? 0 : x <= 8 ? 1 : x <= 16 ? 2 : x <= 32 ? 3 : x <= 64 ? 4 : 5; };
+      if (lane == 0) {
+        atomicAdd(&O.dbg[64 + 16 * (kDbgCls - 3) + bk(maxrun)], 1ull);
+        atomicAdd(&O.dbg[64 + 16 * (kDbgCls - 3) + 8 + bk(nt)], 1ull);
+      }
+    }
     if ((kSeg == 64 || BZG_OETS_SEG) && BZG_OETS_MAX > 0 && round > 0 && maxrun <= BZG_OETS_MAX)
       oets<kSeg, kPer>(K, maxrun);
-    else
+    else if (!(kSeg == 64 && kPer > 1 && kPre && BZG_S2_CSORT && round > 0 && compact_sort<kPer>(K, done, Lx[w])))
       bitonic<kSeg, kPer>(K);
     // ties with the previous / next position of the segment (same run start and key)
     bool tp[kPer], tn[kPer];
@@ -2563,8 +2620,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   O.tdeep = ws.typed<Grp>("sort_tdeep", ccap[0]);
   O.dbg = nullptr;
   if (getenv("BZG_DEBUG")) {
-    O.dbg = reinterpret_cast<unsigned long long*>(ws.u32("sort_dbg", 128));
-    HIP_OK(hipMemsetAsync(O.dbg, 0, 512, st));
+    O.dbg = reinterpret_cast<unsigned long long*>(ws.u32("sort_dbg", 256));
+    HIP_OK(hipMemsetAsync(O.dbg, 0, 1024, st));
   }
   // counters: 0..7 class counts (init), 8..16 class bounds + total, 17 tiles, 18 packed total,
   // 19 n_deep, 20 min depth
@@ -2814,6 +2871,15 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         fprintf(stderr, "[bzg sort S2] class %d waves by round: %llu %llu %llu %llu %llu %llu %llu+ tail %llu\n", c,
                 d[8 + 8 * c], d[9 + 8 * c], d[10 + 8 * c], d[11 + 8 * c], d[12 + 8 * c], d[13 + 8 * c], d[14 + 8 * c],
                 d[15 + 8 * c]);
+      unsigned long long e[48];
+      HIP_OK(hipMemcpyAsync(e, O.dbg + 64, sizeof(e), hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      for (int c = 3; c < 6; c++) {
+        const unsigned long long* x = e + 16 * (c - 3);
+        fprintf(stderr, "[bzg sort S2] class %d later rounds: longest run <=4:%llu <=8:%llu <=16:%llu <=32:%llu <=64:%llu >64:%llu"
+                " | tied <=4:%llu <=8:%llu <=16:%llu <=32:%llu <=64:%llu >64:%llu\n", c, x[0], x[1], x[2], x[3], x[4], x[5],
+                x[8], x[9], x[10], x[11], x[12], x[13]);
+      }
     }
   }
   HIP_OK(hipGetLastError());
