@@ -1564,6 +1564,46 @@ __device__ __forceinline__ bool compact_sort(BsortKey (&K)[kPer], const bool (&d
   return true;
 }
 
+// A group whose members are all still tied (one run: boilerplate, long repeats) advances its
+// depth by the members' common prefix, 32 characters per step, instead of 6-7 characters per
+// sorting round: every member's next 64 characters are compared with those of the first
+// member (lane 0, register 0), word by word; the depth moves to the first word where some
+// member differs.  Stops at `limit` and where a member's window wraps past the unit end.
+#ifndef BZG_S2_SKIP
+#define BZG_S2_SKIP 1
+#endif
+template <int kPer>
+__device__ __forceinline__ uint32_t common_depth(const uint8_t* t, uint32_t len, const uint32_t (&v)[kPer],
+                                                 const bool (&live)[kPer], uint32_t depth, uint32_t limit) {
+  constexpr int kW = 8;  // words (32 characters) per step; one member at a time keeps few registers live
+  while (depth < limit) {
+    bool wrap = false;
+#pragma unroll
+    for (int r = 0; r < kPer; r++) wrap |= live[r] && cyc_pos(v[r], depth, len) + 4 * kW + 4 > len;
+    if (__ballot(wrap)) break;
+    uint32_t ref[kW], diff = 0;  // bit j: some member differs from the first in word j
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const uint32_t q = live[r] ? cyc_pos(v[r], depth, len) : 0u;
+      uint32_t raw[kW + 1], k[kW];
+      text_raw<kW>(t + q, raw);
+      text_words_of<kW>(t + q, raw, k);
+#pragma unroll
+      for (int j = 0; j < kW; j++) {
+        if (r == 0) ref[j] = (uint32_t)__builtin_amdgcn_readlane((int)k[j], 0);
+        if (__ballot(live[r] && k[j] != ref[j])) diff |= 1u << j;
+      }
+    }
+    if (diff == 0) {
+      depth += 4 * kW;
+    } else {
+      depth += 4u * (uint32_t)__builtin_ctz(diff);
+      break;
+    }
+  }
+  return depth;
+}
+
 // Runs still tied after kRounds bitonic rounds (few rotations, often long repeats) are
 // finished in place: every tied rotation ranks itself among the members of its run that are
 // still tied with it (same class, named by the lowest position of the class) on the next 16
@@ -1902,6 +1942,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
 #pragma unroll
   for (int r = 0; r < kPer; r++) done[r] = false;
   int round = 0;
+  bool skipped = false;  // common_depth moved the depth: the second-round keys in Lx are stale
   uint32_t maxrun = 0;  // longest tied run of the previous round (kSeg = 64)
   // BZG_DEBUG: waves entering each round, per class (dbg[8 + 8 * class + round]; round 7:
   // the rank-counting tail)
@@ -1979,6 +2020,23 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
     }
     if (__ballot(any_tied) == 0) break;
     depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
+    if constexpr (kSeg == 64 && kPer <= 2 && BZG_S2_SKIP) {  // (kPer 4: the registers would cost a wave per SIMD)
+      bool split = false;  // the group is no longer one run
+#pragma unroll
+      for (int r = 0; r < kPer; r++) split |= key_valid(K[r]) && (done[r] || rsn[r] != 0);
+      if (__ballot(split) == 0 && depth < B.dwave) {
+        uint32_t vv[kPer];
+        bool live[kPer];
+#pragma unroll
+        for (int r = 0; r < kPer; r++) {
+          live[r] = key_valid(K[r]);
+          vv[r] = live[r] ? Lv[w][key_idx(K[r])] : 0u;
+        }
+        const uint32_t d2 = common_depth<kPer>(t, U.len, vv, live, depth, B.dwave);
+        skipped |= d2 != depth;
+        depth = d2;
+      }
+    }
     if constexpr (kCompact) {
       if (depth < B.dwave && bsort_compact_tail<kPer>(B, O, g, U, depth, K, done, tn, rsn, Lv[w], Lc[w], SC[w])) break;
     }
@@ -2031,7 +2089,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         K[r] = make_key2(p, 0, 0, idx);
       } else {
         uint32_t hi, lo;
-        if (kPre && round == 1) {
+        if (kPre && round == 1 && !skipped) {
           const uint64_t x = Lx[w][kPre ? idx : 0];
           hi = (uint32_t)(x >> 32);
           lo = (uint32_t)x;
