@@ -519,9 +519,15 @@ __global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_
   if (i == n - 1 || P[i + 1] / kSG != t) last[t] = i + 1;
 }
 
-__global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ sizes) {
+// Group sizes (for the tile prefix) and each group's unit beside it, so that a packed tile
+// reads its groups and their units in one round trip instead of two dependent ones.
+__global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, const Unit* __restrict__ units,
+                              uint32_t* __restrict__ sizes, Unit* __restrict__ gunits) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) sizes[g] = L[g].size;
+  if (g >= n) return;
+  const Grp gr = L[g];
+  sizes[g] = gr.size;
+  gunits[g] = units[gr.unit];
 }
 
 // packed kernels: 512 threads x 8 elements (a tile holds < 2 kSG rotations; kSG on average,
@@ -544,14 +550,15 @@ struct S1sLds {
 };
 
 // Loads the tile's groups; returns the number of groups (0: empty tile).
-__device__ __forceinline__ uint32_t s1s_setup(S1sLds& S, const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
-                                              const uint32_t* __restrict__ last, uint32_t t, const SortBufs& B) {
+__device__ __forceinline__ uint32_t s1s_setup(S1sLds& S, const Grp* __restrict__ SG, const Unit* __restrict__ GU,
+                                              const uint32_t* __restrict__ first, const uint32_t* __restrict__ last,
+                                              uint32_t t) {
   const uint32_t i0 = first[t];
   if (i0 == 0xffffffffu) return 0;
   const uint32_t ni = min(last[t], i0 + kSGrp) - i0;
   if (threadIdx.x < ni) {
     const Grp g = SG[i0 + threadIdx.x];
-    const Unit U = B.units[g.unit];
+    const Unit U = GU[i0 + threadIdx.x];
     S.gstart[threadIdx.x] = g.start;
     S.goff[threadIdx.x + 1] = g.size;
     S.gfl[threadIdx.x] = g.flags;
@@ -603,7 +610,8 @@ __device__ __forceinline__ uint32_t rec_pack(uint32_t j, uint32_t start, uint32_
   return (j << 27) | (start << 14) | size;  // group:5 | start:13 | size:14 (tiles < 8192 rotations)
 }
 static_assert(kSGrp <= 32 && 2 * kSG <= 8192, "packed bucket records");
-__global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
+__global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __restrict__ SG, const Unit* __restrict__ GU,
+                                                 const uint32_t* __restrict__ first,
                                                  const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
                                                  SortBufs B, SortOut O, uint32_t* __restrict__ rec,
                                                  uint32_t* __restrict__ nrec, uint32_t* __restrict__ ccnt, uint32_t nTot,
@@ -612,7 +620,7 @@ __global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __re
   __shared__ uint32_t Lv[2 * kSG];  // the tile's rotations in bucket order
   __shared__ uint32_t nr;
   const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t ni = s1s_setup(S, SG, first, last, t, B);
+  const uint32_t ni = s1s_setup(S, SG, GU, first, last, t);
   if (ni == 0) {
     if (threadIdx.x < (uint32_t)kNCls) ccnt[(size_t)threadIdx.x * nTot + ibase + t] = 0;
     if (threadIdx.x == 0) nrec[t] = 0;
@@ -2694,6 +2702,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* tot = ws.u32("sort_tot", ccap[7] * 256);
   uint32_t* ccnt = ws.u32("sort_ccnt", kNCls * max_tot + 16);
   uint32_t* P = ws.u32("sort_P", ccap[6] + 16);
+  Unit* gunits = ws.typed<Unit>("sort_gunits", ccap[6] + 16);  // the packed groups' units
   uint32_t* first = ws.u32("sort_first", max_ptiles);
   uint32_t* last = ws.u32("sort_last", max_ptiles);
   uint32_t* nrec = ws.u32("sort_nrec", max_ptiles);
@@ -2749,7 +2758,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     if (n6) {
-      k_group_sizes<<<grid(n6), kT, 0, st>>>(cur6, n6, P);
+      k_group_sizes<<<grid(n6), kT, 0, st>>>(cur6, n6, units, P, gunits);
       HIP_OK(hipGetLastError());
       scan_u32(ScanOp::Sum, true, P, P, n6, cnt + 18, scratch, st);
     }
@@ -2770,7 +2779,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       if (use_s1p)
         k_s1p<<<nT, kPT, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7, nT);
       else
-        k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
+        k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, gunits, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
       HIP_OK(hipGetLastError());
     }
     if (n7) {
