@@ -452,7 +452,7 @@ def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False, nb_text=0):
 
 def pmc_traffic(a):
     """HBM bytes per step of this workload, from the newest committed PMC summary
-    (profiles/*_hbm_traffic_v*.json, written by tools/tools_traffic.py); None if there is none."""
+    (profiles/*_hbm_traffic_v*.json, written by tools/traffic.py); None if there is none."""
     import glob
     import re
 

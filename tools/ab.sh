@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 same-box A/B (development tool): optional -k GPU tests per variant, then the bench
 # round-robin over the variants (3 rounds), then a one-stream kernel trace per variant.
-# usage: tools/r04_ab.sh <tag> <pytest -k expr | none> <variant> [variant ...]
+# usage: tools/ab.sh <tag> <pytest -k expr | none> <variant> [variant ...]
 #   variant: "base" or a name under bzip2_amd/var/ (tools/variant.sh), optionally ":ENV=1,ENV2=2"
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 final measurement on one GPU (development tool): full GPU tests, the default bench
 # line, a kernel trace of one text step, and the FETCH_SIZE / WRITE_SIZE passes.
-# usage: tools/r03_final.sh <tag> [tests|notests]
+# usage: tools/final.sh <tag> [tests|notests]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=$1; O=gpurun_out/$T; mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over one 1e9-byte step (kernel trace + one counter set per rocprofv3 run).
-# usage: tools_r02_pmc.sh <tag> "<set1>" "<set2>" ...
+# usage: tools/pmc_passes.sh <tag> "<set1>" "<set2>" ...
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=$1; shift; O=gpurun_out/$T; mkdir -p $O

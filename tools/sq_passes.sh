@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counter passes over one 1e9-byte text step (development tool), one-stream and production
 # two-stream settings: issue split (active / stall / parked), instruction mix, LDS conflicts.
-# usage: tools/r04_sq.sh <tag>
+# usage: tools/sq_passes.sh <tag>
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=$1; O=gpurun_out/$T; mkdir -p $O
@@ -17,6 +17,6 @@ for mode in one two; do
       timeout -s KILL 240 rocprofv3 --pmc $set --output-format csv -d $O/${mode}$i -o run -- python bench.py --steps 1 --warmup 0 --no-cpu --no-h2h --no-extra > $O/${mode}$i.log 2>&1 || { echo "pass failed"; tail -20 $O/${mode}$i.log; exit 1; }
     fi
   done
-  python tools/tools_sq.py $O/${mode}1/run_counter_collection.csv 40 --tmpl > $O/sq_${mode}.txt
+  python tools/sq_summary.py $O/${mode}1/run_counter_collection.csv 40 --tmpl > $O/sq_${mode}.txt
 done
 echo "done $(date)"

@@ -1,5 +1,5 @@
 """Per-kernel SQ counter summary from a rocprofv3 --pmc counter_collection.csv:
-python tools_sq.py <counter_collection.csv> [top] [--tmpl]   (--tmpl: keep template arguments)
+python tools/sq_summary.py <counter_collection.csv> [top] [--tmpl]   (--tmpl: keep template arguments)
 Prints per kernel: waves, VALU / LDS / VMEM-read instructions per wave, and the split of wave
 cycles into active-issue, issue-stall (WAIT_INST_ANY) and parked (WAIT_ANY) fractions."""
 import collections

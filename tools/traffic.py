@@ -3,7 +3,7 @@ Correction per MI355X_MICROARCH.md (HBM section): on gfx950 FETCH_SIZE counts ha
 of WIDE COALESCED STREAMING reads (16 B per lane), so only the kernels whose reads are such
 streams (STREAMING below) get 2 x FETCH_SIZE; every other kernel (the sort's 4-12-byte
 gathers, the MTF and coding kernels) is reported raw, since the rule is uncalibrated for them.
-usage: python tools_traffic.py <pmc_dir> <bench.json> <out.json>"""
+usage: python tools/traffic.py <pmc_dir> <bench.json> <out.json>"""
 import collections
 import csv
 import json

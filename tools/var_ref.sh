@@ -1,6 +1,6 @@
 #!/bin/bash
 # Builds the library of a git revision into bzip2_amd/var/<name>/ (development A/B tool):
-#   tools/r04_var_ref.sh <name> <rev> ["-DFOO=1 ..."]
+#   tools/var_ref.sh <name> <rev> ["-DFOO=1 ..."]
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
