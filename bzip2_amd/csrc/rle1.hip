@@ -110,6 +110,19 @@ __device__ __forceinline__ bool rle_interior(uint64_t tile, uint64_t n) {
   return tile > 0 && (tile + 1) * kTile < n;
 }
 
+// An interior tile inside one run (config 4): its bytes, the byte before it and the byte
+// after it are all equal.  Such a tile starts no run and ends none; every thread must call.
+__device__ __forceinline__ bool tile_in_run(const uint8_t* __restrict__ x, uint64_t ts, const uint32_t (&w)[4],
+                                            uint32_t pw) {
+  const uint32_t c = x[ts], pat = c * 0x01010101u;
+  bool ok = w[0] == pat && w[1] == pat && w[2] == pat && w[3] == pat && (pw >> 24) == c;
+  if (threadIdx.x == kT - 1) ok = ok && x[ts + kTile] == c;
+  return !__syncthreads_or(!ok);
+}
+// RLE1 output bytes of run offsets [0, x): offsets r mod 255 <= 3 emit the byte, r mod 255 ==
+// 254 closes a chunk with its count byte (the closed form of k_rle_fix)
+__device__ __forceinline__ uint64_t run_emitted(uint64_t x);
+
 // k_rle_count for one tile that needs the per-byte rules (first, last or run-holding tiles).
 __device__ void rle_count_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t tile, uint32_t* __restrict__ tmax,
                                uint32_t* __restrict__ tinfo, uint32_t* sh, uint32_t* thr) {
@@ -178,6 +191,14 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_rle_count(const uint8_t* 
     bool done = false;
     if (rle_interior(tile, n)) {  // SWAR run bits first
       const uint32_t w[4] = {q[g].x, q[g].y, q[g].z, q[g].w};
+      if (tile_in_run(x, tile * kTile, w, pw[g])) {  // no run start: h = kTile, closed form
+        if (threadIdx.x == 0) {
+          tmax[tile] = 0;
+          tinfo[tile] = (uint32_t)kTile << 16;
+        }
+        __syncthreads();
+        continue;
+      }
       const RunBitsW rw = run_bits_w(w, pw[g]);
       if (!__syncthreads_or(rw.longrun)) {  // every byte emits itself: size kTile, last run start
         const uint64_t m = __ballot(rw.starts != 0);
@@ -211,6 +232,8 @@ __device__ __forceinline__ uint64_t rle_cnt(uint64_t x, uint32_t lo, uint32_t w)
   const uint64_t q = x / 255u, r = x % 255u;
   return q * w + (uint64_t)min<uint64_t>(r > lo ? r - lo : 0u, w);
 }
+__device__ __forceinline__ uint64_t run_emitted(uint64_t x) { return rle_cnt(x, 0, 4) + rle_cnt(x, 254, 1); }
+
 __global__ void k_rle_fix(const uint32_t* __restrict__ carry, const uint32_t* __restrict__ tinfo, uint64_t tiles,
                           uint32_t* __restrict__ tsum) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -418,6 +441,26 @@ __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict_
       const uint4 q = qs[g];
       const uint32_t w[4] = {q.x, q.y, q.z, q.w};
       const uint32_t pw = pws[g];
+      if (tile_in_run(x, tile * kTile, w, pw)) {
+        // the run that started at carry[tile] covers the tile: byte i (run offset r) emits the
+        // byte when r mod 255 <= 3 and the count byte 251 when r mod 255 == 254; output
+        // positions in closed form, chunk starts (r mod 255 == 0) into the bitmap
+        const uint32_t c = x[tile * kTile];
+        const uint64_t a = tile * kTile - carry[tile], i0 = a + (uint64_t)threadIdx.x * kPer;
+        uint32_t pos = out_base[tile] + (uint32_t)(run_emitted(i0) - run_emitted(a));
+        uint32_t r = (uint32_t)(i0 % 255u);
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+          if (r <= 3u || r == 254u) {
+            if (out != nullptr) out[pos] = (uint8_t)(r <= 3u ? c : 251u);
+            if (r == 0) atomicOr(&cbits[pos >> 5], 1u << (pos & 31u));
+            pos++;
+          }
+          r = r == 254u ? 0u : r + 1u;
+        }
+        __syncthreads();
+        continue;
+      }
       const RunBitsW rw = run_bits_w(w, pw);
       if (!__syncthreads_or(rw.longrun)) {
         // every byte emits itself and starts a chunk iff it starts a run: the tile's output is

@@ -1170,6 +1170,9 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_split_pairs(const Grp* __
 // ---- tiny buckets: lane l takes rotation l % kW of bucket (64 / kW) * wave + l / kW.  Every step
 // compares the next 16 characters with the rotations of its bucket still tied with it
 // (same class, named by its first lane) and adds the smaller ones to its position.
+#ifndef BZG_TINY_SKIP
+#define BZG_TINY_SKIP 1
+#endif
 template <int kW>
 __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint32_t n_tiny, SortBufs B, SortOut O) {
   static_assert(kW == 2 || kW == 8, "lanes per bucket");
@@ -1200,6 +1203,7 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
   bool done = !act;
   uint32_t cls = act ? (lane & ~(uint32_t)(kW - 1)) : 0xffffffffu;
   uint32_t pos = 0;
+  bool pos_step = false;  // a 16-character step has been taken (pairs still live are tied)
   for (;;) {
     const uint64_t live = __ballot(!done);
     if (live == 0) break;
@@ -1235,6 +1239,42 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
         if (deep_now && el == 0 && bi < n_tiny) O.dnum[bi] = (uint32_t)__popcll(bl);
       }
       if (deep_now) break;
+    }
+    if constexpr (kW == 2 && BZG_TINY_SKIP) {
+      // a pair still tied after a step (long repeats) skips its common prefix 64 characters
+      // at a time: both members' next 64 characters, exchanged with the partner lane by DPP,
+      // compared word by word; the depth moves to the first differing word (the next 16-
+      // character step then orders the pair there)
+      bool skipping = !done && pos_step;
+      for (;;) {
+        const uint32_t q = skipping ? cyc_pos(v, d, U.len) : 0u;
+        const bool wrap = skipping && q + 68 > U.len;
+        skipping = skipping && !wrap && d < B.dwave_tiny;
+        // both members of the pair skip or neither (a member near the unit end stops both)
+        // (the exchange runs on every lane: under `skipping &&` it would read disabled lanes)
+        const int partner = __builtin_amdgcn_mov_dpp(skipping ? 1 : 0, 0xB1, 0xF, 0xF, false);
+        skipping = skipping && partner != 0;
+        if (__ballot(skipping) == 0) break;
+        uint32_t raw[17], w[16];
+        text_raw<16>(t + q, raw);
+        text_words_of<16>(t + q, raw, w);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          const uint32_t o = (uint32_t)__builtin_amdgcn_mov_dpp((int)w[j], 0xB1, 0xF, 0xF, false);  // lane ^ 1
+          diff |= (o != w[j] ? 1u : 0u) << j;
+        }
+        if (skipping) {
+          if (diff == 0) {
+            d += 64;
+          } else {
+            d += 4u * (uint32_t)__builtin_ctz(diff);
+            skipping = false;
+          }
+        }
+      }
+      pos_step = true;
+      if (__ballot(!done && d >= B.dwave_tiny)) continue;  // to the deep branch above
     }
     uint32_t k[4] = {0u, 0u, 0u, 0u};
     if (!done) text_key16(t, U.len, cyc_pos(v, d, U.len), k);
