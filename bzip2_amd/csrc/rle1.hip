@@ -310,6 +310,9 @@ __device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_
 #ifndef BZG_EMIT_WAVES
 #define BZG_EMIT_WAVES 0  // 6 or 8: VGPR spills, measured slower (+0.3 / +0.7 ms)
 #endif
+#ifndef BZG_EMIT_INRUN
+#define BZG_EMIT_INRUN 1  // tiles inside one run known from pass 1's tile info: no input read
+#endif
 #if BZG_EMIT_WAVES > 0
 #define BZG_EMIT_BOUNDS __launch_bounds__(kT, BZG_EMIT_WAVES)
 #else
@@ -409,11 +412,84 @@ __device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t ti
   }
 }
 
+// The output of an interior tile inside one run (config 4): the run that started at
+// carry[tile] covers the tile, so its output is the run's output from run offset a on: the
+// period-5 pattern c c c c 251 (4 bytes and the count byte of each 255-byte chunk), chunk
+// starts at pattern phase 0.  The tile's ~80 output bytes are written as whole words (edge
+// words, shared with the neighbouring tiles, byte by byte) and its <= 4 chunk-start words
+// likewise (edge words with atomicOr).  Words [w_lo, w_hi) of each kind by this thread.
+struct RunTile {
+  uint32_t c, t0, tot, ph0;
+  __device__ uint32_t phase(uint32_t p) const { return (ph0 + (p - t0)) % 5u; }
+};
+__device__ __forceinline__ RunTile run_tile(const uint8_t* __restrict__ x, uint64_t tile,
+                                            const uint32_t* __restrict__ carry, const uint32_t* __restrict__ out_base) {
+  const uint64_t a = tile * kTile - carry[tile];
+  const uint64_t e0 = run_emitted(a);
+  return RunTile{x[tile * kTile], out_base[tile], (uint32_t)(run_emitted(a + kTile) - e0), (uint32_t)(e0 % 5u)};
+}
+__device__ __forceinline__ void run_tile_word(const RunTile& R, uint8_t* __restrict__ out, uint32_t wi) {
+  const uint32_t b0 = wi * 4;
+  uint32_t word = 0, inside = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    const uint32_t p = b0 + k;
+    if (p >= R.t0 && p < R.t0 + R.tot) {
+      word |= (R.phase(p) == 4u ? 251u : R.c) << (8 * k);
+      inside++;
+    }
+  }
+  if (inside == 4) {
+    reinterpret_cast<uint32_t*>(out)[wi] = word;
+  } else {
+    for (uint32_t k = 0; k < 4; k++)
+      if (b0 + k >= R.t0 && b0 + k < R.t0 + R.tot) out[b0 + k] = (uint8_t)(word >> (8 * k));
+  }
+}
+__device__ __forceinline__ void run_tile_bits(const RunTile& R, uint32_t* __restrict__ cbits, uint32_t cw) {
+  const uint32_t c0 = R.t0 >> 5, c1 = (R.t0 + R.tot - 1) >> 5;
+  const uint32_t lo = max(cw * 32, R.t0), hi = min(cw * 32 + 32, R.t0 + R.tot);
+  uint32_t bits = 0;
+  for (uint32_t p = lo; p < hi; p++)
+    if (R.phase(p) == 0u) bits |= 1u << (p & 31u);
+  if (cw == c0 || cw == c1) {
+    if (bits) atomicOr(&cbits[cw], bits);
+  } else {
+    cbits[cw] = bits;
+  }
+}
+// by the 64 lanes of one wave
+__device__ __forceinline__ void emit_run_tile(const uint8_t* __restrict__ x, uint64_t tile,
+                                              const uint32_t* __restrict__ carry,
+                                              const uint32_t* __restrict__ out_base, uint8_t* __restrict__ out,
+                                              uint32_t* __restrict__ cbits, uint32_t lane) {
+  const RunTile R = run_tile(x, tile, carry, out_base);
+  const uint32_t w0 = R.t0 >> 2, w1 = (R.t0 + R.tot + 3) >> 2;
+  if (out != nullptr && lane < w1 - w0) run_tile_word(R, out, w0 + lane);
+  const uint32_t c0 = R.t0 >> 5, c1 = (R.t0 + R.tot - 1) >> 5;
+  if (lane >= 32 && lane - 32 <= c1 - c0) run_tile_bits(R, cbits, c0 + lane - 32);
+}
+
+// Interior tiles inside one run (pass 1's tile info: h = kTile, no run end, S = 0), one thread
+// each; k_emit skips them without reading their input.
+__global__ void __launch_bounds__(kT) k_emit_runs(const uint8_t* __restrict__ x, uint64_t n, uint64_t tiles,
+                                                  const uint32_t* __restrict__ carry,
+                                                  const uint32_t* __restrict__ out_base,
+                                                  const uint32_t* __restrict__ tinfo, uint8_t* __restrict__ out,
+                                                  uint32_t* __restrict__ cbits) {
+  const uint64_t tile = (uint64_t)blockIdx.x * kT + threadIdx.x;
+  if (tile >= tiles || !rle_interior(tile, n) || tinfo[tile] != (uint32_t)kTile << 16) return;
+  const RunTile R = run_tile(x, tile, carry, out_base);
+  if (out != nullptr)
+    for (uint32_t wi = R.t0 >> 2; wi < (R.t0 + R.tot + 3) >> 2; wi++) run_tile_word(R, out, wi);
+  for (uint32_t cw = R.t0 >> 5; cw <= (R.t0 + R.tot - 1) >> 5; cw++) run_tile_bits(R, cbits, cw);
+}
+
 __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict__ x, uint64_t n, uint64_t tiles,
                                              const uint32_t* __restrict__ carry,
                                              const uint32_t* __restrict__ out_base,
                                              uint8_t* __restrict__ out, uint32_t* __restrict__ cbits,
-                                             uint32_t* __restrict__ last_len1) {
+                                             uint32_t* __restrict__ last_len1, const uint32_t* __restrict__ tinfo) {
   __shared__ uint32_t sh[kT / 64];
   __shared__ uint32_t thr[kT];
   // a tile's output (<= 5/4 of its input) staged so that LDS word k is output word
@@ -423,10 +499,12 @@ __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict_
   const uint64_t t0g = (uint64_t)blockIdx.x * kRleG;
   uint4 qs[kRleG];
   uint32_t pws[kRleG];
+  bool inrun[kRleG];  // pass 1 found the tile inside one run (tinfo: h = kTile, no end, S = 0)
 #pragma unroll
   for (uint32_t g = 0; g < kRleG; g++) {
     const uint64_t base = (t0g + g) * kTile + (uint64_t)threadIdx.x * kPer;
-    if (rle_interior(t0g + g, n)) {
+    inrun[g] = BZG_EMIT_INRUN && rle_interior(t0g + g, n) && tinfo[t0g + g] == (uint32_t)kTile << 16;
+    if (rle_interior(t0g + g, n) && !inrun[g]) {
       qs[g] = *reinterpret_cast<const uint4*>(x + base);
       pws[g] = *reinterpret_cast<const uint32_t*>(x + base - 4);
     }
@@ -435,29 +513,15 @@ __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict_
   for (uint32_t g = 0; g < kRleG; g++) {
     const uint64_t tile = t0g + g;
     if (tile >= tiles) break;
+    if (inrun[g]) continue;  // k_emit_runs (uniform; no LDS touched)
     for (uint32_t i = threadIdx.x; i < kTile * 5 / 128 + 4; i += kT) cb[i] = 0;
     bool done = false;
     if (rle_interior(tile, n)) {  // SWAR run bits first
       const uint4 q = qs[g];
       const uint32_t w[4] = {q.x, q.y, q.z, q.w};
       const uint32_t pw = pws[g];
-      if (tile_in_run(x, tile * kTile, w, pw)) {
-        // the run that started at carry[tile] covers the tile: byte i (run offset r) emits the
-        // byte when r mod 255 <= 3 and the count byte 251 when r mod 255 == 254; output
-        // positions in closed form, chunk starts (r mod 255 == 0) into the bitmap
-        const uint32_t c = x[tile * kTile];
-        const uint64_t a = tile * kTile - carry[tile], i0 = a + (uint64_t)threadIdx.x * kPer;
-        uint32_t pos = out_base[tile] + (uint32_t)(run_emitted(i0) - run_emitted(a));
-        uint32_t r = (uint32_t)(i0 % 255u);
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-          if (r <= 3u || r == 254u) {
-            if (out != nullptr) out[pos] = (uint8_t)(r <= 3u ? c : 251u);
-            if (r == 0) atomicOr(&cbits[pos >> 5], 1u << (pos & 31u));
-            pos++;
-          }
-          r = r == 254u ? 0u : r + 1u;
-        }
+      if (!BZG_EMIT_INRUN && tile_in_run(x, tile * kTile, w, pw)) {
+        if (threadIdx.x < 64) emit_run_tile(x, tile, carry, out_base, out, cbits, threadIdx.x);
         __syncthreads();
         continue;
       }
@@ -722,13 +786,15 @@ __device__ __forceinline__ uint32_t xpow8(const uint32_t* __restrict__ xp2, uint
 }
 
 // Block CRC over input [binst[b], binst[b+1]).  The CRC without init / final xor is linear:
-// crc(A || B) = crc(A) * x^(8|B|) + crc(B) over GF(2).  kCrcSplit workgroups per block take
-// equal sub-ranges; in a sub-range, round r gives thread t the 16 bytes at 4096 r + 16 t
+// crc(A || B) = crc(A) * x^(8|B|) + crc(B) over GF(2).  `split` workgroups per block take
+// equal sub-ranges (8 for ordinary blocks; up to kCrcSplitMax for blocks of long runs, whose
+// input spans up to 46 MB); in a sub-range, round r gives thread t the 16 bytes at 4096 r + 16 t
 // (coalesced loads), whose CRC (slicing by 16, LDS tables) is folded into the thread's
 // accumulator as acc = acc * x^(8*4096) + crc(piece) (the multiplication by a constant is a
 // linear map: 4 LDS table lookups).  The accumulators are then shifted to their end
 // positions and xor-ed; k_crc_combine folds the sub-ranges and the init/final xor.
-constexpr uint32_t kCrcSplit = 8;
+constexpr uint32_t kCrcSplit = 8;       // sub-ranges per block, at least
+constexpr uint32_t kCrcSplitMax = 256;  // and at most (>= 512 KB each in between)
 constexpr uint32_t kCrcRound = kT * 16;
 
 __device__ __forceinline__ uint32_t crc_pow_mul(uint32_t a, const uint32_t* __restrict__ xp2, uint64_t len) {
@@ -737,7 +803,9 @@ __device__ __forceinline__ uint32_t crc_pow_mul(uint32_t a, const uint32_t* __re
 
 __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x, const uint32_t* __restrict__ binst,
                                                   const uint32_t* __restrict__ crc_table_g,
-                                                  const uint32_t* __restrict__ xp2_g, uint32_t* __restrict__ part) {
+                                                  const uint32_t* __restrict__ xp2_g, uint32_t split,
+                                                  uint32_t* __restrict__ part, const uint32_t* __restrict__ tinfo,
+                                                  uint64_t n) {
   __shared__ uint32_t tab[16][256];  // tab[k][b] = crc of byte b followed by k zero bytes
   __shared__ uint32_t mul[4][256];   // byte k of a (from the top) times x^(8*4096)
   __shared__ uint32_t xp2[48];
@@ -761,7 +829,7 @@ __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x,
     for (int k = 0; k < 4; k++) mul[k][threadIdx.x] = gf_mul(threadIdx.x << (8 * (3 - k)), xr);
   }
   const uint32_t lo = binst[b], hi = binst[b + 1];
-  const uint32_t per = ceil_div(hi - lo, kCrcSplit);
+  const uint32_t per = ceil_div(hi - lo, split);
   const uint32_t s0 = min(hi, lo + w * per), s1 = min(hi, s0 + per);
   const uint32_t len = s1 - s0, R = len / kCrcRound, T = len - R * kCrcRound;
   __syncthreads();
@@ -783,6 +851,16 @@ __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x,
   uint32_t acc = 0;
   const uint8_t* px = x + s0 + 16 * threadIdx.x;
   uint32_t r = 0;
+  // a sub-range inside one run (its tiles all inside one run by pass 1's tile info, config 4):
+  // every round's piece is 16 copies of the run's byte, so the rounds fold without loads
+  bool in_run = len > 0;
+  for (uint32_t t = s0 / kTile + threadIdx.x; in_run && t <= (s1 - 1) / kTile; t += kT)
+    in_run = rle_interior(t, n) && tinfo[t] == (uint32_t)kTile << 16;
+  if (!__syncthreads_or(!in_run) && R) {
+    const uint32_t pat = x[s0] * 0x01010101u;
+    const uint32_t v = crc16q(make_uint4(pat, pat, pat, pat));
+    for (; r < R; r++) acc = fold(acc, v);
+  }
   // 4 rounds' loads in flight before their folds
   for (; r + 4 <= R; r += 4) {
     uint4 q[4];
@@ -811,27 +889,27 @@ __global__ void __launch_bounds__(kT) k_block_crc(const uint8_t* __restrict__ x,
   for (int o = 1; o < 64; o <<= 1) res ^= (uint32_t)__shfl_xor((int)res, o, 64);
   if (__lane_id() == 0) red[threadIdx.x >> 6] = res;
   __syncthreads();
-  if (threadIdx.x == 0) part[b * kCrcSplit + w] = red[0] ^ red[1] ^ red[2] ^ red[3];
+  if (threadIdx.x == 0) part[b * split + w] = red[0] ^ red[1] ^ red[2] ^ red[3];
 }
 
-// One wave per block: lane w < kCrcSplit shifts sub-range w's CRC to the block end, lane
-// kCrcSplit shifts the initial register through the whole block; the lanes' terms are xor-ed.
+// One wave per block: lane l shifts the CRCs of sub-ranges l, l + 64, ... to the block end,
+// lane 63 also the initial register through the whole block; the lanes' terms are xor-ed.
 __global__ void __launch_bounds__(64) k_crc_combine(const uint32_t* __restrict__ binst, const uint32_t* __restrict__ part,
-                                                    const uint32_t* __restrict__ xp2, uint32_t nb, uint32_t* __restrict__ bcrc) {
-  const uint32_t b = blockIdx.x, w = threadIdx.x;
+                                                    const uint32_t* __restrict__ xp2, uint32_t nb, uint32_t split,
+                                                    uint32_t* __restrict__ bcrc) {
+  const uint32_t b = blockIdx.x, l = threadIdx.x;
   if (b >= nb) return;
   const uint32_t lo = binst[b], hi = binst[b + 1];
-  const uint32_t per = ceil_div(hi - lo, kCrcSplit);
+  const uint32_t per = ceil_div(hi - lo, split);
   uint32_t c = 0;
-  if (w < kCrcSplit) {
+  for (uint32_t w = l; w < split; w += 64) {
     const uint32_t e = min(hi, min(hi, lo + w * per) + per);
-    c = crc_pow_mul(part[b * kCrcSplit + w], xp2, hi - e);
-  } else if (w == kCrcSplit) {
-    c = crc_pow_mul(0xffffffffu, xp2, hi - lo);  // the initial register, shifted through
+    c ^= crc_pow_mul(part[b * split + w], xp2, hi - e);
   }
+  if (l == 63) c ^= crc_pow_mul(0xffffffffu, xp2, hi - lo);  // the initial register, shifted through
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
-  if (w == 0) bcrc[b] = ~c;
+  for (int o = 1; o < 64; o <<= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
+  if (l == 0) bcrc[b] = ~c;
 }
 
 // In-use bitmap (8 words) per block; blocks are boff[b]..boff[b+1] of blk.  kInUseSplit
@@ -1021,8 +1099,12 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
   HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
-  k_emit<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tsum, blk, cbits, mtot + 8);
+  k_emit<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tsum, blk, cbits, mtot + 8, tinfo);
   HIP_OK(hipGetLastError());
+  if (BZG_EMIT_INRUN) {
+    k_emit_runs<<<ceil_div64(tiles, kT), kT, 0, st>>>(d_in, n, tiles, tmax, tsum, tinfo, blk, cbits);
+    HIP_OK(hipGetLastError());
+  }
 
   // the cut walk of k_segment_fill from fill 0 (cuts into boff[1..]), then boff/nblocks
   k_segment_fill<<<1, 64, 0, st>>>(cbits, mtot, nblock_max, 0u, (final_batch && tail_merge) ? 1 : 0, mtot + 8,
@@ -1064,10 +1146,13 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
 
   const int B = (int)res.nblocks;
   uint32_t* bcrc = ws.u32("bcrc", max_blocks + 2);
-  uint32_t* cpart = ws.u32("crc_part", (size_t)(max_blocks + 2) * kCrcSplit);
-  k_block_crc<<<dim3(kCrcSplit, B), kT, 0, st>>>(d_in, binst, ws.crc_table(), ws.xpow2_table(), cpart);
+  // sub-ranges per block from the mean block input (long runs: a block spans up to 46 MB)
+  const uint32_t split = (uint32_t)std::min<uint64_t>(
+      kCrcSplitMax, std::max<uint64_t>(kCrcSplit, ceil_div64(res.consumed, (uint64_t)B << 19)));
+  uint32_t* cpart = ws.u32("crc_part", (size_t)(max_blocks + 2) * kCrcSplitMax);
+  k_block_crc<<<dim3(split, B), kT, 0, st>>>(d_in, binst, ws.crc_table(), ws.xpow2_table(), split, cpart, tinfo, n);
   HIP_OK(hipGetLastError());
-  k_crc_combine<<<B, 64, 0, st>>>(binst, cpart, ws.xpow2_table(), B, bcrc);
+  k_crc_combine<<<B, 64, 0, st>>>(binst, cpart, ws.xpow2_table(), B, split, bcrc);
   HIP_OK(hipGetLastError());
   res.bcrc = bcrc;
   res.blk = blk;
@@ -1097,8 +1182,12 @@ void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t s
   HIP_OK(hipGetLastError());
   scan_u32(ScanOp::Sum, true, tsum, tsum, tiles, mtot, scratch, st);
   HIP_OK(hipMemsetAsync(cbits, 0, (mcap / 32 + 64) * 4, st));
-  k_emit<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tsum, nullptr, cbits, mtot + 8);
+  k_emit<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tsum, nullptr, cbits, mtot + 8, tinfo);
   HIP_OK(hipGetLastError());
+  if (BZG_EMIT_INRUN) {
+    k_emit_runs<<<ceil_div64(tiles, kT), kT, 0, st>>>(d_in, n, tiles, tmax, tsum, tinfo, nullptr, cbits);
+    HIP_OK(hipGetLastError());
+  }
 }
 
 void seg_walk_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, uint32_t fill_in,
