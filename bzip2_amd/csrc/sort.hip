@@ -1620,6 +1620,9 @@ __device__ __forceinline__ bool compact_sort(BsortKey (&K)[kPer], const bool (&d
 #ifndef BZG_S2_SKIP
 #define BZG_S2_SKIP 1
 #endif
+#ifndef BZG_S2_EARLY
+#define BZG_S2_EARLY 2  // emitting classes: rounds after which runs of at most two are emitted (0: never)
+#endif
 template <int kPer>
 __device__ __forceinline__ uint32_t common_depth(const uint8_t* t, uint32_t len, const uint32_t (&v)[kPer],
                                                  const bool (&live)[kPer], uint32_t depth, uint32_t limit) {
@@ -2088,7 +2091,18 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
     if constexpr (kCompact) {
       if (depth < B.dwave && bsort_compact_tail<kPer>(B, O, g, U, depth, K, done, tn, rsn, Lv[w], Lc[w], SC[w])) break;
     }
-    if (++round >= kRounds || depth >= B.dwave) {
+    if constexpr (kSeg == 64 || BZG_OETS_SEG) {  // longest tied run (next round's network; early emission)
+      uint32_t ml = 0;
+#pragma unroll
+      for (int r = 0; r < kPer; r++)
+        if (key_valid(K[r]) && !done[r] && !tn[r]) ml = max(ml, sl * kPer + r - rsn[r] + 1);
+      maxrun = (uint32_t)__builtin_amdgcn_readlane((int)seg_incl_max<64>(ml), 63);
+    }
+    // only pairs still tied after BZG_S2_EARLY rounds (long repeats: the pairs of a copied
+    // passage stay tied round after round): emitted now, as the pair lists' 64-character skip
+    // (k_tiny<2>) resolves or deepens them far cheaper than further rounds of the whole network
+    const bool early = kEmit && BZG_S2_EARLY > 0 && round + 1 >= BZG_S2_EARLY && maxrun <= 2;
+    if (++round >= kRounds || depth >= B.dwave || early) {
       if constexpr (kEmit) {
         static_assert(kSeg == 64, "one group per wave");
         {
@@ -2119,13 +2133,6 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         bsort_tail<kSeg, kPer, kBatch>(B, O, g, bi, U, depth, K, done, rsn, Lv[w], Lk[w], TK[w], TC[w]);
       }
       break;
-    }
-    if constexpr (kSeg == 64 || BZG_OETS_SEG) {
-      uint32_t ml = 0;
-#pragma unroll
-      for (int r = 0; r < kPer; r++)
-        if (key_valid(K[r]) && !done[r] && !tn[r]) ml = max(ml, sl * kPer + r - rsn[r] + 1);
-      maxrun = (uint32_t)__builtin_amdgcn_readlane((int)seg_incl_max<64>(ml), 63);
     }
     // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
 #pragma unroll
