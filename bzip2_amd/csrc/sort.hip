@@ -1173,6 +1173,9 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_split_pairs(const Grp* __
 #ifndef BZG_TINY_SKIP
 #define BZG_TINY_SKIP 1
 #endif
+#ifndef BZG_TINY_SKIP8
+#define BZG_TINY_SKIP8 1
+#endif
 template <int kW>
 __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint32_t n_tiny, SortBufs B, SortOut O) {
   static_assert(kW == 2 || kW == 8, "lanes per bucket");
@@ -1269,6 +1272,52 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
             d += 64;
           } else {
             d += 4u * (uint32_t)__builtin_ctz(diff);
+            skipping = false;
+          }
+        }
+      }
+      pos_step = true;
+      if (__ballot(!done && d >= B.dwave_tiny)) continue;  // to the deep branch above
+    }
+    if constexpr (kW == 8 && BZG_TINY_SKIP8) {
+      // a bucket whose live members are all still tied with their classes after a step skips
+      // the common prefix of all of them, 64 characters at a time: every live member compares
+      // its next 64 characters with its class's first member (ds_bpermute), and the bucket
+      // advances to the first word where any member differs.  The depth stays one per bucket
+      // (its lanes take the deep branch together), so every DPP source stays active.
+      auto b_or = [](uint32_t x) {
+        x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad xor 1
+        x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad xor 2
+        return x | g8_mirror(x);                                                 // other quad
+      };
+      auto b_min = [](uint32_t x) {
+        x = min(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false));
+        x = min(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false));
+        return min(x, g8_mirror(x));
+      };
+      bool skipping = pos_step;
+      for (;;) {
+        const bool live = !done;
+        const uint32_t q = live ? cyc_pos(v, d, U.len) : 0u;
+        const uint32_t f = b_or((live ? 1u : 0u) | ((live && q + 68 > U.len) ? 2u : 0u));
+        skipping = skipping && f == 1u && d < B.dwave_tiny;  // some member live, none wraps
+        if (__ballot(skipping) == 0) break;
+        uint32_t raw[17], w[16];
+        text_raw<16>(t + q, raw);
+        text_words_of<16>(t + q, raw, w);
+        const int src = (int)(live ? cls : lane);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          const uint32_t o = (uint32_t)__shfl((int)w[j], src, 64);  // the class's first member
+          diff |= (o != w[j] ? 1u : 0u) << j;
+        }
+        const uint32_t fd = b_min(diff ? (uint32_t)__builtin_ctz(diff) : 16u);
+        if (skipping) {
+          if (fd == 16u) {
+            d += 64;
+          } else {
+            d += 4u * fd;
             skipping = false;
           }
         }
