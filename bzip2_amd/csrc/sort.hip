@@ -39,7 +39,7 @@ constexpr int kT = 256;
 constexpr uint32_t kBig = BZG_BIG;    // buckets larger than this are split by S1 byte passes
 static_assert(kBig == 128 || kBig == 256, "S2 classes cover up to 128 or 256 rotations");
 #ifndef BZG_DTILE
-#define BZG_DTILE 2048
+#define BZG_DTILE 4096
 #endif
 constexpr uint32_t kDTile = BZG_DTILE;  // rotations per workgroup in an S1 pass
 constexpr uint32_t kPerT = kDTile / kT;
