@@ -143,7 +143,7 @@ __device__ __forceinline__ int n_groups(uint32_t nmtf) {  // compress.c:266-270
 //   k_cf (final mode): payload bits of every group under the final tables;
 //   k_final: canonical codes, selector MTF, table and header bit counts.
 #ifndef BZG_CF_SLICES
-#define BZG_CF_SLICES 8
+#define BZG_CF_SLICES 2
 #endif
 constexpr uint32_t kCfSlices = BZG_CF_SLICES;  // workgroups per block in k_cf
 

@@ -17,6 +17,6 @@ for mode in one two; do
       timeout -s KILL 240 rocprofv3 --pmc $set --output-format csv -d $O/${mode}$i -o run -- python bench.py --steps 1 --warmup 0 --no-cpu --no-h2h --no-extra > $O/${mode}$i.log 2>&1 || { echo "pass failed"; tail -20 $O/${mode}$i.log; exit 1; }
     fi
   done
-  python tools/sq_summary.py $O/${mode}1/run_counter_collection.csv 40 --tmpl > $O/sq_${mode}.txt
+  python tools/sq_summary.py $O/${mode}1/run_counter_collection.csv 40 --tmpl --lds $O/${mode}2/run_counter_collection.csv > $O/sq_${mode}.txt
 done
 echo "done $(date)"
