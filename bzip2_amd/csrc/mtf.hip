@@ -551,6 +551,15 @@ __global__ void __launch_bounds__(kT) k_mtf_pick(const uint32_t* __restrict__ bo
 // four chunks in lockstep.  Ranks are staged in LDS, then stored as 16-byte words; the
 // zero-run summary is read from them afterwards.
 constexpr uint32_t kRowChunks = kT / 16;
+#ifndef BZG_MTF_TS
+#define BZG_MTF_TS 1  // k_mtf_row ranks from occurrence times (0: the shifting list in the row's registers)
+#endif
+// v_ffbl_b32: lowest set bit, ~0 for 0 (the hardware result; __builtin_ctz leaves 0 undefined)
+__device__ __forceinline__ uint32_t ffbl_hw(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 __global__ void __launch_bounds__(kT) k_mtf_row(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                                 const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
                                                 const uint32_t* __restrict__ hi_list, const uint32_t* __restrict__ n_hi,
@@ -560,6 +569,10 @@ __global__ void __launch_bounds__(kT) k_mtf_row(const uint8_t* __restrict__ L, c
   __shared__ uint32_t sym[kRowChunks][kChunk / 4 + 4];  // the chunk's BWT bytes
   __shared__ uint32_t rk[kRowChunks][kChunk / 4 + 4];   // its ranks
   __shared__ uint32_t part[kRowChunks][16][4];      // zero-run summaries of the lanes' slices
+#if BZG_MTF_TS
+  __shared__ uint16_t last[kRowChunks][256];  // step of each symbol's last occurrence (~0: none yet)
+  __shared__ uint8_t p0[kRowChunks][256];     // its position in the chunk's initial list
+#endif
   const uint32_t nh = *n_hi;
   if (blockIdx.x * kRowChunks >= nh) return;
   const uint32_t t = threadIdx.x, lane = __lane_id(), row = lane >> 4, rl = lane & 15;
@@ -573,7 +586,6 @@ __global__ void __launch_bounds__(kT) k_mtf_row(const uint8_t* __restrict__ L, c
     len = min(boff[b + 1], lo + kChunk) - lo;
     g = cbase[b] + c;
   }
-  uint8_t* sb = reinterpret_cast<uint8_t*>(sym[ci]);
   for (uint32_t j = rl; j < kChunk / 4; j += 16) {
     uint32_t w = 0;
     for (uint32_t k = 0; k < 4; k++)
@@ -591,43 +603,142 @@ __global__ void __launch_bounds__(kT) k_mtf_row(const uint8_t* __restrict__ L, c
 #pragma unroll
   for (int o = 16; o < 64; o <<= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
   uint8_t* rb = reinterpret_cast<uint8_t*>(rk[ci]);
-  const uint32_t rowshift = 16 * row;
-  for (uint32_t j = 0; j < wl; j++) {
-    const bool act = j < len;
-    const uint32_t c = sb[j];  // one address per row: broadcast
-    const uint32_t pat = c * 0x01010101u;
-    const uint32_t x0 = W0 ^ pat, x1 = W1 ^ pat, x2 = W2 ^ pat, x3 = W3 ^ pat;
-    const uint32_t z0 = (x0 - 0x01010101u) & ~x0 & 0x80808080u;
-    const uint32_t z1 = (x1 - 0x01010101u) & ~x1 & 0x80808080u;
-    const uint32_t z2 = (x2 - 0x01010101u) & ~x2 & 0x80808080u;
-    const uint32_t z3 = (x3 - 0x01010101u) & ~x3 & 0x80808080u;
-    const uint32_t local = z0 ? (__builtin_ctz(z0) >> 3)
-                       : z1 ? 4 + (__builtin_ctz(z1) >> 3)
-                       : z2 ? 8 + (__builtin_ctz(z2) >> 3)
-                       : z3 ? 12 + (__builtin_ctz(z3) >> 3) : 16u;
-    const uint64_t m = __ballot(act && local < 16);
-    const uint32_t rowbits = (uint32_t)(m >> rowshift) & 0xffffu;
-    const uint32_t lane0 = rowbits ? (uint32_t)__builtin_ctz(rowbits) : 16u;
-    // bytes of this lane that shift: all before the match, up to the match in its lane
-    const uint32_t nshift = !act ? 0u : rl < lane0 ? 16u : rl == lane0 ? local + 1 : 0u;
-    if (act && rl == lane0) rb[j] = (uint8_t)(16 * rl + local);
-    // the top byte of the previous lane (the symbol itself into lane 0 of the row)
-    uint32_t cin = (uint32_t)__builtin_amdgcn_mov_dpp((int)(W3 >> 24), 0x111, 0xF, 0xF, false);  // row_shr:1
-    if (rl == 0) cin = c;
-    const uint32_t s0 = (W0 << 8) | cin;
-    const uint32_t s1 = __builtin_amdgcn_alignbyte(W1, W0, 3);
-    const uint32_t s2 = __builtin_amdgcn_alignbyte(W2, W1, 3);
-    const uint32_t s3 = __builtin_amdgcn_alignbyte(W3, W2, 3);
-    auto msk = [](uint32_t n, uint32_t k) {  // bytes [0, n - 4k) of word k
-      const uint32_t b = n > 4 * k ? min(n - 4 * k, 4u) : 0u;
-      return (uint32_t)((1ull << (8 * b)) - 1ull);
-    };
-    const uint32_t m0 = msk(nshift, 0), m1 = msk(nshift, 1), m2 = msk(nshift, 2), m3 = msk(nshift, 3);
-    W0 = (s0 & m0) | (W0 & ~m0);
-    W1 = (s1 & m1) | (W1 & ~m1);
-    W2 = (s2 & m2) | (W2 & ~m2);
-    W3 = (s3 & m3) | (W3 & ~m3);
+#if BZG_MTF_TS
+  // Ranks from occurrence times instead of a shifting list.  A symbol seen earlier in the
+  // chunk has rank = the number of distinct symbols used since its last occurrence = the
+  // number of last-occurrence markers between the two steps (a 1024-bit marker map, 64 steps
+  // per lane).  A first occurrence has rank m + p - #{symbols already used with p0 < p} (m
+  // used so far, p its initial-list position: the used symbols lead, the untouched list
+  // follows; a 256-bit map of used positions, 16 per lane).  Either count is a popcount per
+  // lane summed over the row's 16 lanes by DPP, so a step costs the same at any rank.
+  {
+    // p0 = smallest position of each byte in the initial list (past nInUse the list is
+    // unspecified), built with atomicMin in the rank staging words, which are free until the loop
+    for (uint32_t k = rl; k < 256; k += 16) rk[ci][k] = 0xffu;
+    __syncthreads();
+    const uint32_t wv[4] = {W0, W1, W2, W3};
+    if (valid) {
+#pragma unroll
+      for (uint32_t k = 0; k < 16; k++) atomicMin(&rk[ci][(wv[k >> 2] >> (8 * (k & 3))) & 0xffu], 16 * rl + k);
+    }
+    __syncthreads();
+    for (uint32_t k = rl; k < 256; k += 16) {
+      p0[ci][k] = (uint8_t)rk[ci][k];
+      last[ci][k] = 0xffffu;
+    }
+    __syncthreads();
   }
+  {
+    uint64_t M = 0;    // markers of steps 64 rl .. 64 rl + 63
+    uint32_t S = 0;    // used initial positions 16 rl .. 16 rl + 15
+    uint32_t m = 0;    // symbols used so far (row-uniform)
+    const int r64 = 64 * (int)rl, r16 = 16 * (int)rl;
+    auto rsum = [](uint32_t x) {  // inclusive sum over the row; lane 15 of the row holds the total
+      x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+      x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+      x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+      x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+      return x;
+    };
+    auto low64 = [](int n) {  // bits [0, n), n in [0, 64]
+      return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+    };
+    const uint32_t* sw = sym[ci];
+    uint16_t* ls = last[ci];
+    const uint8_t* pz = p0[ci];
+    for (uint32_t j0 = 0; j0 < wl; j0 += 4) {
+      // the group's symbols, their last occurrences before the group and their initial positions
+      const uint32_t cur = sw[j0 >> 2];
+      uint32_t cs[4], tt[4], pp[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        cs[u] = (cur >> (8 * u)) & 0xffu;
+        tt[u] = ls[cs[u]];
+        pp[u] = pz[cs[u]];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t j = j0 + u;
+        if (j >= wl) break;  // (uniform)
+        const bool act = j < len;
+        const uint32_t c = cs[u], p = pp[u];
+        uint32_t tl = tt[u];
+#pragma unroll
+        for (uint32_t v = 0; v < u; v++)
+          if (cs[v] == c) tl = j0 + v;  // an occurrence earlier in this group (latest wins)
+        const bool first = tl == 0xffffu;
+        const int lo = min(max((int)tl + 1 - r64, 0), 64), hi = min(max((int)j - r64, 0), 64);
+        const uint32_t cm = (uint32_t)__builtin_popcountll(M & low64(hi) & ~low64(lo));
+        const uint32_t cf = (uint32_t)__builtin_popcount(S & ((1u << min(max((int)p - r16, 0), 16)) - 1u));
+        const uint32_t tot = rsum(first ? cf : cm);
+        if (act && rl == 15) {
+          rb[j] = (uint8_t)(first ? m + p - tot : tot);
+          ls[c] = (uint16_t)j;
+        }
+        if (act) {
+          if (!first && (tl >> 6) == rl) M &= ~(1ull << (tl & 63u));
+          if ((j >> 6) == rl) M |= 1ull << (j & 63u);
+          if (first && (p >> 4) == rl) S |= 1u << (p & 15u);
+          m += first ? 1u : 0u;
+        }
+      }
+    }
+  }
+#else
+  const uint32_t rowshift = 16 * row;
+  // one step per symbol, branch-free; the symbols of 4 steps come in one LDS word, read a
+  // group ahead (the per-step byte read left its latency in every step)
+  const uint32_t* sw = sym[ci];
+  uint32_t nxt = sw[0];
+  for (uint32_t j0 = 0; j0 < wl; j0 += 4) {
+    const uint32_t cur = nxt;
+    nxt = sw[(j0 >> 2) + 1];  // (the row is padded by 4 words)
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t j = j0 + u;
+      if (j >= wl) break;  // (uniform)
+      const bool act = j < len;
+      const uint32_t pat = __builtin_amdgcn_perm(0u, cur, u * 0x01010101u);  // byte u of cur, 4 times
+      const uint32_t c = pat & 0xffu;
+      // byte of c in each word: the lowest flagged byte of the zero-byte test (the list holds
+      // c once, so at most one word has a true zero, and false flags only sit above it);
+      // v_ffbl gives ~0 for a word without one, and (~0 >> 3) + 4k stays far above 16
+      const uint32_t x0 = W0 ^ pat, x1 = W1 ^ pat, x2 = W2 ^ pat, x3 = W3 ^ pat;
+      const uint32_t z0 = (x0 - 0x01010101u) & ~x0 & 0x80808080u;
+      const uint32_t z1 = (x1 - 0x01010101u) & ~x1 & 0x80808080u;
+      const uint32_t z2 = (x2 - 0x01010101u) & ~x2 & 0x80808080u;
+      const uint32_t z3 = (x3 - 0x01010101u) & ~x3 & 0x80808080u;
+      const uint32_t a0 = ffbl_hw(z0) >> 3, a1 = (ffbl_hw(z1) >> 3) + 4u, a2 = (ffbl_hw(z2) >> 3) + 8u,
+                     a3 = (ffbl_hw(z3) >> 3) + 12u;
+      const uint32_t local = min(min(min(a0, a1), min(a2, a3)), 16u);
+      const uint64_t m = __ballot(act && local < 16);
+      const uint32_t rowbits = (uint32_t)(m >> rowshift) & 0xffffu;
+      const uint32_t lane0 = (uint32_t)__builtin_ctz(rowbits | 0x10000u);
+      // bytes of this lane that shift: all before the match, up to the match in its lane
+      const uint32_t nshift = !act ? 0u : rl < lane0 ? 16u : rl == lane0 ? local + 1 : 0u;
+      if (act && rl == lane0) rb[j] = (uint8_t)(16 * rl + local);
+      // the top byte of the previous lane (the symbol itself into lane 0 of the row)
+      uint32_t cin = (uint32_t)__builtin_amdgcn_mov_dpp((int)(W3 >> 24), 0x111, 0xF, 0xF, false);  // row_shr:1
+      if (rl == 0) cin = c;
+      const uint32_t s0 = (W0 << 8) | cin;
+      const uint32_t s1 = __builtin_amdgcn_alignbyte(W1, W0, 3);
+      const uint32_t s2 = __builtin_amdgcn_alignbyte(W2, W1, 3);
+      const uint32_t s3 = __builtin_amdgcn_alignbyte(W3, W2, 3);
+      // bytes [0, nshift - 4k) of word k: 0xFFFFFFFF >> (32 - 8 clamp(nshift - 4k, 0, 4)) as a
+      // 64-bit shift (a shift by 32 gives 0)
+      const int q = 32 - 8 * (int)nshift;
+      auto msk = [&](int k) {
+        const int sh = min(max(q + 32 * k, 0), 32);
+        return (uint32_t)(0xFFFFFFFFull >> sh);
+      };
+      const uint32_t m0 = msk(0), m1 = msk(1), m2 = msk(2), m3 = msk(3);
+      W0 = (s0 & m0) | (W0 & ~m0);
+      W1 = (s1 & m1) | (W1 & ~m1);
+      W2 = (s2 & m2) | (W2 & ~m2);
+      W3 = (s3 & m3) | (W3 & ~m3);
+    }
+  }
+#endif
   __syncthreads();
   // ranks out (16-byte words) and the zero-run summary: lane rl takes ranks [64 rl, 64 rl + 64)
   if (valid) {
