@@ -551,6 +551,9 @@ __global__ void __launch_bounds__(kT) k_mtf_pick(const uint32_t* __restrict__ bo
 // four chunks in lockstep.  Ranks are staged in LDS, then stored as 16-byte words; the
 // zero-run summary is read from them afterwards.
 constexpr uint32_t kRowChunks = kT / 16;
+#ifndef BZG_MTF_Q
+#define BZG_MTF_Q 1  // high-entropy chunks on a quad of lanes each (k_mtf_q); 0: a row of 16 (k_mtf_row)
+#endif
 #ifndef BZG_MTF_TS
 #define BZG_MTF_TS 1  // k_mtf_row ranks from occurrence times (0: the shifting list in the row's registers)
 #endif
@@ -856,6 +859,143 @@ __global__ void __launch_bounds__(64) k_rle2_plan(const uint32_t* __restrict__ b
 // The zero run that ends at a lane's first nonzero rank started in an earlier lane (or chunk:
 // zin) -- its length comes from a segmented scan over the lanes.  Each lane writes its
 // symbols contiguously at an offset from a wave scan of the per-lane symbol counts.
+// MTF of one high-entropy chunk by a quad of lanes (16 chunks per wave), ranks from occurrence
+// times as in k_mtf_row's BZG_MTF_TS loop, with the per-chunk state small enough for 64
+// chunks per workgroup: lane q keeps the last-occurrence markers of steps 256 q .. 256 q + 255
+// (four 64-bit words and their counts) and the used initial-list positions 64 q .. 64 q + 63.
+// With m symbols used so far, a symbol last seen at step t has rank m - #{markers <= t}; a
+// first occurrence at initial position p has rank m + p - #{used positions < p}.  The symbols
+// stream from the BWT column 16 at a time (every lane of the quad loads the same 16 bytes, one
+// group ahead); the ranks of 16 steps leave as one 16-byte store; the zero-run summary is kept
+// on the way.  Per-chunk LDS: last occurrence (u16) and initial position (u8) of every byte.
+constexpr uint32_t kQChunks = kT / 4;
+__global__ void __launch_bounds__(kT) k_mtf_q(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
+                                              const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
+                                              const uint32_t* __restrict__ hi_list, const uint32_t* __restrict__ n_hi,
+                                              uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
+                                              uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
+  __shared__ uint32_t lastw[kQChunks][128];  // u16 per byte
+  __shared__ uint32_t p0w[kQChunks][64];     // u8 per byte
+  const uint32_t nh = *n_hi;
+  if (blockIdx.x * kQChunks >= nh) return;
+  const uint32_t q = threadIdx.x & 3u, ci = threadIdx.x >> 2;
+  const uint32_t i = blockIdx.x * kQChunks + ci;
+  const bool valid = i < nh;
+  uint32_t len = 0, lo = 0, g = 0;
+  if (valid) {
+    const uint32_t e = hi_list[i], b = e >> 11, c = e & 2047u;
+    lo = boff[b] + c * kChunk;
+    len = min(boff[b + 1], lo + kChunk) - lo;
+    g = cbase[b] + c;
+  }
+  uint16_t* last = reinterpret_cast<uint16_t*>(lastw[ci]);
+  uint8_t* p0 = reinterpret_cast<uint8_t*>(p0w[ci]);
+  for (uint32_t k = q; k < 128; k += 4) lastw[ci][k] = 0xffffffffu;
+  // initial positions, smallest first: lane r writes its 64 positions high to low in round
+  // 3 - r, so the lowest lane writes last (past nInUse the list is unspecified)
+  {
+    uint32_t w[16];
+    const uint4* src = reinterpret_cast<const uint4*>(init + (size_t)(valid ? g : 0u) * 64 + 16 * q);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint4 v = src[k];
+      w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
+    }
+    for (uint32_t r = 0; r < 4; r++) {
+      if (q == 3 - r) {
+#pragma unroll
+        for (int k = 63; k >= 0; k--) p0[(w[k >> 2] >> (8 * (k & 3))) & 0xffu] = (uint8_t)(64 * q + k);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  __syncthreads();
+  uint32_t wl = len;  // the wave runs to its longest chunk
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
+  uint64_t M[4] = {0, 0, 0, 0};   // markers of steps 256 q + 64 w + b
+  uint32_t nm[4] = {0, 0, 0, 0};  // their counts per word
+  uint64_t S = 0;                 // used initial positions 64 q + b
+  uint32_t ns = 0;                // their count
+  uint32_t m = 0;                 // symbols used so far
+  uint32_t ld = 0, z = 0, cnt = 0;
+  bool seen = false;
+  auto quad_sum = [](uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    return x;
+  };
+  auto low64 = [](uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); };
+  const uint8_t* col = L + lo;
+  uint4 nxt;
+  __builtin_memcpy(&nxt, col, 16);  // (the column is padded)
+  uint8_t* rout = ranks + (size_t)(valid ? g : 0u) * kChunk;
+  // (steps past wl are inactive like those past len: the 16 steps of a group unroll to
+  // straight-line code, all per-lane choices as selects)
+  for (uint32_t j16 = 0; j16 < wl; j16 += 16) {
+    const uint4 cur = nxt;
+    if (j16 + 16 < wl) __builtin_memcpy(&nxt, col + j16 + 16, 16);
+    const uint32_t cw[4] = {cur.x, cur.y, cur.z, cur.w};
+    uint32_t racc[4] = {0, 0, 0, 0};
+    const uint32_t setl = j16 >> 8, setw = (j16 >> 6) & 3u;  // the group's steps share lane and word
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) {
+      const uint32_t j = j16 + u;
+      const bool act = j < len;
+      const uint32_t c = (cw[u >> 2] >> (8 * (u & 3))) & 0xffu;
+      const uint32_t t = last[c], p = p0[c];
+      const bool first = t == 0xffffu;
+      // this lane's part of #{markers <= t} and of #{used positions < p}
+      const uint32_t tl = t >> 8, tw = (t >> 6) & 3u, tb = t & 63u;
+      uint64_t mt = M[0];
+      mt = tw == 1 ? M[1] : mt;
+      mt = tw == 2 ? M[2] : mt;
+      mt = tw == 3 ? M[3] : mt;
+      const uint32_t below = (tw > 0 ? nm[0] : 0u) + (tw > 1 ? nm[1] : 0u) + (tw > 2 ? nm[2] : 0u);
+      const uint32_t xin = below + (uint32_t)__builtin_popcountll(mt & (~0ull >> (63u - tb)));  // bits 0..tb
+      const uint32_t nall = nm[0] + nm[1] + nm[2] + nm[3];
+      const uint32_t x = q < tl ? nall : (q == tl ? xin : 0u);
+      const uint32_t pl = p >> 6, pb = p & 63u;
+      const uint32_t yin = (uint32_t)__builtin_popcountll(S & ((1ull << pb) - 1ull));
+      const uint32_t y = q < pl ? ns : (q == pl ? yin : 0u);
+      const uint32_t tot = quad_sum(first ? y : x);
+      const uint32_t rank = first ? m + p - tot : m - tot;
+      racc[u >> 2] |= (act ? rank : 0u) << (8 * (u & 3));
+      if (act && q == 0) last[c] = (uint16_t)j;
+      // the marker moves from step t to step j
+      const uint64_t bt = 1ull << tb, bj = 1ull << ((j16 & 63u) + u);
+      const bool clr = act && !first && q == tl, set = act && q == setl;
+#pragma unroll
+      for (uint32_t w = 0; w < 4; w++) {
+        const bool cw_ = clr && tw == w, sw_ = set && setw == w;
+        M[w] = cw_ ? (M[w] & ~bt) : M[w];
+        M[w] = sw_ ? (M[w] | bj) : M[w];
+        nm[w] = nm[w] - (cw_ ? 1u : 0u) + (sw_ ? 1u : 0u);
+      }
+      const bool fs = act && first && q == pl;
+      S = fs ? (S | (1ull << pb)) : S;
+      ns += fs ? 1u : 0u;
+      m += (act && first) ? 1u : 0u;
+      // zero-run summary (the walk of k_mtf_run)
+      const bool zr = rank == 0;
+      const uint32_t ns_ = seen ? nsym(z) : 0u;
+      const uint32_t z2 = zr ? z + 1 : 0u;
+      const uint32_t c2 = zr ? cnt : cnt + ns_ + 1u;
+      const uint32_t l2 = (!zr && !seen) ? z : ld;
+      z = act ? z2 : z;
+      cnt = act ? c2 : cnt;
+      ld = act ? l2 : ld;
+      seen = seen || (act && !zr);
+    }
+    if (valid && q == 0 && j16 < len) *reinterpret_cast<uint4*>(rout + j16) = make_uint4(racc[0], racc[1], racc[2], racc[3]);
+  }
+  if (valid && q == 0) {
+    lead[g] = seen ? ld : 0xffffffffu;
+    trail[g] = z;
+    inner[g] = cnt;
+  }
+}
+
 constexpr int kEW = 16;  // chunks (waves) per workgroup: one frequency flush per 16 chunks
 __global__ void __launch_bounds__(64 * kEW) k_rle2_emit(const uint8_t* __restrict__ ranks,
                                                         const uint32_t* __restrict__ boff,
@@ -1052,8 +1192,12 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
   k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, siglen, init, frank, ranks, lead, trail, inner);
   HIP_OK(hipGetLastError());
   // grid for every chunk; workgroups past the picked count exit at once
-  k_mtf_row<<<ceil_div(nchunks, kRowChunks), kT, 0, st>>>(bwt, r.boff, cbase, init, hi_list, n_hi, ranks, lead, trail,
-                                                          inner);
+  if (BZG_MTF_Q)
+    k_mtf_q<<<ceil_div(nchunks, kQChunks), kT, 0, st>>>(bwt, r.boff, cbase, init, hi_list, n_hi, ranks, lead, trail,
+                                                        inner);
+  else
+    k_mtf_row<<<ceil_div(nchunks, kRowChunks), kT, 0, st>>>(bwt, r.boff, cbase, init, hi_list, n_hi, ranks, lead, trail,
+                                                            inner);
   HIP_OK(hipGetLastError());
   k_rle2_plan<<<nb, 64, 0, st>>>(r.boff, cbase, lead, trail, inner, zin, coff, finalrun,
                                                 res.nmtf);
