@@ -963,14 +963,30 @@ __global__ void __launch_bounds__(kT) k_mtf_q(const uint8_t* __restrict__ L, con
       racc[u >> 2] |= (act ? rank : 0u) << (8 * (u & 3));
       if (act && q == 0) last[c] = (uint16_t)j;
       // the marker moves from step t to step j
-      const uint64_t bt = 1ull << tb, bj = 1ull << ((j16 & 63u) + u);
-      const bool clr = act && !first && q == tl, set = act && q == setl;
+      // (the cleared bit is set: an xor; the set word is the group's, a uniform branch)
+      const bool clr = act && !first && q == tl;
+      const uint64_t bt = clr ? 1ull << tb : 0ull;
 #pragma unroll
       for (uint32_t w = 0; w < 4; w++) {
-        const bool cw_ = clr && tw == w, sw_ = set && setw == w;
-        M[w] = cw_ ? (M[w] & ~bt) : M[w];
-        M[w] = sw_ ? (M[w] | bj) : M[w];
-        nm[w] = nm[w] - (cw_ ? 1u : 0u) + (sw_ ? 1u : 0u);
+        const bool cw_ = tw == w;
+        M[w] ^= cw_ ? bt : 0ull;
+        nm[w] -= (cw_ && clr) ? 1u : 0u;
+      }
+      if (act && q == setl) {
+        const uint64_t bj = 1ull << ((j16 & 63u) + u);
+        if (setw == 0) {
+          M[0] |= bj;
+          nm[0]++;
+        } else if (setw == 1) {
+          M[1] |= bj;
+          nm[1]++;
+        } else if (setw == 2) {
+          M[2] |= bj;
+          nm[2]++;
+        } else {
+          M[3] |= bj;
+          nm[3]++;
+        }
       }
       const bool fs = act && first && q == pl;
       S = fs ? (S | (1ull << pb)) : S;
