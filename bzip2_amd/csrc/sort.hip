@@ -2939,9 +2939,17 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     ClsLists N{};
     for (int c = 0; c < 6; c++) N.l[c] = ws.typed<Grp>("sort_s2n" + std::to_string(c), ccap[c]);
     {  // block order for the first S2 round (see k_unit_count)
+      // A list of more than S / 32 groups (high-entropy input: millions of small
+      // buckets, most of them settled by their first 16 characters) stays as it is: its
+      // reorder would cost more than the L2 locality it buys.
+      static const uint64_t reorder_div = [] {
+        const char* e = getenv("BZG_S2_REORDER_DIV");
+        return e ? (uint64_t)std::max(0, atoi(e)) : 32u;
+      }();
       uint32_t* ucnt = ws.u32("sort_ucnt", nb + 64);
       for (int c = 0; c < 6; c++) {
         if (ncls[c] < 2) continue;
+        if (reorder_div && (uint64_t)ncls[c] * reorder_div > S) continue;
         HIP_OK(hipMemsetAsync(ucnt, 0, 4 * (size_t)nb, st));
         k_unit_count<<<grid(ncls[c]), kT, 0, st>>>(C.l[c], ncls[c], ucnt);
         HIP_OK(hipGetLastError());
