@@ -1462,13 +1462,37 @@ __device__ __forceinline__ bool key_less(BsortKey a, BsortKey b) { return a < b;
 
 
 
-// x from lane ^ J (J < 64): DPP within quads, ds_swizzle within 32 lanes, bpermute across.
+// x from lane ^ J (J < 64), without the LDS pipe (BZG_XOR_DPP, default): DPP quad permutes
+// for 1 and 2; the half-row mirror (lane ^ 7 in 8) then the quad reverse (^ 3) for 4; a row
+// rotation by 8 (lane ^ 8 in a 16-lane row) for 8; gfx950's permlane16 / permlane32 swaps for
+// 16 and 32 (a swap of x with itself hands every row / half its partner's copy in one of the
+// two results).  BZG_XOR_DPP=0: ds_swizzle within 32 lanes, ds_bpermute across.
+#ifndef BZG_XOR_DPP
+#define BZG_XOR_DPP 0
+#endif
+__device__ __forceinline__ bool lane_in(uint64_t mask) { return __builtin_amdgcn_inverse_ballot_w64(mask); }
 template <int J>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
-  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
-  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
-  else if constexpr (J < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (J << 10) | 0x1F);
-  else return (uint32_t)__shfl_xor((int)x, J, 64);
+  if constexpr (J == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+  } else if constexpr (BZG_XOR_DPP && J == 4) {
+    const int y = __builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    return (uint32_t)__builtin_amdgcn_mov_dpp(y, 0x1B, 0xF, 0xF, false);      // [3,2,1,0]
+  } else if constexpr (BZG_XOR_DPP && J == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (BZG_XOR_DPP && J == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return lane_in(0x0000ffff0000ffffull) ? r[1] : r[0];  // even rows: the odd row's copy
+  } else if constexpr (BZG_XOR_DPP && J == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return lane_in(0x00000000ffffffffull) ? r[1] : r[0];  // low half: the high half's copy
+  } else if constexpr (J < 32) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (J << 10) | 0x1F);
+  } else {
+    return (uint32_t)__shfl_xor((int)x, J, 64);
+  }
 }
 
 // Direction masks of the bitonic network.  Element r of lane l sits at segment position
@@ -1492,7 +1516,6 @@ constexpr uint64_t ascending_mask(int kK, int r) {  // lanes whose position p ha
     if ((((l % kSeg) * kPer + r) & kK) == 0) m |= 1ull << l;
   return m;
 }
-__device__ __forceinline__ bool lane_in(uint64_t mask) { return __builtin_amdgcn_inverse_ballot_w64(mask); }
 
 template <int kSeg, int kPer, int kK, int kJ>
 __device__ __forceinline__ void bitonic_stage(BsortKey (&K)[kPer]) {
