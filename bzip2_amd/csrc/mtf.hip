@@ -77,8 +77,10 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
                                             uint32_t* __restrict__ siglen) {
   const ChunkRef r = chunk_ref(boff, cbase);
   if (!r.valid) return;
-  uint8_t* out = sig + (size_t)r.gidx * 256;
-  uint32_t cnt = 0;
+  // the signature leaves four bytes per store (a store per new symbol was most of the kernel's
+  // time on high-entropy input: ~250 scattered byte stores per chunk)
+  uint32_t* out = reinterpret_cast<uint32_t*>(sig + (size_t)r.gidx * 256);
+  uint32_t cnt = 0, acc = 0;
   uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // seen bytes, in registers
   const uint32_t a_lo = r.lo & ~15u;
   uint32_t a = (r.hi - 1) & ~15u;  // word being processed (walking down to a_lo)
@@ -110,13 +112,18 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
           s1 |= qq == 1 ? bit : 0ull;
           s2 |= qq == 2 ? bit : 0ull;
           s3 |= qq == 3 ? bit : 0ull;
-          out[cnt++] = (uint8_t)c;
+          acc |= c << (8 * (cnt & 3u));
+          if ((++cnt & 3u) == 0) {
+            out[(cnt >> 2) - 1] = acc;
+            acc = 0;
+          }
         }
       }
     }
     if (a <= a_lo) break;
     a -= 16;
   }
+  if (cnt & 3u) out[cnt >> 2] = acc;
   siglen[r.gidx] = cnt;
 }
 
