@@ -142,10 +142,7 @@ __device__ __forceinline__ int n_groups(uint32_t nmtf) {  // compress.c:266-270
 //         k_huff: BZ2_hbMakeCodeLengths for every (block, table), one wave each };
 //   k_cf (final mode): payload bits of every group under the final tables;
 //   k_final: canonical codes, selector MTF, table and header bit counts.
-#ifndef BZG_CF_SLICES
-#define BZG_CF_SLICES 2
-#endif
-constexpr uint32_t kCfSlices = BZG_CF_SLICES;  // workgroups per block in k_cf
+constexpr uint32_t kCfSlices = 2;  // workgroups per block in k_cf
 
 __global__ void k_init_tables(uint32_t b0, const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ freq_g,
                               const uint32_t* __restrict__ ninuse, uint8_t* __restrict__ lens_g,
@@ -178,18 +175,11 @@ __global__ void k_init_tables(uint32_t b0, const uint32_t* __restrict__ nmtf_g, 
 }
 
 constexpr uint32_t kCfVec = (kT * kGroupSize + 8 * kT - 1) / (8 * kT);  // 16-byte words per thread per chunk
-// BZG_CF_MODE 1: one 64-bit length word per symbol (all six tables in 10-bit fields), so a
-// symbol costs one LDS read and one add; 0: two 32-bit words (tables 0-2 / 3-5)
-#ifndef BZG_CF_MODE
-#define BZG_CF_MODE 1
-#endif
+// One 64-bit length word per symbol (all six tables in 10-bit fields), so a symbol costs one
+// LDS read and one add (two 32-bit words measured 0.4 ms per GB slower, round 4).
 struct CfLds {
   alignas(16) uint16_t chunk[kT * kGroupSize + 8];
-#if BZG_CF_MODE == 1
   uint64_t lenp[kMaxAlpha];
-#else
-  uint32_t lenp[2][kMaxAlpha];       // lengths of tables 0-2 / 3-5 in 10-bit fields
-#endif
   uint32_t rfreq[kNGroups][kMaxAlpha * 2];  // 2 bank-spread copies per counter (thread & 1)
   uint32_t sh[8];
 };
@@ -213,15 +203,10 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
   const uint16_t* mv = mtfv + mtf_off[b];
   const uint8_t* L = lens_g + (size_t)b * kNGroups * kMaxAlpha;
   for (int v = threadIdx.x; v < kMaxAlpha; v += kT) {
-#if BZG_CF_MODE == 1
     uint64_t x = 0;
 #pragma unroll
     for (int t = 0; t < kNGroups; t++) x |= (uint64_t)L[t * kMaxAlpha + v] << (10 * t);
     S.lenp[v] = x;
-#else
-    S.lenp[0][v] = L[v] | ((uint32_t)L[kMaxAlpha + v] << 10) | ((uint32_t)L[2 * kMaxAlpha + v] << 20);
-    S.lenp[1][v] = L[3 * kMaxAlpha + v] | ((uint32_t)L[4 * kMaxAlpha + v] << 10) | ((uint32_t)L[5 * kMaxAlpha + v] << 20);
-#endif
   }
   if (!final)
     for (int i = threadIdx.x; i < kNGroups * kMaxAlpha * 2; i += kT) (&S.rfreq[0][0])[i] = 0;
@@ -254,24 +239,12 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
       const uint16_t* c = S.chunk + threadIdx.x * kGroupSize;
       const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
       // 50 lengths <= 17: every 10-bit field sum stays below 1024
-#if BZG_CF_MODE == 1
       uint64_t acc = 0;
 #pragma unroll 10
       for (uint32_t i = 0; i < n; i++) acc += S.lenp[c[i]];
       uint32_t cost[kNGroups];
 #pragma unroll
       for (int t = 0; t < kNGroups; t++) cost[t] = (uint32_t)(acc >> (10 * t)) & 1023u;
-#else
-      uint32_t a = 0, bsum = 0;
-#pragma unroll 10
-      for (uint32_t i = 0; i < n; i++) {
-        const uint32_t v = c[i];
-        a += S.lenp[0][v];
-        bsum += S.lenp[1][v];
-      }
-      const uint32_t cost[kNGroups] = {a & 1023u, (a >> 10) & 1023u, a >> 20,
-                                       bsum & 1023u, (bsum >> 10) & 1023u, bsum >> 20};
-#endif
       if (final) {
         const uint32_t bits = cost[selo[g]];
         gbits_g[(size_t)b * kMaxSelectors + g] = (uint16_t)bits;
@@ -517,19 +490,13 @@ struct BitWriter {
 // nbits up to 32 may overflow the accumulator when nacc > 32 after a put; put() keeps
 // nacc < 32 on exit, so a put of <= 32 bits never loses bits.
 
-#ifndef BZG_PACK_SLICES
-#define BZG_PACK_SLICES 1
-#endif
-constexpr uint32_t kPackSlices = BZG_PACK_SLICES;  // workgroups per block in k_pack
+constexpr uint32_t kPackSlices = 1;  // workgroups per block in k_pack
 
 // The step's bit buffer holds either the whole step (default) or a window of it: a smaller
 // buffer lets more workgroups share a CU, and a step with more bits (high-entropy input) is
 // encoded in several windows, each taking the groups that start inside it.
 constexpr uint32_t kPackFull = (kT * kGroupSize * kMaxCodeLen + 31) / 32 + 2;
-#ifndef BZG_PACK_BITSW
-#define BZG_PACK_BITSW 3328  // 13 KB: 3 workgroups per CU (the whole step, kPackFull words, gives 2)
-#endif
-constexpr uint32_t kPackBitsW = BZG_PACK_BITSW;             // words of the bit buffer
+constexpr uint32_t kPackBitsW = 3328;  // words of the bit buffer: 13 KB, 3 workgroups per CU (the whole step, kPackFull words, gives 2)
 constexpr uint32_t kPackOv = (kGroupSize * kMaxCodeLen + 31) / 32 + 1;  // words a group can reach past its window
 static_assert(kPackBitsW >= kPackFull || kPackBitsW >= 4 * kPackOv, "bit window too small");
 constexpr uint32_t kPackWS = kPackBitsW >= kPackFull ? kPackBitsW * 32 : (kPackBitsW - kPackOv) * 32;  // bits per window

@@ -34,9 +34,14 @@ Workspace::~Workspace() {
 
 void Workspace::set_stream(hipStream_t s) {
   if (s == stream_) return;
-  // no throw: Lease's destructor hands the workspaces back to the engine's own stream
-  if (!bufs_.empty() && (handoff_ || hipEventCreateWithFlags(&handoff_, hipEventDisableTiming) == hipSuccess)) {
-    if (hipEventRecord(handoff_, stream_) == hipSuccess) (void)hipStreamWaitEvent(s, handoff_, 0);
+  // no throw: Lease's destructor hands the workspaces back to the engine's own stream.  The new
+  // stream must not run ahead of work still queued on the old one (a later free or growth on
+  // the new stream would release a buffer in use): an event when possible, else a host wait.
+  if (!bufs_.empty()) {
+    bool ordered = false;
+    if (handoff_ || hipEventCreateWithFlags(&handoff_, hipEventDisableTiming) == hipSuccess)
+      ordered = hipEventRecord(handoff_, stream_) == hipSuccess && hipStreamWaitEvent(s, handoff_, 0) == hipSuccess;
+    if (!ordered) (void)hipStreamSynchronize(stream_);
   }
   stream_ = s;
 }
@@ -266,53 +271,31 @@ struct Engine {
       std::vector<std::promise<void>> sorted(K);
       std::vector<std::future<void>> sorted_f;
       for (auto& x : sorted) sorted_f.push_back(x.get_future());
-      // staggered parts (BZG_STAGGER): part p starts sorting once part p - 1 has finished its
-      // S1 byte passes, so that one part's bandwidth-bound S1 passes run beside the other's
-      // VALU-bound S2 sorts instead of both parts contending in the same phase
-      const bool stagger = S > 1 && cfg("BZG_STAGGER", 0, 0, 1) != 0;
-      std::vector<std::promise<void>> s1p(K);
-      std::vector<std::shared_future<void>> s1f;
-      std::vector<char> s1set(K, 0);  // (each entry touched by its part's thread only)
-      for (auto& x : s1p) s1f.push_back(x.get_future().share());
-      auto s1_release = [&](uint32_t p) {
-        if (!s1set[p]) {
-          s1set[p] = 1;
-          s1p[p].set_value();
-        }
-      };
       const int dev = device;
       auto sorter = [&, dev](int t) {
         try {
           HIP_OK(hipSetDevice(dev));  // the current device is per host thread
         } catch (...) {
-          for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) {
-            s1_release(p);
-            sorted[p].set_exception(std::current_exception());
-          }
+          for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) sorted[p].set_exception(std::current_exception());
           return;
         }
         hipStream_t ss = S == 1 ? s : sstream[t];
         bool failed = false;
         for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) {
           if (failed) {
-            s1_release(p);
             sorted[p].set_exception(std::make_exception_ptr(HipFailure(hipErrorUnknown)));
             continue;
           }
           try {
             Part& P = parts[p];
-            if (stagger && p > 0) s1f[p - 1].wait();  // (a failed part releases it too)
             P.w->set_stream(ss);
             if (ss != s) HIP_OK(hipStreamWaitEvent(ss, ev_rle, 0));
             copyrank_begin(P.r, P.hboff, P.hper, P.hbq, P.a5, ss);  // host copy ranks overlap the sort
-            const std::function<void()> done = [&s1_release, p] { s1_release(p); };
-            bwt_stage(*P.w, P.r, P.hboff, P.hper, bwt + hboff[P.b0], rank0 + P.b0, &P.ss, ss, P.hqp.data(), &done);
-            s1_release(p);
+            bwt_stage(*P.w, P.r, P.hboff, P.hper, bwt + hboff[P.b0], rank0 + P.b0, &P.ss, ss, P.hqp.data());
             HIP_OK(hipEventRecord(psorted[p], ss));
             sorted[p].set_value();
           } catch (...) {
             failed = true;
-            s1_release(p);
             sorted[p].set_exception(std::current_exception());
           }
         }

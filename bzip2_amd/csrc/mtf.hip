@@ -245,133 +245,31 @@ __global__ void __launch_bounds__(64 * kCW) k_compose(const uint32_t* __restrict
 // search and shift, no memory access); positions 32..255 live in LDS as 56 words laid out
 // [word][thread].  Ranks >= 32 are rare (< 0.1% on text), so the LDS part is touched by few
 // steps of a wave.
-#ifndef BZG_MTF_REGW
-#define BZG_MTF_REGW 8
-#endif
-constexpr int kRegW = BZG_MTF_REGW;  // list words (4 positions each) held in registers
-#ifndef BZG_MTF_ROWMIN
-#define BZG_MTF_ROWMIN 64
-#endif
-constexpr uint32_t kRowMin = BZG_MTF_ROWMIN;  // chunks with more distinct symbols go to k_mtf_row
-// BZG_MTF_FIRST (default): a chunk handled here has at most kRowMin (64) distinct symbols, and
-// the symbols it has moved always precede the ones it has not touched, which keep the order of
-// the chunk's initial list.  So the lane keeps only the recency list of the moved symbols (64
-// positions: 8 register words and 8 LDS words instead of 56), and the rank of a symbol's first
-// occurrence, which depends on the initial list only, comes precomputed from k_mtf_first.
-// The LDS footprint drops from 74 KB to 25 KB per workgroup (2 -> 6 waves per SIMD).
-#ifndef BZG_MTF_FIRST
-#define BZG_MTF_FIRST 0
-#endif
-constexpr bool kFirst = BZG_MTF_FIRST != 0;
-constexpr int kListW = kFirst ? 16 : 64;  // list words a lane holds (registers + LDS)
+constexpr int kRegW = 8;  // list words (4 positions each) held in registers
+constexpr uint32_t kRowMin = 64;  // chunks with more distinct symbols go to k_mtf_q
+constexpr int kListW = 64;  // list words a lane holds (registers + LDS)
 
-// k-th distinct symbol of the chunk by first occurrence, s_k: its rank there is
-// k + pos0(s_k) - #{i < k : pos0(s_i) < pos0(s_k)} (pos0: position in the chunk's initial
-// list; the k moved symbols precede the untouched rest).  One wave per chunk; frank[g * 64 + k].
-__global__ void __launch_bounds__(kT) k_mtf_first(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
-                                                  const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ siglen,
-                                                  const uint32_t* __restrict__ init, uint8_t* __restrict__ frank) {
-  __shared__ uint32_t fp[kT / 64][256];  // first offset of each symbol in the chunk
-  __shared__ uint32_t p0[kT / 64][256];  // its position in the chunk's initial list
-  __shared__ uint32_t cs[kT / 64][64];   // distinct symbols: first offset << 8 | symbol
-  __shared__ uint32_t ord[kT / 64][64];  // distinct symbols by first occurrence
-  const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
-  const uint32_t b = blockIdx.y, c = blockIdx.x * (kT / 64) + w;
-  const uint32_t n = boff[b + 1] - boff[b];
-  if (c * kChunk >= n) return;  // (uniform in the wave)
-  const uint32_t g = cbase[b] + c;
-  const uint32_t sl = siglen[g];
-  if (sl > kRowMin) return;
-  const uint32_t lo = boff[b] + c * kChunk, len = min(n - c * kChunk, kChunk);
-  for (uint32_t k = lane; k < 256; k += 64) {
-    fp[w][k] = 0xffffffffu;
-    p0[w][k] = 0xffffffffu;
-  }
-  wave_sync();
-  // (the list past nInUse is unspecified: the smallest position of a byte is its own)
-  const uint32_t iw = init[(size_t)g * 64 + lane];
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++) atomicMin(&p0[w][(iw >> (8 * k)) & 0xffu], lane * 4 + k);
-  uint4 q;
-  __builtin_memcpy(&q, L + lo + 16 * lane, 16);  // unaligned; the column is padded
-  const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (uint32_t k = 0; k < 16; k++)
-    if (16 * lane + k < len) atomicMin(&fp[w][(wd[k >> 2] >> (8 * (k & 3))) & 0xffu], 16 * lane + k);
-  wave_sync();
-  uint32_t have = 0, e[4];
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++) {
-    e[k] = fp[w][lane * 4 + k];
-    have += e[k] != 0xffffffffu ? 1u : 0u;
-  }
-  uint32_t p = wave_incl_sum(have) - have;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; k++)
-    if (e[k] != 0xffffffffu) cs[w][p++] = (e[k] << 8) | (lane * 4 + k);
-  wave_sync();
-  if (lane < sl) {
-    const uint32_t me = cs[w][lane];
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < sl; i++) k += cs[w][i] < me ? 1u : 0u;
-    ord[w][k] = me & 0xffu;
-  }
-  wave_sync();
-  if (lane < sl) {
-    const uint32_t ps = p0[w][ord[w][lane]];
-    uint32_t before = 0;
-    for (uint32_t i = 0; i < lane; i++) before += p0[w][ord[w][i]] < ps ? 1u : 0u;
-    frank[(size_t)g * 64 + lane] = (uint8_t)(lane + ps - before);
-  }
-}
-
-#ifndef BZG_MTF_LB
-#define BZG_MTF_LB 0
-#endif
-#if BZG_MTF_LB > 0
-#define BZG_MTF_BOUNDS __launch_bounds__(kT, BZG_MTF_LB)
-#else
-#define BZG_MTF_BOUNDS __launch_bounds__(kT)
-#endif
-__global__ void BZG_MTF_BOUNDS k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
+__global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                                 const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ siglen,
-                                                const uint32_t* __restrict__ init, const uint8_t* __restrict__ frank,
+                                                const uint32_t* __restrict__ init,
                                                 uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
                                                 uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
   __shared__ uint32_t lst[kListW - kRegW][kT];
-  __shared__ uint32_t frl[kFirst ? 16 : 1][kT];  // kFirst: the chunk's first-occurrence ranks, 4 per word
   // rank words of the wave's 64 chunks for one 64-symbol window, [chunk][word] (17: no bank
   // conflicts on the per-lane writes); flushed as 16-byte stores, 4 lanes per chunk
   __shared__ uint32_t stg[kT / 64][64 * 17];
   const ChunkRef r = chunk_ref(boff, cbase);
   const uint32_t t = threadIdx.x, lane = __lane_id();
   uint32_t* sw = stg[t >> 6];
-  // chunks with many distinct symbols are left to k_mtf_row (their ranks mostly miss the
+  // chunks with many distinct symbols are left to k_mtf_q (their ranks mostly miss the
   // register words)
   const bool mine = r.valid && siglen[r.gidx] <= kRowMin;
   const uint32_t len = mine ? r.hi - r.lo : 0u;
   const uint32_t* src = init + (size_t)(r.valid ? r.gidx : 0u) * 64;
   uint32_t W[kRegW];
-  uint32_t m = 0;  // kFirst: symbols moved so far (list positions in use)
-  const uint32_t* fr = reinterpret_cast<const uint32_t*>(frank + (size_t)(r.valid ? r.gidx : 0u) * 64);
-  uint32_t fcur = 0, fi = 0;  // kFirst: first-occurrence ranks (current word of frl)
-  if constexpr (kFirst) {
 #pragma unroll
-    for (int w = 0; w < kRegW; w++) W[w] = 0;
-    for (int w = kRegW; w < kListW; w++) lst[w - kRegW][t] = 0;
-    if (mine) {
-      uint32_t x[16];
-#pragma unroll
-      for (int k = 0; k < 16; k++) x[k] = fr[k];
-#pragma unroll
-      for (int k = 0; k < 16; k++) frl[k][t] = x[k];
-    }
-    fcur = frl[0][t];
-  } else {
-#pragma unroll
-    for (int w = 0; w < kRegW; w++) W[w] = src[w];
-    for (int w = kRegW; w < kListW; w++) lst[w - kRegW][t] = src[w];
-  }
+  for (int w = 0; w < kRegW; w++) W[w] = src[w];
+  for (int w = kRegW; w < kListW; w++) lst[w - kRegW][t] = src[w];
   uint32_t racc = 0;  // 4 ranks packed
   uint32_t ld = 0, z = 0, cnt = 0;
   bool seen = false;
@@ -392,7 +290,7 @@ __global__ void BZG_MTF_BOUNDS k_mtf_run(const uint8_t* __restrict__ L, const ui
       pos = fw * 4 + ((uint32_t)__builtin_ctz(fz) >> 3);
     } else {  // beyond the register words: LDS words, 4 loads in flight per step (every
               // block byte is in the list)
-      const uint32_t wlim = kFirst ? min((uint32_t)kListW, (m + 3) >> 2) : (uint32_t)kListW;
+      const uint32_t wlim = (uint32_t)kListW;
       uint32_t w = kRegW, x = 0;
       for (; w < wlim; w += 4) {
         uint32_t y[4];
@@ -412,24 +310,13 @@ __global__ void BZG_MTF_BOUNDS k_mtf_run(const uint8_t* __restrict__ L, const ui
           break;
         }
       }
-      if (kFirst) {
-        pos = w < wlim ? w * 4 + ((uint32_t)__builtin_ctz(x) >> 3) : 0xffu;
-      } else {
-        if (w >= 64) {  // only a corrupt input; keeps the loop finite
-          w = 63;
-          x = 0x80000000u;
-        }
-        pos = w * 4 + ((uint32_t)__builtin_ctz(x) >> 3);
+      if (w >= 64) {  // only a corrupt input; keeps the loop finite
+        w = 63;
+        x = 0x80000000u;
       }
+      pos = w * 4 + ((uint32_t)__builtin_ctz(x) >> 3);
     }
-    uint32_t rank = pos;
-    bool fresh = false;
-    if (kFirst && pos >= m) {  // first occurrence in the chunk: enters at the front
-      fresh = true;
-      pos = m++;
-      rank = (fcur >> (8 * (fi & 3))) & 0xffu;
-      if ((++fi & 3) == 0 && fi < 64) fcur = frl[fi >> 2][t];
-    }
+    const uint32_t rank = pos;
     racc |= rank << (8 * (j & 3));
     if ((j & 3) == 3 || j + 1 == len) {
       sw[lane * 17 + ((j >> 2) & 15)] = racc;
@@ -438,7 +325,7 @@ __global__ void BZG_MTF_BOUNDS k_mtf_run(const uint8_t* __restrict__ L, const ui
     // zero-run summary (RUNA/RUNB symbols of inner runs are counted here)
     if (rank == 0) {
       z++;
-      if (!fresh) return;
+      return;
     } else {
       if (!seen) {
         ld = z;
@@ -550,260 +437,6 @@ __global__ void __launch_bounds__(kT) k_mtf_pick(const uint32_t* __restrict__ bo
   if (hi) hi_list[p] = (r.b << 11) | r.c;
 }
 
-// MTF of one chunk by a row of 16 lanes: lane l holds list positions 16 l .. 16 l + 15 in four
-// words, so a symbol is found by one SWAR test per word and a ballot (the list holds every
-// symbol once: exactly one lane of the row matches), and the move to front is a one-byte
-// shift of the lanes before the match (the byte crossing a lane boundary comes from the
-// previous lane by a DPP row shift) and a partial shift in the matching lane.  A wave runs
-// four chunks in lockstep.  Ranks are staged in LDS, then stored as 16-byte words; the
-// zero-run summary is read from them afterwards.
-constexpr uint32_t kRowChunks = kT / 16;
-#ifndef BZG_MTF_Q
-#define BZG_MTF_Q 1  // high-entropy chunks on a quad of lanes each (k_mtf_q); 0: a row of 16 (k_mtf_row)
-#endif
-#ifndef BZG_MTF_TS
-#define BZG_MTF_TS 1  // k_mtf_row ranks from occurrence times (0: the shifting list in the row's registers)
-#endif
-// v_ffbl_b32: lowest set bit, ~0 for 0 (the hardware result; __builtin_ctz leaves 0 undefined)
-__device__ __forceinline__ uint32_t ffbl_hw(uint32_t x) {
-  uint32_t r;
-  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
-  return r;
-}
-__global__ void __launch_bounds__(kT) k_mtf_row(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
-                                                const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
-                                                const uint32_t* __restrict__ hi_list, const uint32_t* __restrict__ n_hi,
-                                                uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
-                                                uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
-  // (rows 4 words apart: the four rows of a wave read and write different banks)
-  __shared__ uint32_t sym[kRowChunks][kChunk / 4 + 4];  // the chunk's BWT bytes
-  __shared__ uint32_t rk[kRowChunks][kChunk / 4 + 4];   // its ranks
-  __shared__ uint32_t part[kRowChunks][16][4];      // zero-run summaries of the lanes' slices
-#if BZG_MTF_TS
-  __shared__ uint16_t last[kRowChunks][256];  // step of each symbol's last occurrence (~0: none yet)
-  __shared__ uint8_t p0[kRowChunks][256];     // its position in the chunk's initial list
-#endif
-  const uint32_t nh = *n_hi;
-  if (blockIdx.x * kRowChunks >= nh) return;
-  const uint32_t t = threadIdx.x, lane = __lane_id(), row = lane >> 4, rl = lane & 15;
-  const uint32_t ci = (t >> 4);  // chunk of this row within the workgroup
-  const uint32_t i = blockIdx.x * kRowChunks + ci;
-  const bool valid = i < nh;
-  uint32_t len = 0, lo = 0, g = 0;
-  if (valid) {
-    const uint32_t e = hi_list[i], b = e >> 11, c = e & 2047u;
-    lo = boff[b] + c * kChunk;
-    len = min(boff[b + 1], lo + kChunk) - lo;
-    g = cbase[b] + c;
-  }
-  for (uint32_t j = rl; j < kChunk / 4; j += 16) {
-    uint32_t w = 0;
-    for (uint32_t k = 0; k < 4; k++)
-      if (4 * j + k < len) w |= (uint32_t)L[lo + 4 * j + k] << (8 * k);
-    sym[ci][j] = w;
-  }
-  uint32_t W0 = 0, W1 = 0, W2 = 0, W3 = 0;
-  if (valid) {
-    const uint4 q = reinterpret_cast<const uint4*>(init + (size_t)g * 64)[rl];
-    W0 = q.x, W1 = q.y, W2 = q.z, W3 = q.w;
-  }
-  __syncthreads();
-  // the wave runs to its longest chunk (uniform loop bound)
-  uint32_t wl = len;
-#pragma unroll
-  for (int o = 16; o < 64; o <<= 1) wl = max(wl, (uint32_t)__shfl_xor((int)wl, o, 64));
-  uint8_t* rb = reinterpret_cast<uint8_t*>(rk[ci]);
-#if BZG_MTF_TS
-  // Ranks from occurrence times instead of a shifting list.  A symbol seen earlier in the
-  // chunk has rank = the number of distinct symbols used since its last occurrence = the
-  // number of last-occurrence markers between the two steps (a 1024-bit marker map, 64 steps
-  // per lane).  A first occurrence has rank m + p - #{symbols already used with p0 < p} (m
-  // used so far, p its initial-list position: the used symbols lead, the untouched list
-  // follows; a 256-bit map of used positions, 16 per lane).  Either count is a popcount per
-  // lane summed over the row's 16 lanes by DPP, so a step costs the same at any rank.
-  {
-    // p0 = smallest position of each byte in the initial list (past nInUse the list is
-    // unspecified), built with atomicMin in the rank staging words, which are free until the loop
-    for (uint32_t k = rl; k < 256; k += 16) rk[ci][k] = 0xffu;
-    __syncthreads();
-    const uint32_t wv[4] = {W0, W1, W2, W3};
-    if (valid) {
-#pragma unroll
-      for (uint32_t k = 0; k < 16; k++) atomicMin(&rk[ci][(wv[k >> 2] >> (8 * (k & 3))) & 0xffu], 16 * rl + k);
-    }
-    __syncthreads();
-    for (uint32_t k = rl; k < 256; k += 16) {
-      p0[ci][k] = (uint8_t)rk[ci][k];
-      last[ci][k] = 0xffffu;
-    }
-    __syncthreads();
-  }
-  {
-    uint64_t M = 0;    // markers of steps 64 rl .. 64 rl + 63
-    uint32_t S = 0;    // used initial positions 16 rl .. 16 rl + 15
-    uint32_t m = 0;    // symbols used so far (row-uniform)
-    const int r64 = 64 * (int)rl, r16 = 16 * (int)rl;
-    auto rsum = [](uint32_t x) {  // inclusive sum over the row; lane 15 of the row holds the total
-      x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
-      x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
-      x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
-      x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
-      return x;
-    };
-    auto low64 = [](int n) {  // bits [0, n), n in [0, 64]
-      return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
-    };
-    const uint32_t* sw = sym[ci];
-    uint16_t* ls = last[ci];
-    const uint8_t* pz = p0[ci];
-    for (uint32_t j0 = 0; j0 < wl; j0 += 4) {
-      // the group's symbols, their last occurrences before the group and their initial positions
-      const uint32_t cur = sw[j0 >> 2];
-      uint32_t cs[4], tt[4], pp[4];
-#pragma unroll
-      for (uint32_t u = 0; u < 4; u++) {
-        cs[u] = (cur >> (8 * u)) & 0xffu;
-        tt[u] = ls[cs[u]];
-        pp[u] = pz[cs[u]];
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < 4; u++) {
-        const uint32_t j = j0 + u;
-        if (j >= wl) break;  // (uniform)
-        const bool act = j < len;
-        const uint32_t c = cs[u], p = pp[u];
-        uint32_t tl = tt[u];
-#pragma unroll
-        for (uint32_t v = 0; v < u; v++)
-          if (cs[v] == c) tl = j0 + v;  // an occurrence earlier in this group (latest wins)
-        const bool first = tl == 0xffffu;
-        const int lo = min(max((int)tl + 1 - r64, 0), 64), hi = min(max((int)j - r64, 0), 64);
-        const uint32_t cm = (uint32_t)__builtin_popcountll(M & low64(hi) & ~low64(lo));
-        const uint32_t cf = (uint32_t)__builtin_popcount(S & ((1u << min(max((int)p - r16, 0), 16)) - 1u));
-        const uint32_t tot = rsum(first ? cf : cm);
-        if (act && rl == 15) {
-          rb[j] = (uint8_t)(first ? m + p - tot : tot);
-          ls[c] = (uint16_t)j;
-        }
-        if (act) {
-          if (!first && (tl >> 6) == rl) M &= ~(1ull << (tl & 63u));
-          if ((j >> 6) == rl) M |= 1ull << (j & 63u);
-          if (first && (p >> 4) == rl) S |= 1u << (p & 15u);
-          m += first ? 1u : 0u;
-        }
-      }
-    }
-  }
-#else
-  const uint32_t rowshift = 16 * row;
-  // one step per symbol, branch-free; the symbols of 4 steps come in one LDS word, read a
-  // group ahead (the per-step byte read left its latency in every step)
-  const uint32_t* sw = sym[ci];
-  uint32_t nxt = sw[0];
-  for (uint32_t j0 = 0; j0 < wl; j0 += 4) {
-    const uint32_t cur = nxt;
-    nxt = sw[(j0 >> 2) + 1];  // (the row is padded by 4 words)
-#pragma unroll
-    for (uint32_t u = 0; u < 4; u++) {
-      const uint32_t j = j0 + u;
-      if (j >= wl) break;  // (uniform)
-      const bool act = j < len;
-      const uint32_t pat = __builtin_amdgcn_perm(0u, cur, u * 0x01010101u);  // byte u of cur, 4 times
-      const uint32_t c = pat & 0xffu;
-      // byte of c in each word: the lowest flagged byte of the zero-byte test (the list holds
-      // c once, so at most one word has a true zero, and false flags only sit above it);
-      // v_ffbl gives ~0 for a word without one, and (~0 >> 3) + 4k stays far above 16
-      const uint32_t x0 = W0 ^ pat, x1 = W1 ^ pat, x2 = W2 ^ pat, x3 = W3 ^ pat;
-      const uint32_t z0 = (x0 - 0x01010101u) & ~x0 & 0x80808080u;
-      const uint32_t z1 = (x1 - 0x01010101u) & ~x1 & 0x80808080u;
-      const uint32_t z2 = (x2 - 0x01010101u) & ~x2 & 0x80808080u;
-      const uint32_t z3 = (x3 - 0x01010101u) & ~x3 & 0x80808080u;
-      const uint32_t a0 = ffbl_hw(z0) >> 3, a1 = (ffbl_hw(z1) >> 3) + 4u, a2 = (ffbl_hw(z2) >> 3) + 8u,
-                     a3 = (ffbl_hw(z3) >> 3) + 12u;
-      const uint32_t local = min(min(min(a0, a1), min(a2, a3)), 16u);
-      const uint64_t m = __ballot(act && local < 16);
-      const uint32_t rowbits = (uint32_t)(m >> rowshift) & 0xffffu;
-      const uint32_t lane0 = (uint32_t)__builtin_ctz(rowbits | 0x10000u);
-      // bytes of this lane that shift: all before the match, up to the match in its lane
-      const uint32_t nshift = !act ? 0u : rl < lane0 ? 16u : rl == lane0 ? local + 1 : 0u;
-      if (act && rl == lane0) rb[j] = (uint8_t)(16 * rl + local);
-      // the top byte of the previous lane (the symbol itself into lane 0 of the row)
-      uint32_t cin = (uint32_t)__builtin_amdgcn_mov_dpp((int)(W3 >> 24), 0x111, 0xF, 0xF, false);  // row_shr:1
-      if (rl == 0) cin = c;
-      const uint32_t s0 = (W0 << 8) | cin;
-      const uint32_t s1 = __builtin_amdgcn_alignbyte(W1, W0, 3);
-      const uint32_t s2 = __builtin_amdgcn_alignbyte(W2, W1, 3);
-      const uint32_t s3 = __builtin_amdgcn_alignbyte(W3, W2, 3);
-      // bytes [0, nshift - 4k) of word k: 0xFFFFFFFF >> (32 - 8 clamp(nshift - 4k, 0, 4)) as a
-      // 64-bit shift (a shift by 32 gives 0)
-      const int q = 32 - 8 * (int)nshift;
-      auto msk = [&](int k) {
-        const int sh = min(max(q + 32 * k, 0), 32);
-        return (uint32_t)(0xFFFFFFFFull >> sh);
-      };
-      const uint32_t m0 = msk(0), m1 = msk(1), m2 = msk(2), m3 = msk(3);
-      W0 = (s0 & m0) | (W0 & ~m0);
-      W1 = (s1 & m1) | (W1 & ~m1);
-      W2 = (s2 & m2) | (W2 & ~m2);
-      W3 = (s3 & m3) | (W3 & ~m3);
-    }
-  }
-#endif
-  __syncthreads();
-  // ranks out (16-byte words) and the zero-run summary: lane rl takes ranks [64 rl, 64 rl + 64)
-  if (valid) {
-    for (uint32_t q = rl; q < kChunk / 16; q += 16)
-      if (16 * q < len) reinterpret_cast<uint4*>(ranks + (size_t)g * kChunk)[q] = reinterpret_cast<const uint4*>(rk[ci])[q];
-  }
-  {
-    uint32_t ld = 0, z = 0, cnt = 0;
-    bool seen = false;
-    const uint32_t a = 64 * rl, e = min(len, a + 64);
-    for (uint32_t j = a; j < e; j++) {
-      if (rb[j] == 0) {
-        z++;
-        continue;
-      }
-      if (!seen) {
-        ld = z;
-        seen = true;
-      } else {
-        cnt += nsym(z);
-      }
-      z = 0;
-      cnt++;
-    }
-    part[ci][rl][0] = seen ? ld : (e > a ? e - a : 0u);  // leading zeros (all, if none ranked)
-    part[ci][rl][1] = z;
-    part[ci][rl][2] = cnt;
-    part[ci][rl][3] = seen ? 1u : 0u;
-  }
-  __syncthreads();
-  if (valid && rl == 0) {  // chain the 16 slices as k_mtf_run would have walked them
-    uint32_t ld = 0, z = 0, cnt = 0;
-    bool seen = false;
-    for (uint32_t k = 0; k < 16; k++) {
-      const uint32_t pl = part[ci][k][0], pt = part[ci][k][1], pc = part[ci][k][2];
-      if (!part[ci][k][3]) {
-        z += pl;
-        continue;
-      }
-      // the slice's leading zeros end the carried run at its first ranked symbol
-      if (!seen) {
-        ld = z + pl;
-        seen = true;
-        cnt += pc;
-      } else {
-        cnt += nsym(z + pl) + pc;
-      }
-      z = pt;
-    }
-    lead[g] = seen ? ld : 0xffffffffu;
-    trail[g] = z;
-    inner[g] = cnt;
-  }
-}
-
 // 4b. per block (one wave): carried zero runs, chunk output offsets, nMTF.  The zero run
 // entering chunk c is a reset-and-add scan over the chunks (a chunk with a nonzero rank
 // resets it to its trailing zeros, an all-zero chunk adds its length); a chunk's output is
@@ -867,7 +500,7 @@ __global__ void __launch_bounds__(64) k_rle2_plan(const uint32_t* __restrict__ b
 // zin) -- its length comes from a segmented scan over the lanes.  Each lane writes its
 // symbols contiguously at an offset from a wave scan of the per-lane symbol counts.
 // MTF of one high-entropy chunk by a quad of lanes (16 chunks per wave), ranks from occurrence
-// times as in k_mtf_row's BZG_MTF_TS loop, with the per-chunk state small enough for 64
+// times (a 16-lane row shifting the list in registers, k_mtf_row, was 1.9x slower: round 4), with the per-chunk state small enough for 64
 // chunks per workgroup: lane q keeps the last-occurrence markers of steps 256 q .. 256 q + 255
 // (four 64-bit words and their counts) and the used initial-list positions 64 q .. 64 q + 63.
 // With m symbols used so far, a symbol last seen at step t has rank m - #{markers <= t}; a
@@ -932,7 +565,6 @@ __global__ void __launch_bounds__(kT) k_mtf_q(const uint8_t* __restrict__ L, con
     x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
     return x;
   };
-  auto low64 = [](uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); };
   const uint8_t* col = L + lo;
   uint4 nxt;
   __builtin_memcpy(&nxt, col, 16);  // (the column is padded)
@@ -1206,21 +838,10 @@ void mtf_stage(Workspace& ws, const Rle1Result& r, const uint8_t* bwt, uint32_t 
   HIP_OK(hipMemsetAsync(n_hi, 0, 4, st));
   k_mtf_pick<<<g2, kT, 0, st>>>(r.boff, cbase, siglen, hi_list, n_hi);
   HIP_OK(hipGetLastError());
-  uint8_t* frank = nullptr;
-  if (kFirst) {
-    frank = ws.u8("mtf_frank", (size_t)nchunks * 64 + 64);
-    k_mtf_first<<<dim3(ceil_div(maxch, kT / 64), nb), kT, 0, st>>>(bwt, r.boff, cbase, siglen, init, frank);
-    HIP_OK(hipGetLastError());
-  }
-  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, siglen, init, frank, ranks, lead, trail, inner);
+  k_mtf_run<<<g2, kT, 0, st>>>(bwt, r.boff, cbase, siglen, init, ranks, lead, trail, inner);
   HIP_OK(hipGetLastError());
   // grid for every chunk; workgroups past the picked count exit at once
-  if (BZG_MTF_Q)
-    k_mtf_q<<<ceil_div(nchunks, kQChunks), kT, 0, st>>>(bwt, r.boff, cbase, init, hi_list, n_hi, ranks, lead, trail,
-                                                        inner);
-  else
-    k_mtf_row<<<ceil_div(nchunks, kRowChunks), kT, 0, st>>>(bwt, r.boff, cbase, init, hi_list, n_hi, ranks, lead, trail,
-                                                            inner);
+  k_mtf_q<<<ceil_div(nchunks, kQChunks), kT, 0, st>>>(bwt, r.boff, cbase, init, hi_list, n_hi, ranks, lead, trail, inner);
   HIP_OK(hipGetLastError());
   k_rle2_plan<<<nb, 64, 0, st>>>(r.boff, cbase, lead, trail, inner, zin, coff, finalrun,
                                                 res.nmtf);

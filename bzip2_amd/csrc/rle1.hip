@@ -1139,17 +1139,19 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   }
   // binst[nblocks] is n for a final batch, else the input start of the incomplete block
   // that opens the next batch (a chunk start, so RLE1 restarts there with fresh state).
-  uint32_t tmp;
-  HIP_OK(hipMemcpyAsync(&tmp, binst + res.nblocks, 4, hipMemcpyDeviceToHost, st));
+  std::vector<uint32_t> hbi(res.nblocks + 1);
+  HIP_OK(hipMemcpyAsync(hbi.data(), binst, 4ull * (res.nblocks + 1), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
-  res.consumed = final_batch ? n : tmp;
+  res.consumed = final_batch ? n : hbi[res.nblocks];
 
   const int B = (int)res.nblocks;
   uint32_t* bcrc = ws.u32("bcrc", max_blocks + 2);
-  // sub-ranges per block from the mean block input (long runs: a block spans up to 46 MB)
-  const uint32_t split = (uint32_t)std::min<uint64_t>(
-      kCrcSplitMax, std::max<uint64_t>(kCrcSplit, ceil_div64(res.consumed, (uint64_t)B << 19)));
-  uint32_t* cpart = ws.u32("crc_part", (size_t)(max_blocks + 2) * kCrcSplitMax);
+  // sub-ranges per block from the largest block input (long runs: a block spans up to 46 MB),
+  // so that a batch mixing ordinary blocks with one long-run block still splits the long one
+  uint32_t maxin = 0;
+  for (int b = 0; b < B; b++) maxin = std::max(maxin, hbi[b + 1] - hbi[b]);
+  const uint32_t split = (uint32_t)std::min<uint64_t>(kCrcSplitMax, std::max<uint64_t>(kCrcSplit, ceil_div64(maxin, 1u << 19)));
+  uint32_t* cpart = ws.u32("crc_part", (size_t)(B + 2) * split);
   k_block_crc<<<dim3(split, B), kT, 0, st>>>(d_in, binst, ws.crc_table(), ws.xpow2_table(), split, cpart, tinfo, n);
   HIP_OK(hipGetLastError());
   k_crc_combine<<<B, 64, 0, st>>>(binst, cpart, ws.xpow2_table(), B, split, bcrc);

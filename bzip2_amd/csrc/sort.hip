@@ -33,27 +33,11 @@ namespace bzg {
 namespace {
 
 constexpr int kT = 256;
-#ifndef BZG_BIG
-#define BZG_BIG 256
-#endif
-constexpr uint32_t kBig = BZG_BIG;    // buckets larger than this are split by S1 byte passes
-static_assert(kBig == 128 || kBig == 256, "S2 classes cover up to 128 or 256 rotations");
-#ifndef BZG_DTILE
-#define BZG_DTILE 4096
-#endif
-constexpr uint32_t kDTile = BZG_DTILE;  // rotations per workgroup in an S1 pass
+constexpr uint32_t kBig = 256;        // buckets larger than this are split by S1 byte passes
+constexpr uint32_t kDTile = 4096;     // rotations per workgroup in a tiled S1 pass
 constexpr uint32_t kPerT = kDTile / kT;
 constexpr uint32_t kDBig = 16;        // S1 byte passes stop at this depth (then doubling)
-// 1: tiled S1 passes keep a 4-character key cache beside the slots (sk / sk2); 0: every tiled
-// pass gathers its character from the text (L2: the tiles of an XCD walk one or two blocks)
-#ifndef BZG_S1_TCACHE
-#define BZG_S1_TCACHE 1
-#endif
-constexpr bool kTCache = BZG_S1_TCACHE != 0;
-#ifndef BZG_SG
-#define BZG_SG 2048
-#endif
-constexpr uint32_t kSG = BZG_SG;      // S1 groups up to this size are packed into shared tiles
+constexpr uint32_t kSG = 2048;      // S1 groups up to this size are packed into shared tiles
 // size classes: 0..5 go to S2 (2-8 .. 129-256), 6 / 7 to the next S1 pass (packed / tiled),
 // 8 (still big after kDBig characters) to the doubling fallback
 constexpr int kNCls = 8;
@@ -61,10 +45,7 @@ constexpr uint32_t kClsMax[7] = {8, 16, 32, 64, 128, kBig, kSG};
 constexpr uint32_t kClsDeep = 8;
 // S2 workgroups walk the (block-ordered) group lists XCD by XCD: each XCD's L2 then holds the
 // text and slots of its own few blocks instead of every block's
-#ifndef BZG_S2_XCD
-#define BZG_S2_XCD 1
-#endif
-__device__ __forceinline__ uint32_t s2_wg() { return BZG_S2_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x; }
+__device__ __forceinline__ uint32_t s2_wg() { return xcd_remap(blockIdx.x, gridDim.x); }
 
 __host__ __device__ __forceinline__ uint32_t size_cls(uint32_t n) {
   return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= kBig ? 5u : n <= kSG ? 6u : 7u;
@@ -254,7 +235,7 @@ __device__ __forceinline__ void s1_load(const SortBufs& B, const Grp& gr, const 
   uint32_t* srck = alt ? B.sk2 : B.sk;
   const bool ident = gr.flags & kGrpIdent;
   const uint32_t depth = grp_depth(gr);
-  const bool fresh = ident || ((kCounting || !kTCache) && grp_cache(gr) == 0);
+  const bool fresh = ident || (kCounting && grp_cache(gr) == 0);
   const uint8_t* ut = B.text + U.toff;
   // (whole-loop uniform branches keep vv / kk in registers)
   if (ident) {
@@ -276,7 +257,7 @@ __device__ __forceinline__ void s1_load(const SortBufs& B, const Grp& gr, const 
       const uint32_t q = cyc_pos(vv[i], depth, U.len);
       kk[i] = q + 4 <= U.len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(ut, U.len, q);
     }
-    if (kCounting && !ident && kTCache) {
+    if (kCounting && !ident) {
 #pragma unroll
       for (int i = 0; i < (int)kPerT; i++) {
         const uint32_t e = lo + i * kT + threadIdx.x;
@@ -292,13 +273,9 @@ __device__ __forceinline__ uint32_t s1_next_cache(const Grp& gr) {
   return c ? c - 1 : 3u;
 }
 // the same for the buckets of a tiled pass
-__device__ __forceinline__ uint32_t tiled_next_cache(const Grp& gr) { return kTCache ? s1_next_cache(gr) : 0u; }
+__device__ __forceinline__ uint32_t tiled_next_cache(const Grp& gr) { return s1_next_cache(gr); }
 
-#ifndef BZG_HIST_CP
-#define BZG_HIST_CP 4
-#endif
-constexpr uint32_t kHistCp = BZG_HIST_CP;
-static_assert(kHistCp == 4 || kHistCp == 8, "histogram copies");
+constexpr uint32_t kHistCp = 4;  // (8 copies measured neutral: profiles/r04_ab_*)
 
 __global__ void __launch_bounds__(kT) k_s1_hist(const TileRec* __restrict__ TR, SortBufs B, uint32_t* __restrict__ hist) {
   // kHistCp copies of every bin in consecutive words (lane % kHistCp picks one): lanes of a
@@ -462,7 +439,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
       kk[i] = Lk[x];
       pos[i] = base[kk[i] >> 24] + x;
       dst[pos[i]] = vv[i];
-      if (kTCache && (flag[kk[i] >> 24] & 2u)) dstk[pos[i]] = kk[i] << 8;
+      if (flag[kk[i] >> 24] & 2u) dstk[pos[i]] = kk[i] << 8;
     }
   }
   // a bucket of one: this rotation is ordered (its primary-SA copy is made by k_s1_single,
@@ -532,10 +509,7 @@ __global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, const Unit*
 
 // packed kernels: 512 threads x 8 elements (a tile holds < 2 kSG rotations; kSG on average,
 // so the element loops stop at the tile's last 512-element round)
-#ifndef BZG_TS
-#define BZG_TS 512
-#endif
-constexpr uint32_t kTS = BZG_TS, kPerTS = 2 * kSG / kTS;
+constexpr uint32_t kTS = 512, kPerTS = 2 * kSG / kTS;
 // (group, digit) bins keep kCp copies in consecutive words (thread & 1 picks one), as in k_s1_hist
 constexpr uint32_t kCp = 2;
 struct S1sLds {
@@ -797,294 +771,6 @@ __global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, con
   }
 }
 
-// ---- packed S1 groups finished in LDS (k_s1p): a tile holds all the groups whose element
-// prefix falls in a kSG window (< 2 kSG rotations).  The tile stays in LDS while byte passes
-// split its big segments (> kBig rotations); each pass counts (segment, character) bins with
-// LDS atomics, scans them and moves every element of a big segment to its bucket inside the
-// tile.  A bucket of one is final (SA, BWT byte, origPtr); a bucket of 2..kBig rotations goes
-// to the S2 class list of its size (its rotations stored at their slots of the primary SA);
-// a bucket still larger than kBig after kDLds characters goes to the doubling fallback.  So
-// the rotations of a packed group are read from HBM once and written once, whatever the
-// number of passes; the text is gathered 4 characters at a time per rotation.
-constexpr uint32_t kPE = 2 * kSG;                 // elements per tile
-constexpr uint32_t kPT = 512;                     // threads
-constexpr uint32_t kPPer = kPE / kPT;             // elements per thread
-constexpr uint32_t kPSeg = kPE / (kBig + 1) + 2;  // big segments at once (>= kSGrp)
-constexpr uint32_t kDLds = 64;                    // depth at which a big bucket goes deep
-static_assert(kPSeg >= kSGrp, "the initial groups of a tile are big segments");
-
-struct S1pLds {
-  uint32_t v[kPE];                 // rotation at each tile position
-  uint32_t key[kPE];               // its next characters, most significant first
-  uint8_t seg[kPE];                // big segment of the position, 0xff once settled
-  uint32_t cnt[kPSeg * 256];       // (segment, character) bin counts
-  uint32_t cur[kPSeg * 256];       // bin bases (tile positions)
-  uint8_t nseg[kPSeg * 256];       // next segment of a bin: 0..kPSeg-1, 0xfe settled
-  // segment tables (current and next): tile start, size, depth, valid key bytes, slot delta
-  // (global slot = tile position + delta), unit
-  uint32_t sstart[2][kPSeg], ssize[2][kPSeg], sdepth[2][kPSeg], scache[2][kPSeg], sdelta[2][kPSeg], sunit[2][kPSeg];
-  uint32_t stoff[2][kPSeg], slen[2][kPSeg];  // text offset / length of the segment's unit
-  uint32_t segb[kPSeg];             // scan value at each segment's first bin
-  uint32_t ccls[8];                 // S2 groups of the tile per size class; [7] = records
-  uint32_t nbig[2];
-  uint32_t sh[kPT / 64];
-};
-
-// Appends n groups of class c (wave-aggregated).  app[c] holds the next free list index.
-__device__ __forceinline__ void cls_append(const ClsLists& C, uint32_t* __restrict__ app, bool act, uint32_t c,
-                                           const Grp& g) {
-#pragma unroll
-  for (uint32_t k = 0; k < 6; k++) {
-    const uint32_t p = wave_append(app + k, act && c == k);
-    if (act && c == k) C.l[k][p] = g;
-  }
-}
-
-__global__ void __launch_bounds__(kPT) k_s1p(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
-                                            const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
-                                            SortBufs B, SortOut O, uint32_t* __restrict__ rec,
-                                            uint32_t* __restrict__ nrec, uint32_t* __restrict__ ccnt, uint32_t nTot,
-                                            uint32_t ibase, uint32_t nT) {
-  __shared__ S1pLds S;
-  const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t i0 = first[t];
-  const uint32_t tid = threadIdx.x;
-  if (i0 == 0xffffffffu) {
-    if (tid < (uint32_t)kNCls) ccnt[(size_t)tid * nTot + ibase + t] = 0;
-    if (tid == 0) nrec[t] = 0;
-    return;
-  }
-  const uint32_t ni = min(last[t], i0 + kSGrp) - i0;
-  if (tid < 8) S.ccls[tid] = 0;
-  // S2 groups leave as 2-word records (slot; unit:16 | depth:7 | size:9) in the tile's own part
-  // of `rec` (a tile of n rotations has at most n / 2 groups), for k_s1p_emit
-  uint32_t* trec = rec + P[i0];
-  // ---- load the tile's groups: segment tables 0 and every element's rotation and key
-  if (tid < ni) {
-    const Grp g = SG[i0 + tid];
-    S.ssize[0][tid] = g.size;
-    S.sdepth[0][tid] = grp_depth(g);
-    S.scache[0][tid] = (g.flags & kGrpIdent) ? 0u : grp_cache(g);
-    S.sunit[0][tid] = g.unit;
-    S.sdelta[0][tid] = g.start;  // fixed below
-    S.sstart[0][tid] = g.flags;  // flags, replaced by the tile start below
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t o = 0;
-    for (uint32_t j = 0; j < ni; j++) {
-      const uint32_t fl = S.sstart[0][j];
-      S.sstart[0][j] = o;
-      S.sdelta[0][j] -= o;
-      S.ssize[0][j] |= (fl & (kGrpIdent | kGrpAlt)) << 30;  // source buffer bits, stripped below
-      o += S.ssize[0][j] & 0x3fffffffu;
-    }
-    S.nbig[0] = ni;
-  }
-  __syncthreads();
-  if (tid < ni) {
-    const Unit U = B.units[S.sunit[0][tid]];
-    S.stoff[0][tid] = U.toff;
-    S.slen[0][tid] = U.len;
-  }
-  uint32_t n = 0;
-  for (uint32_t j = 0; j < ni; j++) n += S.ssize[0][j] & 0x3fffffffu;
-  for (uint32_t j = 0; j < ni; j++) {  // elements of group j (reads of the source slots, coalesced)
-    const uint32_t sz = S.ssize[0][j] & 0x3fffffffu, st = S.sstart[0][j], fl = S.ssize[0][j] >> 30;
-    const uint32_t slot0 = st + S.sdelta[0][j];
-    const uint32_t* src = (fl & (kGrpAlt << 0)) ? B.sa2 : B.sa;
-    const uint32_t* srck = (fl & kGrpAlt) ? B.sk2 : B.sk;
-    const bool ident = fl & kGrpIdent;
-    const bool cached = S.scache[0][j] != 0;
-    for (uint32_t e = tid; e < sz; e += kPT) {
-      S.v[st + e] = ident ? e : src[slot0 + e];
-      S.key[st + e] = cached ? srck[slot0 + e] : 0u;
-      S.seg[st + e] = (uint8_t)j;
-    }
-  }
-  __syncthreads();
-  if (tid < ni) S.ssize[0][tid] &= 0x3fffffffu;
-  __syncthreads();
-  const Unit* __restrict__ units = B.units;
-  uint32_t cur_t = 0;
-  uint32_t npass = 0, nact = 0;
-  for (;;) {
-    const uint32_t nb = S.nbig[cur_t];
-    if (nb == 0) break;
-    if (O.dbg && tid == 0) {
-      npass++;
-      for (uint32_t j = 0; j < nb; j++) nact += S.ssize[cur_t][j];
-    }
-    for (uint32_t b = tid; b < nb * 256; b += kPT) S.cnt[b] = 0;
-    __syncthreads();
-    // ---- count: every element of a big segment takes its next character
-    uint32_t vv[kPPer], kk[kPPer], rk[kPPer];
-    uint8_t sg[kPPer];
-#pragma unroll
-    for (int i = 0; i < (int)kPPer; i++) {
-      const uint32_t p = i * kPT + tid;
-      sg[i] = p < n ? S.seg[p] : (uint8_t)0xff;
-      vv[i] = p < n ? S.v[p] : 0u;
-      kk[i] = p < n ? S.key[p] : 0u;
-    }
-    // refill empty caches: 4 characters from the text (loads issued before use)
-    uint32_t q[kPPer];
-#pragma unroll
-    for (int i = 0; i < (int)kPPer; i++) {
-      q[i] = 0;
-      if (sg[i] != 0xff && S.scache[cur_t][sg[i]] == 0) {
-        const uint32_t len = S.slen[cur_t][sg[i]];
-        q[i] = cyc_pos(vv[i], S.sdepth[cur_t][sg[i]], len);
-        kk[i] = ld_u32(B.text + S.stoff[cur_t][sg[i]] + q[i]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < (int)kPPer; i++) {
-      if (sg[i] != 0xff && S.scache[cur_t][sg[i]] == 0) {
-        const uint32_t len = S.slen[cur_t][sg[i]];
-        kk[i] = q[i] + 4 <= len ? __builtin_bswap32(kk[i]) : text_key4_wrap_long(B.text + S.stoff[cur_t][sg[i]], len, q[i]);
-      }
-      if (sg[i] != 0xff) rk[i] = atomicAdd(&S.cnt[sg[i] * 256u + (kk[i] >> 24)], 1u);
-    }
-    __syncthreads();
-    // ---- bins -> tile positions: one exclusive scan over all bins (segments are contiguous in
-    // the tile and listed in tile order, so a bin's base is its segment start plus the counts of
-    // the segment's lower bins = the scan minus the counts of the lower segments)
-    {
-      constexpr uint32_t kB = (kPSeg * 256 + kPT - 1) / kPT;
-      uint32_t c[kB], sum = 0;
-#pragma unroll
-      for (int x = 0; x < (int)kB; x++) {
-        const uint32_t b = tid * kB + x;
-        c[x] = b < nb * 256 ? S.cnt[b] : 0u;
-        sum += c[x];
-      }
-      uint32_t run = block_incl_sum(sum, S.sh, (uint32_t*)nullptr) - sum;
-#pragma unroll
-      for (int x = 0; x < (int)kB; x++) {
-        const uint32_t b = tid * kB + x;
-        if (b < nb * 256) S.cur[b] = run;
-        run += c[x];
-      }
-    }
-    __syncthreads();
-    // segment j's bins start at scan value sum_{j' < j} ssize[j']; shift to its tile start
-    if (tid < nb) S.segb[tid] = S.cur[tid * 256];
-    __syncthreads();
-    for (uint32_t b = tid; b < nb * 256; b += kPT) {
-      const uint32_t j = b >> 8;
-      S.cur[b] = S.cur[b] - S.segb[j] + S.sstart[cur_t][j];
-    }
-    __syncthreads();
-    // ---- classify the bins: settled (S2 / final / deep) or a big segment of the next pass
-    const uint32_t nxt = cur_t ^ 1u;
-    if (tid == 0) S.nbig[nxt] = 0;
-    __syncthreads();
-    for (uint32_t b = tid; b < nb * 256; b += kPT) {
-      const uint32_t c = S.cnt[b];
-      uint8_t ns = 0xfe;
-      if (c > kBig) {
-        const uint32_t j = b >> 8, d = S.sdepth[cur_t][j] + 1;
-        if (d < kDLds) {
-          const uint32_t k = atomicAdd(&S.nbig[nxt], 1u);  // < kPSeg: each holds > kBig of < kPE
-          S.sstart[nxt][k] = S.cur[b];
-          S.ssize[nxt][k] = c;
-          S.sdepth[nxt][k] = d;
-          S.scache[nxt][k] = S.scache[cur_t][j] ? S.scache[cur_t][j] - 1 : 3u;
-          S.sdelta[nxt][k] = S.sdelta[cur_t][j];
-          S.sunit[nxt][k] = S.sunit[cur_t][j];
-          S.stoff[nxt][k] = S.stoff[cur_t][j];
-          S.slen[nxt][k] = S.slen[cur_t][j];
-          ns = (uint8_t)k;
-        }
-      }
-      S.nseg[b] = ns;
-    }
-    __syncthreads();
-    // ---- move: every element of a big segment to its bucket position
-    uint32_t np[kPPer];
-#pragma unroll
-    for (int i = 0; i < (int)kPPer; i++) {
-      if (sg[i] == 0xff) continue;
-      const uint32_t b = sg[i] * 256u + (kk[i] >> 24);
-      np[i] = S.cur[b] + rk[i];
-      rk[i] = b;
-      S.v[np[i]] = vv[i];
-      S.key[np[i]] = kk[i] << 8;
-      S.seg[np[i]] = S.nseg[b] == 0xfe ? (uint8_t)0xff : S.nseg[b];
-    }
-    // ---- settle: finals, and the rotations of S2 / deep groups to the primary SA
-#pragma unroll
-    for (int i = 0; i < (int)kPPer; i++) {
-      if (sg[i] == 0xff) continue;
-      const uint32_t b = rk[i];
-      if (S.nseg[b] != 0xfe) continue;
-      const uint32_t j = b >> 8;
-      const uint32_t slot = np[i] + S.sdelta[cur_t][j];
-      if (S.cnt[b] == 1) {
-        const uint32_t u = S.sunit[cur_t][j];
-        emit_final(B, O, units[u], u, slot, vv[i], true);
-      } else {
-        B.sa[slot] = vv[i];
-      }
-    }
-    // one group record per bin of 2.. rotations (S2 record, or deep)
-    for (uint32_t b = tid; b < nb * 256; b += kPT) {
-      const uint32_t c = S.cnt[b];
-      if (c < 2 || S.nseg[b] != 0xfe) continue;
-      const uint32_t j = b >> 8;
-      const uint32_t d = S.sdepth[cur_t][j] + 1, slot = S.cur[b] + S.sdelta[cur_t][j];
-      if (c <= kBig) {
-        atomicAdd(&S.ccls[size_cls(c)], 1u);
-        const uint32_t x = atomicAdd(&S.ccls[7], 1u);
-        trec[2 * x] = slot;
-        trec[2 * x + 1] = (S.sunit[cur_t][j] << 16) | (d << 9) | c;
-      } else {  // still big at kDLds characters (rare): to the doubling fallback
-        O.deep[atomicAdd(O.n_deep, 1u)] = Grp{slot, c, S.sunit[cur_t][j], grp_flags(0u, d, 0u)};
-      }
-    }
-    __syncthreads();
-    cur_t = nxt;
-  }
-  __syncthreads();
-  // every class of the scan (6 and 7 stay empty: packed groups end in S2 or the deep list)
-  if (tid < (uint32_t)kNCls) ccnt[(size_t)tid * nTot + ibase + t] = tid < 6 ? S.ccls[tid] : 0u;
-  if (tid == 0) nrec[t] = S.ccls[7];
-  if (O.dbg && tid == 0) {
-    atomicAdd(&O.dbg[0], 1ull);
-    atomicAdd(&O.dbg[1], (unsigned long long)npass);
-    atomicAdd(&O.dbg[2], (unsigned long long)nact);
-    atomicMax(&O.dbg[3], (unsigned long long)npass);
-  }
-}
-
-// The records of k_s1p into the S2 class lists (class-major offsets from cscan); one wave per
-// tile (the order inside a tile is immaterial).
-__global__ void __launch_bounds__(kT) k_s1p_emit(const uint32_t* __restrict__ first, const uint32_t* __restrict__ P,
-                                                 uint32_t nT, const uint32_t* __restrict__ rec,
-                                                 const uint32_t* __restrict__ nrec, const uint32_t* __restrict__ cscan,
-                                                 uint32_t nTot, uint32_t ibase, ClsLists C) {
-  __shared__ uint32_t Wcc[kT / 64][8];
-  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
-  const uint32_t t = blockIdx.x * (kT / 64) + wv;
-  if (t >= nT) return;
-  const uint32_t i0 = first[t];
-  if (i0 == 0xffffffffu) return;
-  uint32_t* cc = Wcc[wv];
-  if (lane < 8) cc[lane] = 0;
-  wave_sync();
-  const uint32_t* trec = rec + P[i0];
-  const uint32_t m = nrec[t];
-  for (uint32_t x = lane; x < m; x += 64) {
-    const uint32_t slot = trec[2 * x], w = trec[2 * x + 1];
-    const uint32_t size = w & 511u, depth = (w >> 9) & 127u, unit = w >> 16;
-    const uint32_t cl = size_cls(size);
-    const uint32_t q = atomicAdd(&cc[cl], 1u);
-    C.l[cl][C.base[cl] + cscan[(size_t)cl * nTot + ibase + t] - cscan[(size_t)cl * nTot] + q] =
-        Grp{slot, size, unit, grp_flags(0u, depth, 0u)};
-  }
-}
-
 // out[c] = start of class c in the class-major scan (c < kNCls), out[kNCls] = total.
 __global__ void k_cls_bounds(const uint32_t* __restrict__ cscan, uint32_t nTot, const uint32_t* __restrict__ total,
                              uint32_t* __restrict__ out) {
@@ -1170,12 +856,6 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_split_pairs(const Grp* __
 // ---- tiny buckets: lane l takes rotation l % kW of bucket (64 / kW) * wave + l / kW.  Every step
 // compares the next 16 characters with the rotations of its bucket still tied with it
 // (same class, named by its first lane) and adds the smaller ones to its position.
-#ifndef BZG_TINY_SKIP
-#define BZG_TINY_SKIP 1
-#endif
-#ifndef BZG_TINY_SKIP8
-#define BZG_TINY_SKIP8 1
-#endif
 template <int kW>
 __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint32_t n_tiny, SortBufs B, SortOut O) {
   static_assert(kW == 2 || kW == 8, "lanes per bucket");
@@ -1243,7 +923,7 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
       }
       if (deep_now) break;
     }
-    if constexpr (kW == 2 && BZG_TINY_SKIP) {
+    if constexpr (kW == 2) {
       // a pair still tied after a step (long repeats) skips its common prefix 64 characters
       // at a time: both members' next 64 characters, exchanged with the partner lane by DPP,
       // compared word by word; the depth moves to the first differing word (the next 16-
@@ -1279,7 +959,7 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
       pos_step = true;
       if (__ballot(!done && d >= B.dwave_tiny)) continue;  // to the deep branch above
     }
-    if constexpr (kW == 8 && BZG_TINY_SKIP8) {
+    if constexpr (kW == 8) {
       // a bucket whose live members are all still tied with their classes after a step skips
       // the common prefix of all of them, 64 characters at a time: every live member compares
       // its next 64 characters with its class's first member (ds_bpermute), and the bucket
@@ -1442,10 +1122,6 @@ __global__ void __launch_bounds__(kT) k_deep_compact2(const Grp* __restrict__ sl
 // padded segment has fewer than 256 elements); later rounds give valid run starts < 0xff
 // there as well, and a run start 0xff would be a singleton, whose key is (position, 0).
 using BsortKey = uint64_t;
-// bit c (3..5): class c uses the compacted tail after its first round
-#ifndef BZG_S2_COMPACT
-#define BZG_S2_COMPACT 0
-#endif
 constexpr BsortKey kPadKey = ~0ull;
 
 __device__ __forceinline__ BsortKey make_key1(uint32_t hi, uint32_t lo, uint32_t idx) {
@@ -1462,14 +1138,9 @@ __device__ __forceinline__ bool key_less(BsortKey a, BsortKey b) { return a < b;
 
 
 
-// x from lane ^ J (J < 64), without the LDS pipe (BZG_XOR_DPP, default): DPP quad permutes
-// for 1 and 2; the half-row mirror (lane ^ 7 in 8) then the quad reverse (^ 3) for 4; a row
-// rotation by 8 (lane ^ 8 in a 16-lane row) for 8; gfx950's permlane16 / permlane32 swaps for
-// 16 and 32 (a swap of x with itself hands every row / half its partner's copy in one of the
-// two results).  BZG_XOR_DPP=0: ds_swizzle within 32 lanes, ds_bpermute across.
-#ifndef BZG_XOR_DPP
-#define BZG_XOR_DPP 0
-#endif
+// x from lane ^ J (J < 64): DPP quad permutes for 1 and 2, ds_swizzle within 32 lanes,
+// ds_bpermute across (DPP / permlane forms for 4..32 measured no faster: the issue stall of the
+// network is its dependency chain, profiles/r04_ab_xor_dpp.txt).
 __device__ __forceinline__ bool lane_in(uint64_t mask) { return __builtin_amdgcn_inverse_ballot_w64(mask); }
 template <int J>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
@@ -1477,17 +1148,6 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
   } else if constexpr (J == 2) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
-  } else if constexpr (BZG_XOR_DPP && J == 4) {
-    const int y = __builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    return (uint32_t)__builtin_amdgcn_mov_dpp(y, 0x1B, 0xF, 0xF, false);      // [3,2,1,0]
-  } else if constexpr (BZG_XOR_DPP && J == 8) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
-  } else if constexpr (BZG_XOR_DPP && J == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    return lane_in(0x0000ffff0000ffffull) ? r[1] : r[0];  // even rows: the odd row's copy
-  } else if constexpr (BZG_XOR_DPP && J == 32) {
-    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    return lane_in(0x00000000ffffffffull) ? r[1] : r[0];  // low half: the high half's copy
   } else if constexpr (J < 32) {
     return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (J << 10) | 0x1F);
   } else {
@@ -1563,21 +1223,10 @@ __device__ __forceinline__ void bitonic(BsortKey (&K)[kPer]) {
 // odd-even transposition sort over the whole segment needs as many steps as the longest run,
 // a handful of compare-exchanges with the neighbouring position each, against a full bitonic
 // network (21..36 stages).  Positions p = lane * kPer + r; kSeg = 64 (no segment edges).
-// 1: the one-group-per-wave classes gather 16 characters in their first round (the second
-// round's keys come from LDS instead of a second dependent gather)
-#ifndef BZG_S2_PRE
-#define BZG_S2_PRE 1
-#endif
-// the same two for the several-groups-per-wave classes (9..32)
-#ifndef BZG_S2_PRE_SEG
-#define BZG_S2_PRE_SEG 1
-#endif
-#ifndef BZG_OETS_SEG
-#define BZG_OETS_SEG 1
-#endif
-#ifndef BZG_OETS_MAX
-#define BZG_OETS_MAX 16
-#endif
+// Every class gathers 16 characters in its first round (the second round's keys come from LDS
+// instead of a second dependent gather).  Rounds after the first whose longest tied run is at
+// most kOetsMax use odd-even transposition steps instead of the bitonic network.
+constexpr uint32_t kOetsMax = 16;
 __device__ __forceinline__ void key_ce(BsortKey& a, BsortKey& b) {
   const bool sw = key_less(b, a);
   const BsortKey x = a, y = b;
@@ -1654,9 +1303,6 @@ __device__ __forceinline__ void oets(BsortKey (&K)[kPer], uint32_t steps) {
 // sorted by a 64-key network (21 stages instead of 28 / 36) and put back.  The tied runs keep
 // their places (their keys lead with the run start), so the packed order maps back 1:1.
 // Returns false (nothing done) when more than 64 are tied.
-#ifndef BZG_S2_CSORT
-#define BZG_S2_CSORT 1
-#endif
 template <int kPer>
 __device__ __forceinline__ bool compact_sort(BsortKey (&K)[kPer], const bool (&done)[kPer], uint64_t* X) {
   uint32_t mine = 0;
@@ -1689,12 +1335,7 @@ __device__ __forceinline__ bool compact_sort(BsortKey (&K)[kPer], const bool (&d
 // sorting round: every member's next 64 characters are compared with those of the first
 // member (lane 0, register 0), word by word; the depth moves to the first word where some
 // member differs.  Stops at `limit` and where a member's window wraps past the unit end.
-#ifndef BZG_S2_SKIP
-#define BZG_S2_SKIP 1
-#endif
-#ifndef BZG_S2_EARLY
-#define BZG_S2_EARLY 2  // emitting classes: rounds after which runs of at most two are emitted (0: never)
-#endif
+constexpr int kS2Early = 2;  // emitting classes: rounds after which runs of at most two are emitted
 template <int kPer>
 __device__ __forceinline__ uint32_t common_depth(const uint8_t* t, uint32_t len, const uint32_t (&v)[kPer],
                                                  const bool (&live)[kPer], uint32_t depth, uint32_t limit) {
@@ -1845,109 +1486,6 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, ui
 }
 
 
-// Compacted tail of the one-group-per-wave classes: after the first bitonic round most
-// rotations are final (text: about 80%) and the tied ones form short runs.  When at most 64
-// are tied, they are packed into one lane each (LDS, in sorted order, so every run is a range
-// of lanes) and ranked inside their run on 16 characters per step, as in bsort_tail, instead
-// of re-sorting the whole segment.  Returns false (nothing done) when more than 64 are tied.
-struct S2Compact {
-  uint32_t v[64], p[64], rl[64];
-  uint4 key[64];
-  uint32_t cls[64];
-  uint8_t c[64];
-};
-template <int kPer>
-__device__ bool bsort_compact_tail(const SortBufs& B, const SortOut& O, const Grp& g, const Unit& U, uint32_t depth,
-                                   const BsortKey (&K)[kPer], const bool (&done)[kPer], const bool (&tn)[kPer],
-                                   const uint32_t (&rsn)[kPer], const uint32_t* Lv, const uint8_t* Lc,
-                                   S2Compact& C) {
-  const uint32_t lane = __lane_id();
-  bool tied[kPer];
-  uint32_t mine = 0;
-#pragma unroll
-  for (int r = 0; r < kPer; r++) {
-    tied[r] = key_valid(K[r]) && !done[r];
-    mine += tied[r] ? 1u : 0u;
-  }
-  const uint32_t incl = wave_incl_sum(mine);
-  const uint32_t nt = (uint32_t)__shfl((int)incl, 63, 64);
-  if (nt > 64) return false;
-  uint32_t ci = incl - mine;
-#pragma unroll
-  for (int r = 0; r < kPer; r++) {
-    if (!tied[r]) continue;
-    const uint32_t p = lane * kPer + r, idx = key_idx(K[r]);
-    C.v[ci] = Lv[idx];
-    C.c[ci] = Lc[idx];
-    C.p[ci] = (rsn[r] << 16) | p;
-    if (!tn[r]) C.rl[ci - (p - rsn[r])] = p - rsn[r] + 1;  // run length at the run's first lane
-    ci++;
-  }
-  wave_sync();
-  const uint8_t* t = B.text + U.toff;
-  bool live = lane < nt;
-  uint32_t v = 0, pos = 0, cls = 0xffffffffu, cst = 0, rl = 0;
-  uint8_t lastc = 0;
-  if (live) {
-    v = C.v[lane];
-    lastc = C.c[lane];
-    const uint32_t pp = C.p[lane], rs = pp >> 16;
-    cst = lane - ((pp & 0xffffu) - rs);
-    rl = C.rl[cst];
-    pos = rs;
-    cls = cst;
-  }
-  for (;;) {
-    if (__ballot(live) == 0) break;
-    const bool deep = depth >= B.dwave;
-    uint32_t k[4] = {0u, 0u, 0u, 0u};
-    if (live && !deep) text_key16(t, U.len, cyc_pos(v, depth, U.len), k);
-    C.key[lane] = make_uint4(k[0], k[1], k[2], k[3]);
-    C.cls[lane] = live ? cls : 0xffffffffu;
-    wave_sync();
-    if (deep) {  // still tied after B.dwave characters: leave to the doubling fallback
-      uint32_t rank = 0, cnt = 0;
-      if (live)
-        for (uint32_t q = cst; q < cst + rl; q++)
-          if (C.cls[q] == cls) {
-            cnt++;
-            rank += q < lane;
-          }
-      if (live) B.sa[g.start + pos + rank] = v;
-      const uint32_t ds = wave_append(O.n_deep, live && rank == 0);
-      if (live && rank == 0) O.deep[ds] = Grp{g.start + pos, cnt, g.unit, grp_flags(0u, depth, 2u)};
-      break;
-    }
-    if (live) {
-      const uint64_t mh = ((uint64_t)k[0] << 32) | k[1], ml = ((uint64_t)k[2] << 32) | k[3];
-      uint32_t lt = 0, eq = 0, rep = 0xffffffffu;
-      for (uint32_t q = cst; q < cst + rl; q++) {
-        if (C.cls[q] != cls) continue;
-        const uint4 o = C.key[q];
-        const uint64_t oh = ((uint64_t)o.x << 32) | o.y, ol = ((uint64_t)o.z << 32) | o.w;
-        lt += (oh < mh) || (oh == mh && ol < ml);
-        if (oh == mh && ol == ml) {
-          if (rep == 0xffffffffu) rep = q;
-          eq++;
-        }
-      }
-      pos += lt;
-      cls = rep;
-      if (eq == 1) {
-        live = false;
-        const uint32_t slot = g.start + pos;
-        B.sa[slot] = v;
-        const uint32_t rr = slot - U.sbase;
-        if (U.k == 1) O.bwt[U.toff + rr] = lastc;
-        if (v == 0) O.rank0[g.unit] = rr;
-      }
-    }
-    wave_sync();
-    depth += 16;
-  }
-  return true;
-}
-
 // S2 run emission (classes with one group per wave): after kRounds rounds the runs still tied
 // are left as new groups.  Their rotations are stored at their slots (primary SA) and each run
 // becomes a record (depth:15 | run start:8 | size:9) in the group's own part of `rec` (from
@@ -1973,9 +1511,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   __shared__ uint32_t Lk[kT / 64][kEmit ? 8 : kE];
   __shared__ uint4 TK[kT / 64][kTE];
   __shared__ uint32_t TC[kT / 64][kTE];
-  constexpr bool kCompact = kEmit && ((BZG_S2_COMPACT >> (kPer == 1 ? 3 : kPer == 2 ? 4 : 5)) & 1);
-  __shared__ S2Compact SC[kCompact ? kT / 64 : 1];
-  constexpr bool kPre = (kEmit || BZG_S2_PRE_SEG) && BZG_S2_PRE;
+  constexpr bool kPre = true;
   __shared__ uint64_t Lx[kT / 64][kPre ? kE : 1];  // characters depth + 7 .. + 14 (second-round keys)
   const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
   const uint32_t sl = lane % kSeg;
@@ -2083,9 +1619,9 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         atomicAdd(&O.dbg[64 + 16 * (kDbgCls - 3) + 8 + bk(nt)], 1ull);
       }
     }
-    if ((kSeg == 64 || BZG_OETS_SEG) && BZG_OETS_MAX > 0 && round > 0 && maxrun <= BZG_OETS_MAX)
+    if (round > 0 && maxrun <= kOetsMax)
       oets<kSeg, kPer>(K, maxrun);
-    else if (!(kSeg == 64 && kPer > 1 && kPre && BZG_S2_CSORT && round > 0 && compact_sort<kPer>(K, done, Lx[w])))
+    else if (!(kSeg == 64 && kPer > 1 && kPre && round > 0 && compact_sort<kPer>(K, done, Lx[w])))
       bitonic<kSeg, kPer>(K);
     // ties with the previous / next position of the segment (same run start and key)
     bool tp[kPer], tn[kPer];
@@ -2143,7 +1679,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
     }
     if (__ballot(any_tied) == 0) break;
     depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
-    if constexpr (kSeg == 64 && kPer <= 2 && BZG_S2_SKIP) {  // (kPer 4: the registers would cost a wave per SIMD)
+    if constexpr (kSeg == 64 && kPer <= 2) {  // (kPer 4: the registers would cost a wave per SIMD)
       bool split = false;  // the group is no longer one run
 #pragma unroll
       for (int r = 0; r < kPer; r++) split |= key_valid(K[r]) && (done[r] || rsn[r] != 0);
@@ -2160,20 +1696,17 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         depth = d2;
       }
     }
-    if constexpr (kCompact) {
-      if (depth < B.dwave && bsort_compact_tail<kPer>(B, O, g, U, depth, K, done, tn, rsn, Lv[w], Lc[w], SC[w])) break;
-    }
-    if constexpr (kSeg == 64 || BZG_OETS_SEG) {  // longest tied run (next round's network; early emission)
+    {  // longest tied run (next round's network; early emission)
       uint32_t ml = 0;
 #pragma unroll
       for (int r = 0; r < kPer; r++)
         if (key_valid(K[r]) && !done[r] && !tn[r]) ml = max(ml, sl * kPer + r - rsn[r] + 1);
       maxrun = (uint32_t)__builtin_amdgcn_readlane((int)seg_incl_max<64>(ml), 63);
     }
-    // only pairs still tied after BZG_S2_EARLY rounds (long repeats: the pairs of a copied
+    // only pairs still tied after kS2Early rounds (long repeats: the pairs of a copied
     // passage stay tied round after round): emitted now, as the pair lists' 64-character skip
     // (k_tiny<2>) resolves or deepens them far cheaper than further rounds of the whole network
-    const bool early = kEmit && BZG_S2_EARLY > 0 && round + 1 >= BZG_S2_EARLY && maxrun <= 2;
+    const bool early = kEmit && round + 1 >= kS2Early && maxrun <= 2;
     if (++round >= kRounds || depth >= B.dwave || early) {
       if constexpr (kEmit) {
         static_assert(kSeg == 64, "one group per wave");
@@ -2717,7 +2250,7 @@ __global__ void __launch_bounds__(kT) k_qsa(const QBlock* __restrict__ qb, const
 // ------------------------------------------------------------------------------------
 void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& h_boff,
                const std::vector<uint32_t>& h_period, uint8_t* bwt, uint32_t* rank0, SortStats* stats,
-               hipStream_t st, const uint32_t* h_qper, const std::function<void()>* s1_done) {
+               hipStream_t st, const uint32_t* h_qper) {
   const uint32_t nb = r.nblocks;
   if (nb == 0) return;
   if (nb > 0xffffu) throw HipFailure(hipErrorInvalidValue);  // S2 keys carry 16-bit unit ids
@@ -2776,18 +2309,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   B.sk2 = ws.u32("sort_sk2", S + 16);
   B.text = r.blk;
   B.units = units;
-  {
-    static const uint32_t dwave = [] {
-      const char* e = getenv("BZG_DWAVE");
-      return e ? (uint32_t)std::max(16, atoi(e)) : 256u;  // tuned: profiles/r02_dwave_sweep.txt
-    }();
-    B.dwave = dwave;
-    static const uint32_t dwave_tiny = [] {
-      const char* e = getenv("BZG_DWAVE_TINY");
-      return e ? (uint32_t)std::max(16, atoi(e)) : dwave;
-    }();
-    B.dwave_tiny = dwave_tiny;
-  }
+  B.dwave = 256;  // S2 -> S3 handoff depth (profiles/r02_dwave_sweep.txt; 64 / 128 measured slower in round 4)
+  B.dwave_tiny = 256;
   // class lists: a class-c bucket holds more than kClsMax[c-1] rotations
   ClsLists C{};
   size_t ccap[kNCls];
@@ -2825,7 +2348,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* first = ws.u32("sort_first", max_ptiles);
   uint32_t* last = ws.u32("sort_last", max_ptiles);
   uint32_t* nrec = ws.u32("sort_nrec", max_ptiles);
-  uint32_t* srec = ws.u32("sort_rec", S + 64);  // packed-pass group records (k_s1p: 2 words per group)
+  uint32_t* srec = ws.u32("sort_rec", S + 64);  // bucket records of the packed passes and of S2
   uint32_t* scratch =
       ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[6])) + 64);
   uint32_t hc[48];
@@ -2848,10 +2371,6 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       fprintf(stderr, "[bzg check] %s iter %d class %d: %u bad groups of %u; first start %u size %u unit %u depth %u flags %u\n",
               what, it, cls, h[0], n, h[1], h[2], h[3], h[4] >> kGrpDepthShift, h[4] & 31u);
   };
-  static const bool use_s1p = [] {  // 1: packed groups finished in LDS (k_s1p); default: one pass per kernel (k_s1s)
-    const char* e = getenv("BZG_S1P");
-    return e && atoi(e) != 0;
-  }();
 
   HIP_OK(hipMemsetAsync(cnt, 0, 64 * 4, st));
   k_init_units<<<grid(nb), kT, 0, st>>>(units, nb, B, O, C, cnt);
@@ -2895,10 +2414,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipMemsetAsync(first, 0xff, (size_t)nT * 4, st));
       k_tile_first<<<grid(n6), kT, 0, st>>>(P, n6, first, last);
       HIP_OK(hipGetLastError());
-      if (use_s1p)
-        k_s1p<<<nT, kPT, 0, st>>>(cur6, first, last, P, B, O, srec, nrec, ccnt, nTot, n7, nT);
-      else
-        k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, gunits, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
+      k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, gunits, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
       HIP_OK(hipGetLastError());
     }
     if (n7) {
@@ -2922,10 +2438,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     if (nT) {
-      if (use_s1p)
-        k_s1p_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(first, P, nT, srec, nrec, ccnt, nTot, n7, Cp);
-      else
-        k_s1s_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(cur6, first, last, P, nT, O, srec, nrec, ccnt, nTot, n7, Cp);
+      k_s1s_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(cur6, first, last, P, nT, O, srec, nrec, ccnt, nTot, n7, Cp);
       HIP_OK(hipGetLastError());
     }
     read_counters();
@@ -2935,13 +2448,6 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     std::swap(cur6, nxt6);
     std::swap(cur7, nxt7);
   }
-  if (s1_done) (*s1_done)();  // (read_counters above synchronised the stream)
-  if (debug && O.dbg) {
-    unsigned long long d[4];
-    HIP_OK(hipMemcpyAsync(d, O.dbg, sizeof(d), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    fprintf(stderr, "[bzg sort S1] k_s1p tiles=%llu passes=%llu (max %llu) element-passes=%llu\n", d[0], d[1], d[3], d[2]);
-  }
   // ---- S2: every size class
   if (debug)
     fprintf(stderr, "[bzg sort S2] buckets by class: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", ncls[0],
@@ -2949,15 +2455,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   // bitonic rounds before the rank-counting tail (classes 1, 2) or before the still-tied runs
   // are emitted as new groups (classes 3..5, one group per wave; the S2 loop repeats until
   // every list is empty)
-#ifndef BZG_R5
-#define BZG_R5 2
-#endif
-#ifndef BZG_R4
-#define BZG_R4 2
-#endif
-#ifndef BZG_R3
-#define BZG_R3 8
-#endif
+  constexpr int kR3 = 8, kR4 = 2, kR5 = 2;  // (profiles/r03_*, r04_*: 3 or 4 rounds for class 3 slower)
   {
     ClsLists N{};
     for (int c = 0; c < 6; c++) N.l[c] = ws.typed<Grp>("sort_s2n" + std::to_string(c), ccap[c]);
@@ -2965,14 +2463,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       // A list of more than S / 32 groups (high-entropy input: millions of small
       // buckets, most of them settled by their first 16 characters) stays as it is: its
       // reorder would cost more than the L2 locality it buys.
-      static const uint64_t reorder_div = [] {
-        const char* e = getenv("BZG_S2_REORDER_DIV");
-        return e ? (uint64_t)std::max(0, atoi(e)) : 32u;
-      }();
+      constexpr uint64_t reorder_div = 32;  // profiles/r04_ab_s2_reorder.txt
       uint32_t* ucnt = ws.u32("sort_ucnt", nb + 64);
       for (int c = 0; c < 6; c++) {
         if (ncls[c] < 2) continue;
-        if (reorder_div && (uint64_t)ncls[c] * reorder_div > S) continue;
+        if ((uint64_t)ncls[c] * reorder_div > S) continue;
         HIP_OK(hipMemsetAsync(ucnt, 0, 4 * (size_t)nb, st));
         k_unit_count<<<grid(ncls[c]), kT, 0, st>>>(C.l[c], ncls[c], ucnt);
         HIP_OK(hipGetLastError());
@@ -3039,11 +2534,11 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       if (total == 0) break;
       HIP_OK(hipMemsetAsync(ccnt2, 0, (6 * (size_t)total + 1) * 4, st));
       S2Emit E{srec, ccnt2, total, 0};
-      if (ncls[3]) k_bsort<64, 1, BZG_R3, false, true><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O, E);
+      if (ncls[3]) k_bsort<64, 1, kR3, false, true><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O, E);
       E.gbase += ncls[3];
-      if (ncls[4]) k_bsort<64, 2, BZG_R4, true, true><<<ceil_div(ncls[4], kT / 64), kT, 0, st>>>(C.l[4], ncls[4], B, O, E);
+      if (ncls[4]) k_bsort<64, 2, kR4, true, true><<<ceil_div(ncls[4], kT / 64), kT, 0, st>>>(C.l[4], ncls[4], B, O, E);
       E.gbase += ncls[4];
-      if (ncls[5]) k_bsort<64, 4, BZG_R5, false, true><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O, E);
+      if (ncls[5]) k_bsort<64, 4, kR5, false, true><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O, E);
       HIP_OK(hipGetLastError());
       scan_u32(ScanOp::Sum, true, ccnt2, ccnt2, 6 * (size_t)total + 1, nullptr, scratch2, st);
       S2Lists Ls{{C.l[3], C.l[4], C.l[5]}, {0, ncls[3], ncls[3] + ncls[4], total}};
@@ -3122,12 +2617,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     }
     k_fb_copy<<<grid(n_deep), kT, 0, st>>>(O.deep, n_deep, L0, B);
     HIP_OK(hipGetLastError());
-    static const bool pairs = [] {
-      const char* e = getenv("BZG_S3_PAIRS");
-      return !e || atoi(e) != 0;
-    }();
     uint32_t n_left = n_deep;
-    if (pairs) {  // deep pairs by their run's first mismatch (k_pair_resolve)
+    {  // deep pairs by their run's first mismatch (k_pair_resolve)
       const uint32_t nu = (uint32_t)fb_units.size();
       std::vector<uint32_t> htb(nu + 1, 0u), huo(nb, 0u);
       uint32_t maxt = 0;
@@ -3209,11 +2700,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
               (unsigned long long)hist[4], fb_units.size(), h0);
     }
     doubling_sort(ws, B, L0, n_left, h0, &dbl_iters, &dbl_elems, st);
-    if (getenv("BZG_FULL_UNIT_OUT")) {
-      k_unit_out<<<dim3(ceil_div(flen, kT), (unsigned)fb_units.size()), kT, 0, st>>>(ulist, units, B.sa, r.blk, bwt);
-    } else {
-      k_deep_out<<<grid(n_left), kT, 0, st>>>(L0, n_left, units, B.sa, r.blk, bwt);
-    }
+    k_deep_out<<<grid(n_left), kT, 0, st>>>(L0, n_left, units, B.sa, r.blk, bwt);
     HIP_OK(hipGetLastError());
     k_rank0_isa<<<grid(fb_units.size()), kT, 0, st>>>(ulist, (uint32_t)fb_units.size(), units, B.isa, rank0);
     HIP_OK(hipGetLastError());

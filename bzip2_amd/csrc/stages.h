@@ -113,12 +113,9 @@ struct SortStats {
   int s2_iters = 0;             // S2 rounds of run emission
 };
 // h_qper (optional): r.qper on the host; those blocks are ordered analytically (qsa.h).
-// s1_done (optional): called on the host once the S1 byte passes have been queued and have
-// finished (the S2 register sorts follow).
 void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& h_boff,
                const std::vector<uint32_t>& h_period, uint8_t* bwt, uint32_t* rank0,
-               SortStats* stats, hipStream_t st, const uint32_t* h_qper = nullptr,
-               const std::function<void()>* s1_done = nullptr);
+               SortStats* stats, hipStream_t st, const uint32_t* h_qper = nullptr);
 
 // ---- stage A6 ------------------------------------------------------------------------
 struct MtfResult {
