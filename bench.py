@@ -39,7 +39,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--bytes", type=int, default=1_000_000_000, help="input bytes per GPU")
+    p.add_argument("--bytes", type=int, default=1_000_000_000, help="input bytes per GPU (weak scaling)")
+    p.add_argument("--total-bytes", type=int, default=0,
+                   help="strong scaling: ONE stream of this many bytes split into N contiguous shards, one per "
+                        "rank (BASELINE config 3: --total-bytes 1000000000); implies --mode stream")
     p.add_argument("--level", type=int, default=9)
     p.add_argument("--cpu-sample", type=int, default=300_000_000, help="bytes for the CPU reference timing")
     p.add_argument("--no-cpu", action="store_true")
@@ -73,6 +76,25 @@ def job_mbps(bytes_per_rank: int, world: int, steps: int, elapsed: float) -> flo
 def rank_seed(rank: int) -> int:
     """Each rank compresses its own synthetic object (weak scaling, no shared input)."""
     return 0x5EED0001 + rank
+
+
+def shard_bounds(total: int, world: int, rank: int) -> tuple:
+    """Strong scaling: rank r holds input[total * r // world, total * (r + 1) // world) of the one
+    job input (contiguous, in rank order, sizes differing by at most one byte)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+def job_layout(a, world: int, rank: int) -> dict:
+    """What this rank compresses.  Weak (default): its own a.bytes (one shard of a stream of world x
+    a.bytes bytes in stream mode, or an independent stream).  Strong (--total-bytes T): shard
+    `rank` of ONE stream of T bytes (BASELINE config 3 at T = 1e9)."""
+    if a.total_bytes:
+        lo, hi = shard_bounds(a.total_bytes, world, rank)
+        return {"scaling": "strong", "mode": "stream", "lo": lo, "n": hi - lo, "job_bytes": a.total_bytes,
+                "seed": rank_seed(0)}
+    mode = a.mode or ("stream" if world > 1 else "independent")
+    return {"scaling": "weak", "mode": mode, "lo": rank * a.bytes, "n": a.bytes, "job_bytes": world * a.bytes,
+            "seed": rank_seed(rank)}
 
 
 def launch_cmd(argv, n: int, port: int) -> list:
@@ -115,9 +137,13 @@ def main():
         print(f"bench.py: world size {world} != --gpus {a.gpus}", file=sys.stderr)
         sys.exit(2)
     if os.environ.get("BZG_BENCH_PROBE") == "1":  # launcher test (CPU): report the rank layout only
-        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world,
-                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
-                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+        r = int(os.environ.get("RANK", "0"))
+        probe = {"rank": r, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                 "master": os.environ.get("MASTER_ADDR")}
+        if a.total_bytes:
+            lay = job_layout(a, world, r)
+            probe.update(scaling=lay["scaling"], mode=lay["mode"], lo=lay["lo"], n=lay["n"], job_bytes=lay["job_bytes"])
+        print(json.dumps(probe), flush=True)
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -125,7 +151,9 @@ def main():
     if os.environ.get("BZG_DIST_BACKEND") == "gloo":  # rehearsal: every rank on the box's one GPU
         local = 0
     torch.cuda.set_device(local)
-    mode = a.mode or ("stream" if world > 1 else "independent")
+    lay = job_layout(a, world, rank)
+    mode = lay["mode"]
+    strong = lay["scaling"] == "strong"
     if dist:
         backend = os.environ.get("BZG_DIST_BACKEND", "nccl")  # gloo: multi-rank rehearsal on one GPU
         if backend == "nccl":
@@ -134,7 +162,10 @@ def main():
             torch.distributed.init_process_group(backend)
 
     t0 = time.time()
-    data = datagen.text(a.bytes, rank_seed(rank))
+    if strong:  # every rank makes the one job input and keeps its shard
+        data = datagen.text(a.total_bytes, lay["seed"])[lay["lo"]:lay["lo"] + lay["n"]]
+    else:
+        data = datagen.text(a.bytes, lay["seed"])
     gen_s = time.time() - t0
     d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
     if a.repeat_frac > 0:
@@ -151,7 +182,7 @@ def main():
         if mode == "stream":
             from bzip2_amd import shard
 
-            res = shard.compress_sharded(d_in, rank * a.bytes, world * a.bytes, a.level)
+            res = shard.compress_sharded(d_in, lay["lo"], lay["job_bytes"], a.level)
             last_stream[0] = res
             return res.numel() / world if res is not None else 0  # per-rank share of the one stream
         nb, cons, _ = B.compress_device(d_in.data_ptr(), len(data), a.level, d_out.data_ptr(), cap, stream_ptr=sp)
@@ -178,16 +209,32 @@ def main():
         elapsed = max_over_ranks(elapsed, "cuda")
     stats = B.last_stats()
     ms_per_step = elapsed * 1000.0 / a.steps
-    value = job_mbps(a.bytes, world, a.steps, elapsed)  # MB/s, whole job
+    value = lay["job_bytes"] * a.steps / elapsed / 1e6  # MB/s, whole job (= job_mbps(a.bytes, world, ...) when weak)
+    phases = None
+    if mode == "stream":  # one more step, untimed, with a synchronisation after each phase
+        from bzip2_amd import shard
+
+        shard.compress_sharded(d_in, lay["lo"], lay["job_bytes"], a.level, timing=True)
+        tm = dict(shard.last_timing)
+        prev, phases = 0.0, {}
+        for k in ("map", "chain", "halo", "compress", "gather", "trailer"):
+            if k in tm:
+                phases[k] = round((tm[k] - prev) * 1e3, 3)
+                prev = tm[k]
+        if dist:
+            allp = [None] * world
+            torch.distributed.all_gather_object(allp, phases)
+            phases = {"rank%d" % r: p for r, p in enumerate(allp)}
 
     if mode == "stream" and rank != 0:
         stream_parity(None, d_in, a, world)  # sends this rank's shard to rank 0
         stream_ref_check(d_in, a, world)
     if rank == 0:
-        ratio = out_bytes / a.bytes
-        rho = stats["rle_bytes"] / a.bytes
+        nbytes = lay["n"] if not (mode == "stream") else lay["job_bytes"] / world  # per-rank share
+        ratio = out_bytes / nbytes
+        rho = stats["rle_bytes"] / lay["n"]
         b_alg = 1.0 + 25.0 * rho + 3.0 * ratio
-        achieved = a.bytes * b_alg / (ms_per_step / 1000.0) / 1e9
+        achieved = lay["job_bytes"] / world * b_alg / (ms_per_step / 1000.0) / 1e9
         bwt_alg = 11.0 * stats["rle_bytes"]  # read T + write SA + read SA + gather T + write L
         result = {
             "metric": METRIC,
@@ -198,14 +245,17 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": lay["scaling"],
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": f"enwik9-class synthetic text (tests/datagen.py), {a.bytes} B per GPU, -{a.level}",
-                       "level": a.level, "bytes_per_gpu": a.bytes, "blocks": stats["nblocks"],
+            "config": {"workload": (f"BASELINE config 3: enwik9-class synthetic text (tests/datagen.py), ONE stream of "
+                                    f"{a.total_bytes} B split over {world} rank(s), -{a.level}") if strong else
+                                   f"enwik9-class synthetic text (tests/datagen.py), {a.bytes} B per GPU, -{a.level}",
+                       "level": a.level, "bytes_per_gpu": lay["n"], "job_bytes": lay["job_bytes"],
+                       "blocks": stats["nblocks"],
                        "bz2_ratio": round(ratio, 4), "rle1_rho": round(rho, 4),
-                       "parallelism": (f"one stream of {world} x {a.bytes} B sharded over {world} ranks "
+                       "parallelism": (f"one stream of {lay['job_bytes']} B sharded over {world} ranks "
                                        "(RCCL cut chain, P2P halo, bitstream gather to rank 0)")
                        if mode == "stream" else f"{world} independent streams"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -219,14 +269,14 @@ def main():
                                             if stage_ms["bwt"] > 0 else None}},
             "stages_ms": {k: round(v, 3) for k, v in stage_ms.items()},
             "sort_iterations": stats["sort_iterations"],
-            **({"shard_timing_s": __import__("bzip2_amd.shard", fromlist=["x"]).last_timing}
-               if mode == "stream" and os.environ.get("BZG_SHARD_TIMING") == "1" else {}),
+            **({"phases_ms": phases, "phases_note": "one extra untimed step synchronised after each phase of "
+                                                     "compress_sharded (bzip2_amd/shard.py)"} if phases else {}),
             "gen_s": round(gen_s, 1),
         }
         if mode == "stream" and last_stream[0] is not None:
             result["stream_check"] = stream_parity(last_stream[0], d_in, a, world)
             result["stream_check"]["reference"] = stream_ref_check(d_in, a, world)
-        pmc = pmc_traffic(a)
+        pmc = pmc_traffic(a) if not strong and mode == "independent" else None
         if pmc is not None:
             rl = result["roofline"]
             rl["traffic"] = round(pmc["traffic_B_per_step"] / (ms_per_step / 1e3) / 1e9, 2)
@@ -234,7 +284,7 @@ def main():
                                   f"workload ({pmc['file']}, {pmc['correction']}; uncorrected "
                                   f"{pmc['traffic_lower_B_per_step'] / 1e9:.1f} GB) over this run's step time")
             rl["traffic_B_per_step"] = round(pmc["traffic_B_per_step"])
-        if not a.no_h2h:
+        if not a.no_h2h and not strong:
             result["host_to_host"] = host_to_host(data, a, cap)
         if not a.no_cpu:
             result.update(cpu_and_parity(data, a, d_in))
@@ -257,26 +307,28 @@ def stream_parity(stream, d_in, a, world):
     if rank != 0:
         dist.send(d_in.cpu() if gloo else d_in, 0)
         return None
-    n = a.bytes
-    full = torch.empty(n * world, dtype=torch.uint8, device="cuda")
-    full[:n].copy_(d_in)
+    lays = [job_layout(a, world, r) for r in range(world)]
+    total = lays[0]["job_bytes"]
+    full = torch.empty(total, dtype=torch.uint8, device="cuda")
+    full[:lays[0]["n"]].copy_(d_in)
     for r in range(1, world):
+        lo, n = lays[r]["lo"], lays[r]["n"]
         if gloo:
             tmp = torch.empty(n, dtype=torch.uint8)
             dist.recv(tmp, r)
-            full[r * n:(r + 1) * n].copy_(tmp)
+            full[lo:lo + n].copy_(tmp)
         else:
-            dist.recv(full[r * n:(r + 1) * n], r)
-    cap = B.bound(n * world)
+            dist.recv(full[lo:lo + n], r)
+    cap = B.bound(total)
     out = torch.empty(cap, dtype=torch.uint8, device="cuda")
-    nb, _, _ = B.compress_device(full.data_ptr(), n * world, a.level, out.data_ptr(), cap)
+    nb, _, _ = B.compress_device(full.data_ptr(), total, a.level, out.data_ptr(), cap)
     torch.cuda.synchronize()
     s = stream.to("cuda")
     eq = nb == s.numel() and bool(torch.equal(out[:nb], s))
     del full, out
     torch.cuda.empty_cache()
     return {"bytes": int(s.numel()), "ranks": world, "equals_single_device_stream": eq,
-            "against": f"bzg_compress_device over all {n * world} B on one device"}
+            "against": f"bzg_compress_device over all {total} B on one device"}
 
 
 def stream_ref_check(d_in, a, world, per_rank: int = 3_000_000):
@@ -289,7 +341,7 @@ def stream_ref_check(d_in, a, world, per_rank: int = 3_000_000):
 
     rank = dist.get_rank() if world > 1 else 0
     gloo = world > 1 and dist.get_backend() == "gloo"
-    k = min(per_rank, d_in.numel())
+    k = min(per_rank, min(job_layout(a, world, r)["n"] for r in range(world)))  # the same on every rank
     piece = d_in[:k].contiguous()
     res = shard.compress_sharded(piece, rank * k, world * k, a.level)
     if rank != 0:

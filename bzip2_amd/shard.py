@@ -30,7 +30,6 @@ The GPU backend is the product path; tests inject a CPU stand-in backend (gloo, 
 from __future__ import annotations
 
 import ctypes
-import os
 import time
 
 import torch
@@ -41,15 +40,15 @@ from . import BZG_FLAG_END_SEGMENT, BZG_FLAG_TAIL_MERGE, bound, bzg_stream_state
 
 TRAILER_MAGIC = 0x177245385090
 PIECE_MAX = 1_500_000_000  # bzg_seg_map region limit (32-bit RLE1 offsets)
-# BZG_SHARD_TIMING=1: synchronise after each step of compress_sharded and keep the host times
-# (seconds since the call started) in last_timing
-_TIMING = os.environ.get("BZG_SHARD_TIMING") == "1"
+# compress_sharded(..., timing=True): synchronise after each step and keep the host times
+# (seconds since the call started) in last_timing (bench.py's phases_ms, outside its timed region)
+_timing = False
 last_timing: dict = {}
 last_meta: dict = {}  # rank 0: blocks and payload bits of the last stream
 
 
 def _mark(name: str, t0: float, dev) -> None:
-    if _TIMING:
+    if _timing:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         last_timing[name] = round(time.perf_counter() - t0, 6)
@@ -209,12 +208,14 @@ def _all_gather_i64(vals, device):
     return [o.tolist() for o in out]
 
 
-def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int, backend=None):
+def compress_sharded(d: torch.Tensor, shard_start: int, n_total: int, level: int, backend=None, timing: bool = False):
     """Compress input[shard_start, shard_start + len(d)) as this rank's shard of one stream of
     n_total bytes.  Every rank calls it (without a process group: one rank holding it all);
     rank 0 returns the whole .bz2 stream (a uint8 tensor on d's device, or on the CPU under
     gloo), the others None.  Shards are contiguous, in rank
-    order and non-empty; n_total >= 1."""
+    order and non-empty; n_total >= 1.  timing: record the phase times in last_timing."""
+    global _timing
+    _timing = timing
     be = backend or GpuBackend(level, torch.cuda.current_stream().cuda_stream if d.is_cuda else 0)
     t0 = time.perf_counter()
     last_timing.clear()

@@ -81,3 +81,32 @@ def test_bench_world_size_must_match_gpus():
     assert rc == 2 and not lines and "!= --gpus 2" in err
     rc, lines, _ = _run_bench(["--gpus", "1"], {"BZG_BENCH_PROBE": "1"})
     assert rc == 0 and lines == [{"rank": 0, "world": 1, "local_rank": 0, "master": None}]
+
+
+def test_bench_total_bytes_strong_layout():
+    """`--total-bytes T` (BASELINE config 3, strong scaling): ONE stream of T bytes, rank r holding
+    input[T r / N, T (r + 1) / N); the shards tile [0, T) in rank order."""
+    T = 1_000_000_007
+    for world in (2, 3):
+        rc, lines, err = _run_bench(["--gpus", str(world), "--total-bytes", str(T)],
+                                    {"BZG_BENCH_PROBE": "1", "BZG_DIST_BACKEND": "gloo"})
+        assert rc == 0, err[-2000:]
+        lines.sort(key=lambda x: x["rank"])
+        assert [x["rank"] for x in lines] == list(range(world))
+        assert all(x["scaling"] == "strong" and x["mode"] == "stream" and x["job_bytes"] == T for x in lines)
+        assert lines[0]["lo"] == 0 and lines[-1]["lo"] + lines[-1]["n"] == T
+        assert all(lines[r]["lo"] + lines[r]["n"] == lines[r + 1]["lo"] for r in range(world - 1))
+        assert max(x["n"] for x in lines) - min(x["n"] for x in lines) <= 1
+
+
+def test_job_layout_weak_and_strong():
+    import argparse
+
+    a = argparse.Namespace(total_bytes=0, bytes=1000, mode=None)
+    assert bench.job_layout(a, 1, 0)["mode"] == "independent"
+    w = bench.job_layout(a, 4, 2)
+    assert (w["scaling"], w["mode"], w["lo"], w["n"], w["job_bytes"]) == ("weak", "stream", 2000, 1000, 4000)
+    a.total_bytes = 10
+    s = [bench.job_layout(a, 3, r) for r in range(3)]
+    assert [(x["lo"], x["n"]) for x in s] == [(0, 3), (3, 3), (6, 4)]
+    assert all(x["scaling"] == "strong" and x["seed"] == bench.rank_seed(0) for x in s)
