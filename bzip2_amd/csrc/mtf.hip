@@ -242,19 +242,22 @@ __global__ void __launch_bounds__(64 * kCW) k_compose(const uint32_t* __restrict
 
 // 3. per-chunk MTF from the chunk's initial list, fused with the chunk's zero-run summary.
 // List positions 0..31 live in eight registers (byte k of word w = position 4w+k; SWAR
-// search and shift, no memory access); positions 32..255 live in LDS as 56 words laid out
-// [word][thread].  Ranks >= 32 are rare (< 0.1% on text), so the LDS part is touched by few
-// steps of a wave.
+// search and shift, no memory access); positions 32..95 live in LDS as 16 words laid out
+// [word][thread]; positions 96..255 stay in the chunk's initial-list words in global memory
+// (`init`, updated in place: no other kernel reads a chunk this kernel owns).  Ranks >= 32 are
+// rare (< 0.1% on text) and ranks >= 96 rarer still, so the LDS and global parts are touched by
+// few steps of a wave, and the small LDS part lets 4 waves share a SIMD instead of 2.
 constexpr int kRegW = 8;  // list words (4 positions each) held in registers
 constexpr uint32_t kRowMin = 64;  // chunks with more distinct symbols go to k_mtf_q
-constexpr int kListW = 64;  // list words a lane holds (registers + LDS)
+constexpr int kLdsW = 24;   // list words below this index live in registers or LDS
+constexpr int kListW = 64;  // list words a lane holds (registers + LDS + global)
 
 __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                                 const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ siglen,
-                                                const uint32_t* __restrict__ init,
+                                                uint32_t* __restrict__ init,
                                                 uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
                                                 uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
-  __shared__ uint32_t lst[kListW - kRegW][kT];
+  __shared__ uint32_t lst[kLdsW - kRegW][kT];
   // rank words of the wave's 64 chunks for one 64-symbol window, [chunk][word] (17: no bank
   // conflicts on the per-lane writes); flushed as 16-byte stores, 4 lanes per chunk
   __shared__ uint32_t stg[kT / 64][64 * 17];
@@ -265,11 +268,17 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
   // register words)
   const bool mine = r.valid && siglen[r.gidx] <= kRowMin;
   const uint32_t len = mine ? r.hi - r.lo : 0u;
-  const uint32_t* src = init + (size_t)(r.valid ? r.gidx : 0u) * 64;
+  uint32_t* const src = init + (size_t)(r.valid ? r.gidx : 0u) * 64;
   uint32_t W[kRegW];
 #pragma unroll
   for (int w = 0; w < kRegW; w++) W[w] = src[w];
-  for (int w = kRegW; w < kListW; w++) lst[w - kRegW][t] = src[w];
+  for (int w = kRegW; w < kLdsW; w++) lst[w - kRegW][t] = src[w];
+  // list word w >= kRegW (LDS below kLdsW, else the chunk's own global words)
+  auto lget = [&](uint32_t w) -> uint32_t { return w < (uint32_t)kLdsW ? lst[w - kRegW][t] : src[w]; };
+  auto lput = [&](uint32_t w, uint32_t v) {
+    if (w < (uint32_t)kLdsW) lst[w - kRegW][t] = v;
+    else src[w] = v;
+  };
   uint32_t racc = 0;  // 4 ranks packed
   uint32_t ld = 0, z = 0, cnt = 0;
   bool seen = false;
@@ -295,7 +304,7 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
       for (; w < wlim; w += 4) {
         uint32_t y[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) y[k] = lst[w + k - kRegW][t] ^ pat;
+        for (int k = 0; k < 4; k++) y[k] = lget(w + k) ^ pat;
         uint32_t hit = 4;
 #pragma unroll
         for (int k = 3; k >= 0; k--) {
@@ -359,21 +368,21 @@ __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, c
       for (; w + 4 <= tw; w += 4) {  // 4 loads in flight per step
         uint32_t y[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) y[k] = lst[w + k - kRegW][t];
+        for (int k = 0; k < 4; k++) y[k] = lget(w + k);
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-          lst[w + k - kRegW][t] = (y[k] << 8) | carry;
+          lput(w + k, (y[k] << 8) | carry);
           carry = y[k] >> 24;
         }
       }
       for (; w < tw; w++) {
-        const uint32_t v = lst[w - kRegW][t];
-        lst[w - kRegW][t] = (v << 8) | carry;
+        const uint32_t v = lget(w);
+        lput(w, (v << 8) | carry);
         carry = v >> 24;
       }
-      const uint32_t v = lst[tw - kRegW][t];
+      const uint32_t v = lget(tw);
       const uint32_t lowmask = (tb == 3) ? 0xffffffffu : ((1u << (8 * (tb + 1))) - 1u);
-      lst[tw - kRegW][t] = (v & ~lowmask) | (((v << 8) | carry) & lowmask);
+      lput(tw, (v & ~lowmask) | (((v << 8) | carry) & lowmask));
     }
   };
   // chunk g's ranks go to ranks[g * kChunk, g * kChunk + len): chunk-aligned, so the wave's

@@ -165,7 +165,7 @@ def ref_stream_compress(chunks, level: int, finish_with_last=False, flush_after=
     chunks = list(chunks)
     for i, c in enumerate(chunks):
         b = ctypes.create_string_buffer(bytes(c), len(c))
-        keep.append(b)
+        keep[:] = [b]  # only the chunk being consumed (4 GiB inputs come in 256 MiB chunks)
         strm.next_in = ctypes.cast(b, ctypes.c_void_p)
         strm.avail_in = len(c)
         if finish_with_last and i == len(chunks) - 1:
