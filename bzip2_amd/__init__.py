@@ -43,7 +43,7 @@ EXPORTS = [
 ENGINE_EXPORTS = [
     "bzg_stream_init", "bzg_compress_device", "bzg_compress_host", "bzg_compress_host_stream",
     "bzg_bound", "bzg_stage_rle1", "bzg_stage_bwt", "bzg_stage_mtf", "bzg_stage_code_lengths", "bzg_last_stats",
-    "bzg_release", "bzg_device_ok", "bzg_periodic_origptr", "bzg_qperiodic_bwt", "bzg_seg_map", "bzg_seg_walk",
+    "bzg_release", "bzg_device_ok", "bzg_periodic_origptr", "bzg_copy_rank_closed_form", "bzg_qperiodic_bwt", "bzg_seg_map", "bzg_seg_walk",
     "bzg_find_magics", "bzg_decompress_device", "bzg_decompress_host", "bzg_last_decode_stats",
 ]
 
@@ -81,7 +81,7 @@ class bzg_stats(ctypes.Structure):
         ("code_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
         ("nblocks", ctypes.c_uint32), ("sort_iterations", ctypes.c_uint32),
         ("rle_bytes", ctypes.c_uint64), ("sort_unsorted", ctypes.c_uint64),
-        ("mtf_symbols", ctypes.c_uint64),
+        ("mtf_symbols", ctypes.c_uint64), ("a5_roots", ctypes.c_uint32), ("a5_host", ctypes.c_uint32),
     ]
 
 
@@ -128,6 +128,8 @@ def lib() -> ctypes.CDLL:
         L.bzg_find_magics.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64), vp]
         L.bzg_seg_walk.argtypes = [u32, ci, vp, u32, ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.bzg_periodic_origptr.restype = ctypes.c_int32
+        L.bzg_copy_rank_closed_form.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
+        L.bzg_copy_rank_closed_form.restype = ctypes.c_int32
         L.bzg_qperiodic_bwt.argtypes = [vp, u32, vp, ctypes.POINTER(u32)]
         L.bzg_qperiodic_bwt.restype = u32
         L.bzg_decompress_device.argtypes = [vp, u64, vp, u64, ctypes.POINTER(u64), vp]
@@ -318,6 +320,12 @@ def code_lengths(tables, max_len: int = 17):
 def periodic_origptr(block: bytes) -> int:
     """origPtr the reference assigns to an exactly periodic block (host replay, A5)."""
     return int(lib().bzg_periodic_origptr(bytes(block), len(block)))
+
+
+def copy_rank_closed_form(root: bytes, k: int) -> int:
+    """The copy rank the device computes in closed form for root^k (origptr.hip's rules), or -1
+    when the host model decides (A5; host mirror, no GPU)."""
+    return int(lib().bzg_copy_rank_closed_form(bytes(root), len(root), k))
 
 
 def qperiodic_bwt(block: bytes):

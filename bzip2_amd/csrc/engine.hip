@@ -290,7 +290,7 @@ struct Engine {
             Part& P = parts[p];
             P.w->set_stream(ss);
             if (ss != s) HIP_OK(hipStreamWaitEvent(ss, ev_rle, 0));
-            copyrank_begin(P.r, P.hboff, P.hper, P.hbq, P.a5, ss);  // host copy ranks overlap the sort
+            copyrank_begin(*P.w, P.r, P.hboff, P.hper, P.hbq, P.a5, ss);  // (side stream: overlaps the sort)
             bwt_stage(*P.w, P.r, P.hboff, P.hper, bwt + hboff[P.b0], rank0 + P.b0, &P.ss, ss, P.hqp.data());
             HIP_OK(hipEventRecord(psorted[p], ss));
             sorted[p].set_value();
@@ -339,6 +339,7 @@ struct Engine {
         code_tables(ws, r, P.m, nb, P.t, s, split_tables() ? sstream[0] : nullptr);
         HIP_OK(hipEventRecord(e2, s));
         HIP_OK(hipEventSynchronize(e2));
+        for (uint32_t p = 0; p < nparts; p++) copyrank_check(parts[p].a5);
         (void)hipEventElapsedTime(&mtf_ms, e0, e1);
         (void)hipEventElapsedTime(&tab_ms, e1, e2);
         last_post = mtf_ms + tab_ms;
@@ -389,6 +390,10 @@ struct Engine {
     last.sort_iterations = (int)sort_iters;
     last.rle_bytes = nb ? hboff[nb] : 0;
     last.sort_unsorted = sort_unsorted;
+    for (uint32_t p = 0; p < nparts; p++) {
+      last.a5_roots += (uint32_t)parts[p].a5.need.size();
+      last.a5_host += parts[p].a5.n_host;
+    }
     for (uint32_t p = 0; p < K; p++) {
       const Part& P = parts[p];
       if (!P.r.nblocks) continue;
@@ -445,6 +450,8 @@ void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_strea
     acc.rle_bytes += one.rle_bytes;
     acc.sort_unsorted += one.sort_unsorted;
     acc.mtf_symbols += one.mtf_symbols;
+    acc.a5_roots += one.a5_roots;
+    acc.a5_host += one.a5_host;
     done_in += cons;
     done_out += ob;
     if (last_piece) break;
@@ -1220,6 +1227,16 @@ void bzg_release(void) {
   S.n = 0;
 }
 
+int32_t bzg_copy_rank_closed_form(const uint8_t* root, int32_t p, int32_t k) {
+  if (!root || p < 2 || k < 2) return -1;
+  try {
+    const int32_t r = copy_rank_single(root, p, k);
+    return r >= 0 ? r : copy_rank_distinct(root, p, k);
+  } catch (...) {
+    return -1;
+  }
+}
+
 int32_t bzg_periodic_origptr(const uint8_t* block, int32_t n) {
   if (!block || n <= 0) return -1;
   try {
@@ -1227,8 +1244,10 @@ int32_t bzg_periodic_origptr(const uint8_t* block, int32_t n) {
     if (p == n) return -1;  // not periodic: the sort's rank is the origPtr
     if (p == 1) return 0;   // one symbol: no B* rotation
     const int32_t k = n / p;
-    const int32_t single = copy_rank_single(block, p, k);  // the device's closed form
-    return root_rotation_rank(block, p) * k + (single >= 0 ? single : copy_rank(block, p, k));
+    int32_t r = copy_rank_single(block, p, k);  // the device's closed forms first (origptr.hip)
+    if (r < 0) r = copy_rank_distinct(block, p, k);
+    if (r < 0) r = copy_rank(block, p, k);
+    return root_rotation_rank(block, p) * k + r;
   } catch (const CopyRankFailure&) {
     return -1;
   } catch (const std::bad_alloc&) {
@@ -1305,11 +1324,12 @@ int bzg_stage_bwt(const uint8_t* blocks, const uint32_t* offsets, uint32_t nb, u
     uint32_t* rank0 = e.ws.u32("rank0", nb + 2);
     uint32_t* d_orig = e.ws.u32("origptr", nb + 2);
     CopyRankJob a5;
-    copyrank_begin(r, hboff, hper, hbq, a5, e.stream);
+    copyrank_begin(e.ws, r, hboff, hper, hbq, a5, e.stream);
     bwt_stage(e.ws, r, hboff, hper, bwt, rank0, nullptr, e.stream, hqp.data());
     copyrank_finish(e.ws, r, rank0, d_orig, a5, e.stream);
     HIP_OK(hipMemcpyAsync(origptr, d_orig, 4 * nb, hipMemcpyDeviceToHost, e.stream));
     HIP_OK(hipStreamSynchronize(e.stream));
+    copyrank_check(a5);
     stage_copy(e, bwt_out, bwt, total, hipMemcpyDeviceToHost);
     return BZ_OK;
   } catch (const HipFailure&) {

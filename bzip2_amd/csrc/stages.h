@@ -87,21 +87,32 @@ void seg_walk_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, u
                     hipStream_t st);
 
 // ---- stage A5 (origptr.hip) ----------------------------------------------------------
-// B* offsets per periodic root (part of block_info_stage); the host copy rank of the roots
-// with more than one (started before the sort, overlapping it); origptr after the sort.
+// B* offsets per periodic root (part of block_info_stage); the copy ranks of the roots with
+// more than one (origptr.hip: the device's closed form, then the host model for the rest on a
+// side stream, started before the sort and overlapping it); origptr after the sort.
 struct CopyRankJob {
-  std::vector<int32_t> r;
-  std::vector<uint8_t> roots;
-  std::thread th;
-  std::exception_ptr err;
+  std::vector<uint32_t> need, per, len;  // blocks with such roots, their periods and lengths
+  int32_t* dev_r = nullptr;              // per block: r (workspace buffer)
+  int32_t* pin_r = nullptr;              // pinned: the device's answers, then the merged ones
+  uint8_t* pin_roots = nullptr;          // pinned: the roots of `need`, concatenated
+  hipStream_t side = nullptr;
+  hipEvent_t ev_cf = nullptr, ev_done = nullptr;
+  uint32_t n_host = 0;  // roots the host model resolved
+  int failed = 0;
+  CopyRankJob() = default;
+  CopyRankJob(const CopyRankJob&) = delete;
+  CopyRankJob& operator=(const CopyRankJob&) = delete;
   ~CopyRankJob();
 };
 void copyrank_count_stage(Rle1Result& r, Workspace& ws, hipStream_t st);
 void copyrank_memo_clear();  // bzg_release: drops the memoised periodic roots
-void copyrank_begin(const Rle1Result& r, const std::vector<uint32_t>& hboff, const std::vector<uint32_t>& hper,
-                    const std::vector<uint32_t>& hbq, CopyRankJob& job, hipStream_t st);
+void copyrank_begin(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& hboff,
+                    const std::vector<uint32_t>& hper, const std::vector<uint32_t>& hbq, CopyRankJob& job,
+                    hipStream_t st);
 void copyrank_finish(Workspace& ws, const Rle1Result& r, const uint32_t* rank0, uint32_t* origptr, CopyRankJob& job,
                      hipStream_t st);
+// after the batch's last synchronisation: throws if the host model failed on a root
+void copyrank_check(const CopyRankJob& job);
 
 // ---- stage A4 ------------------------------------------------------------------------
 // Sorts the rotations of every block (of its primitive root when periodic) and writes the

@@ -79,6 +79,13 @@ int bzg_stage_code_lengths(const uint32_t *freq, const int32_t *alpha, uint32_t 
  * Returns -1 on failure.  Needs no GPU. */
 int32_t bzg_periodic_origptr(const uint8_t *block, int32_t n);
 
+/* The copy rank r (origPtr = rank of rotation 0 among the p rotations of the root, times k, plus
+ * r) of the block root^k that the DEVICE computes in closed form (origptr.hip: one B* offset per
+ * period, or several B* offsets in pairwise different (c0, c1) buckets within the reference's
+ * rank-stage budget; bzip2_amd/csrc/copyrank_cf.cpp), or -1 when the root is left to the host
+ * model.  root must be primitive, p >= 2, k >= 2.  Needs no GPU (the host mirror of the rules). */
+int32_t bzg_copy_rank_closed_form(const uint8_t *root, int32_t p, int32_t k);
+
 /* BWT and origPtr of a quasi-periodic block (smallest period p <= 256 with 2p <= n not
  * dividing n, e.g. the last block of a single-repeated-byte input), computed on the host by the
  * analytic order of bzip2_amd/csrc/qsa.cpp that the GPU sort uses for such blocks (k_qsa).
@@ -93,6 +100,8 @@ typedef struct {
   uint64_t rle_bytes;         /* RLE1 output bytes (block bytes) */
   uint64_t sort_unsorted;     /* elements revisited by doubling iterations */
   uint64_t mtf_symbols;       /* total nMTF */
+  uint32_t a5_roots;          /* periodic roots with several B* offsets (A5) */
+  uint32_t a5_host;           /* of those, the ones the host model resolved (the rest: on the device) */
 } bzg_stats;
 /* One region of a sharded stream (the ranks of a job each hold a contiguous
  * shard of one input stream).  The global block cuts of bzlib.c:211-315 copy_input_until_stop

@@ -351,3 +351,49 @@ def test_randomised_block_streaming_decoder(lib, tmp_path):
     assert e.value == B.BZ_STREAM_END and bytes(got) == want
     L.BZ2_bzReadClose(ctypes.byref(e), h)
     c.fclose(f)
+
+
+def test_copy_rank_closed_forms_vs_reference(lib):
+    """A5 on the device, section 8f row 4: the closed forms origptr.hip evaluates (one B* offset
+    per period; several B* offsets in pairwise different (c0, c1) buckets within the reference's
+    rank-stage budget, copyrank_cf.cpp) against the reference build, on random roots of every
+    shape; the roots they leave go to the host model.  Also pins the share they cover."""
+    from tests import datagen, oracles as O
+    if not O.has_ref():
+        pytest.skip("oracle/_ref not built")
+    import random
+    rng = random.Random(8402)
+    txt = datagen.text(200_000, 21)
+    multi = covered = checked = 0
+    cases = [(b"hello world\n", k) for k in (2, 3, 8, 9, 10, 1024, 1025, 2049, 74_998)]
+    cases += [(b"abac", k) for k in (2, 9, 17, 1000, 1025, 1026, 224_995)]
+    cases += [(b"cab", k) for k in (2, 9, 1025)]  # (class q - 1 has the smallest bucket)
+    for _ in range(1500):
+        mode = rng.random()
+        if mode < 0.5:
+            w = bytes(rng.randrange(rng.choice([2, 3, 4, 8, 26, 256])) for _ in range(rng.randint(2, 16)))
+        elif mode < 0.8:
+            s = rng.randrange(0, len(txt) - 200)
+            w = txt[s:s + rng.randint(4, 200)]
+        else:
+            w = bytes(rng.randrange(256) for _ in range(rng.randint(2, 40)))
+        k = rng.choice([2, 3, 7, 9, 16, 100, 1023, 1024, 1025, 1026, 3000, rng.randint(2, 20000)])
+        cases.append((w, k))
+    for w, k in cases:
+        if len(set(w)) < 2 or len(w) * k > 899_981:
+            continue
+        blk = w * k
+        # primitive roots only
+        p = len(w)
+        if any(p % d == 0 and w == w[:d] * (p // d) for d in range(1, p)):
+            continue
+        r = B.copy_rank_closed_form(w, k)
+        multi += 1
+        if r < 0:
+            continue
+        covered += 1
+        ref = O.ref_blocksort(blk)[1]
+        rank = sum(1 for i in range(1, p) if (w[i:] + w[:i]) < w)
+        assert rank * k + r == ref, (w[:24], k, r, ref)
+        checked += 1
+    assert checked >= 500 and covered / multi > 0.3, (checked, covered, multi)

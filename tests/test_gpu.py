@@ -173,6 +173,10 @@ def _periodic_blocks(seed):
     for w, k in ((b"ab", 4096), (b"abc", 17), (b"abc", 1026), (b"aab", 300), (b"abcabcabd", 11109),
                  (b"bababac", 4096)):
         parts.append(w * k)
+    # several B* per period in pairwise different buckets (device closed form, k_copyrank_cf)
+    for w, k in ((b"hello world\n", 9), (b"hello world\n", 1025), (b"abac", 2), (b"abac", 1026),
+                 (b"cab", 1025), (b"abac", 224_995)):
+        parts.append(w * k)
     for _ in range(40):
         mode = rng.random()
         if mode < 0.4:
@@ -202,6 +206,26 @@ def test_periodic_blocks_origptr_vs_reference():
         want_l, want_o = O.ref_blocksort(blk)
         assert orig[b] == want_o, (b, blk[:16], len(blk))
         assert bwt[offs[b]:offs[b + 1]] == want_l, (b, len(blk))
+
+
+def test_periodic_roots_resolved_on_device():
+    """periodic roots with several B* offsets in pairwise different buckets are
+    resolved by the device (k_copyrank_cf): a stream of only such blocks leaves nothing to the
+    host model; mixed with shared-bucket roots, only those reach it.  Bytes vs the reference."""
+    if not O.has_ref():
+        pytest.skip("needs oracle/_ref")
+    # root lengths divide the -1 block (99,981 = 3^3 7 23^2): every block is exactly periodic;
+    # q = 2..6 B* offsets per root
+    roots = (b"cab", b"</text>", b"</revis", b"</revisio", b"></title>\n  <id></id>", b"></title>\n  <id></id>\n ",
+             b"  <id></id>\n  <revision>\n  ")
+    data = b"".join(w * (99_981 // len(w)) * 2 for w in roots)
+    assert B.buff_to_buff_compress(data, 1) == O.ref_compress(data, 1)
+    st = B.last_stats()
+    assert st["a5_roots"] >= 12 and st["a5_host"] == 0, st
+    mixed = data + b"abcabcabd" * (99_981 // 9) * 2
+    assert B.buff_to_buff_compress(mixed, 1) == O.ref_compress(mixed, 1)
+    st = B.last_stats()
+    assert st["a5_roots"] >= 14 and 0 < st["a5_host"] < st["a5_roots"], st
 
 
 def test_periodic_blocks_stream_vs_reference():
