@@ -498,16 +498,21 @@ __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict_
   __shared__ uint32_t cb[kTile * 5 / 128 + 4];  // chunk-start bits, word k = global word (t0 >> 5) + k
   const uint64_t t0g = (uint64_t)blockIdx.x * kRleG;
   uint4 qs[kRleG];
-  uint32_t pws[kRleG];
+  uint32_t pws[kRleG], tb[kRleG];
   bool inrun[kRleG];  // pass 1 found the tile inside one run (tinfo: h = kTile, no end, S = 0)
+  // the tile's info, output base and input are loaded together (no dependent round trip; an
+  // in-run tile's input load is wasted, but such tiles cost nothing else)
 #pragma unroll
   for (uint32_t g = 0; g < kRleG; g++) {
     const uint64_t base = (t0g + g) * kTile + (uint64_t)threadIdx.x * kPer;
-    inrun[g] = BZG_EMIT_INRUN && rle_interior(t0g + g, n) && tinfo[t0g + g] == (uint32_t)kTile << 16;
-    if (rle_interior(t0g + g, n) && !inrun[g]) {
+    const bool interior = rle_interior(t0g + g, n);
+    const uint32_t ti = interior ? tinfo[t0g + g] : 0u;
+    tb[g] = (t0g + g) < tiles ? out_base[t0g + g] : 0u;
+    if (interior) {
       qs[g] = *reinterpret_cast<const uint4*>(x + base);
       pws[g] = *reinterpret_cast<const uint32_t*>(x + base - 4);
     }
+    inrun[g] = BZG_EMIT_INRUN && interior && ti == (uint32_t)kTile << 16;
   }
 #pragma unroll
   for (uint32_t g = 0; g < kRleG; g++) {
@@ -530,7 +535,7 @@ __global__ void BZG_EMIT_BOUNDS BZG_SGPR_LIMIT k_emit(const uint8_t* __restrict_
         // every byte emits itself and starts a chunk iff it starts a run: the tile's output is
         // its input at t0 = out_base, stored as whole words (the first and last word of the tile
         // are shared with the neighbouring tiles: byte stores)
-        const uint32_t t0 = out_base[tile], lofs = t0 & 3u;
+        const uint32_t t0 = tb[g], lofs = t0 & 3u;
         const uint32_t pos = t0 + threadIdx.x * kPer, sh5 = pos & 31u;
         const uint32_t c0 = t0 >> 5, wi = (pos >> 5) - c0;
         if (rw.starts) {

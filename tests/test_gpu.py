@@ -221,11 +221,13 @@ def test_periodic_roots_resolved_on_device():
     data = b"".join(w * (99_981 // len(w)) * 2 for w in roots)
     assert B.buff_to_buff_compress(data, 1) == O.ref_compress(data, 1)
     st = B.last_stats()
-    assert st["a5_roots"] >= 12 and st["a5_host"] == 0, st
-    mixed = data + b"abcabcabd" * (99_981 // 9) * 2
+    # (RLE1 of the last root's runs of spaces shifts the later cuts: 8 blocks stay exactly periodic
+    # with q >= 2, computed from the oracle's blocks in round 5)
+    assert st["a5_roots"] == 8 and st["a5_host"] == 0, st
+    mixed = b"abcabcabd" * (99_981 // 9) * 2 + data  # 2 more blocks, q = 3 in shared buckets: host model
     assert B.buff_to_buff_compress(mixed, 1) == O.ref_compress(mixed, 1)
     st = B.last_stats()
-    assert st["a5_roots"] >= 14 and 0 < st["a5_host"] < st["a5_roots"], st
+    assert st["a5_roots"] == 10 and st["a5_host"] == 2, st
 
 
 def test_periodic_blocks_stream_vs_reference():
