@@ -143,6 +143,7 @@ struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t sstream[kSortStreams] = {};  // block sorts of the batch's parts
+  hipStream_t cstream = nullptr;             // host <-> device copies of the pipelined host calls
   Workspace ws;
   std::vector<std::unique_ptr<Workspace>> pws;  // one per part of a batch
   std::vector<hipEvent_t> psorted;              // per part: its sort is done
@@ -152,6 +153,7 @@ struct Engine {
   explicit Engine(int dev) : device(dev) {
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto& x : sstream) HIP_OK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     for (auto& e : ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipEventCreateWithFlags(&ev_rle, hipEventDisableTiming));
     ws.set_stream(stream);
@@ -1106,6 +1108,138 @@ int bzg_find_magics(const void* d_in, uint64_t n, uint64_t* out, uint64_t cap, u
   });
 }
 
+// Host buffers of large inputs: the input goes over in pieces of growing size (the first small,
+// so that compression starts early; then each twice the one before), on the engine's copy
+// stream from a copier thread, while the main thread compresses the pieces that have arrived as
+// consecutive segments of one stream (a non-final segment emits its complete blocks and the
+// rest is resubmitted with the next piece, exactly as bzg_compress_device cuts a large input into
+// batches, so the bytes equal one call's); each segment's output goes back from a second thread
+// while the next one is compressed.  Only the first piece's upload and the last segment's
+// download are not overlapped.
+static constexpr uint64_t kPipeMin = 192ull << 20;  // smaller inputs: one upload, one call, one download
+static constexpr uint64_t kPipeFirst = 96ull << 20;
+
+static std::vector<uint64_t> pipe_pieces(uint64_t n) {
+  std::vector<uint64_t> b{0};
+  uint64_t s = std::max<uint64_t>(kPipeFirst, n / 10);
+  while (n - b.back() >= 3 * s) {  // the remainder is at least 1.5 pieces of the next size
+    b.push_back(b.back() + s);
+    s *= 2;
+  }
+  b.push_back(n);
+  return b;
+}
+
+static int host_call_pipelined(Engine* e, const uint8_t* src, uint64_t n, unsigned flags, bzg_stream_state* st,
+                               uint8_t* dst, uint64_t dst_cap, uint64_t* dst_len, uint64_t* consumed) {
+  const std::vector<uint64_t> b = pipe_pieces(n);
+  const size_t J = b.size() - 1;
+  const uint64_t cap = bzg_bound(n);
+  uint8_t* din = e->ws.u8("host_in", n + 16);
+  uint8_t* dout = e->ws.u8("host_out", cap);
+  std::vector<hipEvent_t> ev_in(J, nullptr);
+  for (auto& x : ev_in) HIP_OK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t uploaded = 0;     // pieces whose copy is queued (ev_in recorded)
+  bool up_failed = false;
+  struct Down { uint64_t off, len; };
+  std::vector<Down> downs;  // segment outputs to copy back, in order
+  bool all_queued = false, down_failed = false;
+  const int dev = e->device;
+  std::thread up([&] {
+    bool ok = hipSetDevice(dev) == hipSuccess;
+    for (size_t j = 0; j < J && ok; j++) {
+      ok = hipMemcpyAsync(din + b[j], src + b[j], b[j + 1] - b[j], hipMemcpyHostToDevice, e->cstream) == hipSuccess &&
+           hipEventRecord(ev_in[j], e->cstream) == hipSuccess;
+      std::lock_guard<std::mutex> g(mu);
+      if (ok) uploaded = j + 1;
+      else up_failed = true;
+      cv.notify_all();
+    }
+  });
+  std::thread down([&] {
+    bool ok = hipSetDevice(dev) == hipSuccess;
+    for (size_t i = 0;; i++) {
+      Down d;
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return i < downs.size() || all_queued; });
+        if (i >= downs.size()) break;
+        d = downs[i];
+      }
+      if (ok && d.len) ok = hipMemcpy(dst + d.off, dout + d.off, d.len, hipMemcpyDeviceToHost) == hipSuccess;
+      if (!ok) {
+        std::lock_guard<std::mutex> g(mu);
+        down_failed = true;
+      }
+    }
+  });
+  auto finish_threads = [&] {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      all_queued = true;
+    }
+    cv.notify_all();
+    up.join();
+    down.join();
+    for (auto& x : ev_in) (void)hipEventDestroy(x);
+  };
+  uint64_t done_in = 0, done_out = 0;
+  bzg_stats acc{};
+  int rc = BZ_OK;
+  try {
+    for (size_t j = 0; j < J; j++) {
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return uploaded > j || up_failed; });
+        if (uploaded <= j) throw HipFailure(hipErrorUnknown);
+      }
+      HIP_OK(hipStreamWaitEvent(e->stream, ev_in[j], 0));
+      const bool last = j + 1 == J;
+      uint64_t ob = 0, cons = 0;
+      bzg_stats one{};
+      // the output is coded behind the previous segments' bytes (Engine::compress stages a
+      // misaligned destination itself)
+      e->compress(din + done_in, b[j + 1] - done_in, last ? flags : 0u, st, dout + done_out, cap - done_out, &ob,
+                  &cons, e->stream, one);
+      acc.rle1_ms += one.rle1_ms;
+      acc.bwt_ms += one.bwt_ms;
+      acc.mtf_ms += one.mtf_ms;
+      acc.code_ms += one.code_ms;
+      acc.total_ms += one.total_ms;
+      acc.nblocks += one.nblocks;
+      acc.sort_iterations = std::max(acc.sort_iterations, one.sort_iterations);
+      acc.rle_bytes += one.rle_bytes;
+      acc.sort_unsorted += one.sort_unsorted;
+      acc.mtf_symbols += one.mtf_symbols;
+      acc.a5_roots += one.a5_roots;
+      acc.a5_host += one.a5_host;
+      if (done_out + ob > dst_cap) {
+        rc = BZ_OUTBUFF_FULL;
+        break;
+      }
+      {
+        std::lock_guard<std::mutex> g(mu);
+        downs.push_back(Down{done_out, ob});
+      }
+      cv.notify_all();
+      done_in += cons;
+      done_out += ob;
+    }
+  } catch (...) {
+    finish_threads();
+    throw;
+  }
+  finish_threads();
+  publish_stats(acc);
+  if (rc != BZ_OK) return rc;
+  if (up_failed || down_failed) throw HipFailure(hipErrorUnknown);
+  *dst_len = done_out;
+  if (consumed) *consumed = done_in;
+  return BZ_OK;
+}
+
 // Host buffers through one leased engine: staging, compression and copy-out all happen under
 // the lease, so concurrent callers never share staging buffers.
 static int host_call(const void* src, uint64_t n, unsigned flags, bzg_stream_state* st, void* dst, uint64_t dst_cap,
@@ -1113,6 +1247,8 @@ static int host_call(const void* src, uint64_t n, unsigned flags, bzg_stream_sta
   if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
   return guarded([&] {
     Lease L(current_device());
+    if (n >= kPipeMin && (flags & BZG_FLAG_END_SEGMENT))
+      return host_call_pipelined(L.e, (const uint8_t*)src, n, flags, st, (uint8_t*)dst, dst_cap, dst_len, consumed);
     const uint64_t cap = bzg_bound(n);
     uint8_t* din = L->ws.u8("host_in", n + 16);
     uint8_t* dout = L->ws.u8("host_out", cap);

@@ -242,14 +242,14 @@ __global__ void __launch_bounds__(64 * kCW) k_compose(const uint32_t* __restrict
 
 // 3. per-chunk MTF from the chunk's initial list, fused with the chunk's zero-run summary.
 // List positions 0..31 live in eight registers (byte k of word w = position 4w+k; SWAR
-// search and shift, no memory access); positions 32..95 live in LDS as 16 words laid out
-// [word][thread]; positions 96..255 stay in the chunk's initial-list words in global memory
+// search and shift, no memory access); positions 32..87 live in LDS as 14 words laid out
+// [word][thread]; positions 88..255 stay in the chunk's initial-list words in global memory
 // (`init`, updated in place: no other kernel reads a chunk this kernel owns).  Ranks >= 32 are
-// rare (< 0.1% on text) and ranks >= 96 rarer still, so the LDS and global parts are touched by
-// few steps of a wave, and the small LDS part lets 4 waves share a SIMD instead of 2.
+// rare (< 0.1% on text) and ranks >= 88 rarer still, so the LDS and global parts are touched by
+// few steps of a wave, and the small LDS part lets 5 waves share a SIMD instead of 2 (profiles/r05_ab_mtf.txt).
 constexpr int kRegW = 8;  // list words (4 positions each) held in registers
 constexpr uint32_t kRowMin = 64;  // chunks with more distinct symbols go to k_mtf_q
-constexpr int kLdsW = 24;   // list words below this index live in registers or LDS
+constexpr int kLdsW = 22;   // list words below this index live in registers or LDS
 constexpr int kListW = 64;  // list words a lane holds (registers + LDS + global)
 
 __global__ void __launch_bounds__(kT) k_mtf_run(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,

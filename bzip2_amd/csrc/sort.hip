@@ -618,17 +618,27 @@ __global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __re
     qq[i] = e - S.goff[j];
     vv[i] = ((fl & kGrpAlt) ? B.sa2 : B.sa)[S.gstart[j] + qq[i]];
   }
-  // keys: the cache, or 4 characters of the text when the cache is empty
+  // keys: the cache words are loaded beside the slots (their addresses do not depend on the
+  // rotations); 4 characters of the text only where the cache is empty (identity groups, and
+  // every 4th pass), after the rotation has arrived
+#pragma unroll
+  for (int i = 0; i < (int)kPerTS; i++) {
+    if ((uint32_t)i >= rounds) break;
+    const uint32_t j = jj[i], fl = S.gfl[j];
+    kk[i] = ((fl & kGrpAlt) ? B.sk2 : B.sk)[S.gstart[j] + qq[i]];
+  }
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {
     if ((uint32_t)i >= rounds) break;
     const uint32_t j = jj[i], fl = S.gfl[j], o = qq[i];
     if (fl & kGrpIdent) vv[i] = o;
     const bool fresh = (fl & kGrpIdent) || grp_cache(Grp{0, 0, 0, fl}) == 0;
-    const uint32_t q = cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j]);
-    qq[i] = fresh ? q : 0xffffffffu;  // text position, or none
-    kk[i] = ld_u32(fresh ? B.text + S.gtoff[j] + q
-                         : reinterpret_cast<const uint8_t*>(((fl & kGrpAlt) ? B.sk2 : B.sk) + S.gstart[j] + o));
+    qq[i] = 0xffffffffu;  // text position, or none
+    if (fresh) {
+      const uint32_t q = cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j]);
+      qq[i] = q;
+      kk[i] = ld_u32(B.text + S.gtoff[j] + q);
+    }
   }
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {

@@ -663,6 +663,26 @@ def test_multi_device_host_path(monkeypatch, level):
     assert B.buff_to_buff_compress(txt, level) == expected(txt, level)
 
 
+def test_host_pipelined_equals_device():
+    """BZ2_bzBuffToBuffCompress of a large host buffer runs as a pipeline (engine.hip
+    host_call_pipelined: uploads, segment compressions and downloads overlapped); its bytes
+    equal one device-resident call on the same input, and a short destination gives
+    BZ_OUTBUFF_FULL."""
+    torch = pytest.importorskip("torch")
+    data = datagen.text(300_000_000, 404) + datagen.random_bytes(20_000_000, 5) + b"z" * 30_000_000
+    got = B.buff_to_buff_compress(data, 9)
+    d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+    cap = B.bound(len(data))
+    d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    nb, cons, _ = B.compress_device(d_in.data_ptr(), len(data), 9, d_out.data_ptr(), cap,
+                                    stream_ptr=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert cons == len(data) and got == d_out[:nb].cpu().numpy().tobytes()
+    small = ctypes.create_string_buffer(len(got) // 2)
+    dl = ctypes.c_uint(len(got) // 2)
+    assert B.lib().BZ2_bzBuffToBuffCompress(small, ctypes.byref(dl), data, len(data), 9, 0, 30) == B.BZ_OUTBUFF_FULL
+
+
 def test_round_trip_large_properties():
     """At bench-like sizes: decode(encode(x)) == x with the system bzip2 decoder, and the
     stream equals the reference's on a 4 MB slice."""
