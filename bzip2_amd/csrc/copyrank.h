@@ -16,8 +16,9 @@ int32_t root_bstar_count(const uint8_t* w, int32_t p);
 // Closed form for q == 1 (copyrank.cpp section 4); -1 when q != 1.
 int32_t copy_rank_single(const uint8_t* w, int32_t p, int32_t k);
 
-// Closed form for q >= 2 whose B* classes fall in pairwise different (c0, c1) buckets, when the
-// reference's rank-stage budget lasts (copyrank_cf.cpp); -1 when the rule does not apply.
+// Closed form for q >= 2 whose B* classes have pairwise different keys, the first class alone in
+// its (c0, c1) bucket, when the reference's rank-stage budget lasts (copyrank_cf.cpp); -1 when
+// the rule does not apply.
 int32_t copy_rank_distinct(const uint8_t* w, int32_t p, int32_t k);
 
 // Copy index r of rotation 0 of the block w^k (k >= 2, w primitive, |w| >= 2).

@@ -5,8 +5,9 @@
 // index of rotation 0 (copyrank.cpp).  The device evaluates r itself in two closed forms:
 //   * one B* offset per period (copyrank.cpp section 4): every block cut from a long run of one
 //     byte (RLE1 makes it (c c c c n)^k), in k_origptr;
-//   * several B* offsets whose (c0, c1) buckets are pairwise different, while the reference's
-//     rank-stage budget lasts (copyrank_cf.cpp), in k_copyrank_cf, one workgroup per root.
+//   * several B* offsets in classes of pairwise different keys, the first class alone in its
+//     (c0, c1) bucket, while the reference's rank-stage budget lasts (copyrank_cf.cpp), in
+//     k_copyrank_cf, one workgroup per root.
 // The roots left over take r from the host model (copyrank.cpp) on their p bytes.  That runs
 // in a host function on a side stream (D2H of the roots and of the device's answers, the model
 // for the roots the device left, H2D of the merged answers), so no host thread waits for the
@@ -57,14 +58,15 @@ __device__ __forceinline__ uint32_t single_copy_rank(uint32_t p, uint32_t k) {
   return (k > 8 && g == k / 2) ? 0 : g;
 }
 
-// copyrank_cf.cpp: distinct (c0, c1) buckets.  One workgroup per listed root (q >= 2 B*
-// offsets); out[b] = r, or -1 when the rule does not apply (the host model decides).
+// copyrank_cf.cpp: classes of pairwise different keys, the first alone in its bucket.  One
+// workgroup per listed root (q >= 2 B* offsets); out[b] = r, or -1 when the rule does not apply
+// (the host model decides).
 constexpr uint32_t kCT = 1024, kQMax = 1024;
 __device__ __forceinline__ int lg32d(uint32_t v) { return v == 0 ? -1 : 31 - (int)__builtin_clz(v); }
 __global__ void __launch_bounds__(kCT) k_copyrank_cf(const uint8_t* __restrict__ blk, const uint32_t* __restrict__ boff,
                                                      const uint32_t* __restrict__ period, const uint32_t* __restrict__ bq,
                                                      const uint32_t* __restrict__ list, int32_t* __restrict__ out) {
-  __shared__ uint32_t off[kQMax], bk[kQMax], rk[kQMax];
+  __shared__ uint32_t off[kQMax], bk[kQMax], gp[kQMax], rk[kQMax];
   __shared__ uint32_t sh[kCT / 64];
   __shared__ uint32_t fail, first;
   __shared__ unsigned long long work;
@@ -104,21 +106,45 @@ __global__ void __launch_bounds__(kCT) k_copyrank_cf(const uint8_t* __restrict__
     if (threadIdx.x == 0) out[b] = -1;
     return;
   }
-  for (uint32_t c = threadIdx.x; c < q; c += kCT) bk[c] = ((uint32_t)w[off[c]] << 8) | w[off[c] + 1 == p ? 0 : off[c] + 1];
-  __syncthreads();
-  // processing order of the rank stage = bucket order; the buckets must be pairwise different
   for (uint32_t c = threadIdx.x; c < q; c += kCT) {
-    const uint32_t v = bk[c];
-    uint32_t less = 0, same = 0;
+    bk[c] = ((uint32_t)w[off[c]] << 8) | w[off[c] + 1 == p ? 0 : off[c] + 1];
+    gp[c] = (c + 1 < q ? off[c + 1] : off[0] + p) - off[c];
+  }
+  __syncthreads();
+  // full key: bucket, then the substring characters 2 .. gap + 1 (a shorter equal prefix first)
+  auto cmp = [&](uint32_t x, uint32_t y) -> int {
+    if (bk[x] != bk[y]) return bk[x] < bk[y] ? -1 : 1;
+    const uint32_t len = min(gp[x], gp[y]);
+    uint32_t a = off[x] + 2, e = off[y] + 2;
+    a = a >= p ? a - p : a;  // (off < p, p >= 2)
+    e = e >= p ? e - p : e;
+    a = a >= p ? a - p : a;
+    e = e >= p ? e - p : e;
+    for (uint32_t d = 0; d < len; d++) {
+      const uint8_t ca = w[a], ce = w[e];
+      if (ca != ce) return ca < ce ? -1 : 1;
+      a = a + 1 == p ? 0 : a + 1;
+      e = e + 1 == p ? 0 : e + 1;
+    }
+    return gp[x] == gp[y] ? 0 : gp[x] < gp[y] ? -1 : 1;
+  };
+  // processing order of the rank stage = key order; the keys must be pairwise different
+  for (uint32_t c = threadIdx.x; c < q; c += kCT) {
+    uint32_t less = 0;
     for (uint32_t d = 0; d < q; d++) {
-      const uint32_t u = bk[d];
-      less += u < v;
-      same += u == v;
+      if (d == c) continue;
+      const int o = cmp(d, c);
+      less += o < 0;
+      if (o == 0) fail = 1;
     }
     rk[c] = less;
-    if (same != 1) fail = 1;
     if (less == 0) first = c;
   }
+  __syncthreads();
+  // the first class alone in its bucket
+  if (!fail)
+    for (uint32_t c = threadIdx.x; c < q; c += kCT)
+      if (c != first && bk[c] == bk[first]) fail = 1;
   __syncthreads();
   if (fail) {
     if (threadIdx.x == 0) out[b] = -1;
@@ -148,7 +174,7 @@ __global__ void __launch_bounds__(kCT) k_copyrank_cf(const uint8_t* __restrict__
     return;
   }
   const uint32_t f = first;
-  const uint32_t gap = (f + 1 < q ? off[f + 1] : off[0] + p) - off[f];
+  const uint32_t gap = gp[f];
   const bool wrapped = f == q - 1;
   const uint32_t s0 = min(wrapped ? k - 1 : k, 1024u);
   uint32_t g = (wrapped ? 1u : 0u) + ((s0 > 8 && (gap & 1)) ? s0 / 2 : 0u);
