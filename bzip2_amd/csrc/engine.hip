@@ -4,6 +4,7 @@
 // thread's current device, so host threads compress concurrently on separate HIP streams and
 // device buffers.
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <memory>
 #include <new>
@@ -1147,11 +1148,21 @@ static int host_call_pipelined(Engine* e, const uint8_t* src, uint64_t n, unsign
   std::vector<Down> downs;  // segment outputs to copy back, in order
   bool all_queued = false, down_failed = false;
   const int dev = e->device;
+  // BZG_DEBUG: host times (ms since the call) of each piece's upload, compression and download
+  static const bool dbg = getenv("BZG_DEBUG") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
   std::thread up([&] {
     bool ok = hipSetDevice(dev) == hipSuccess;
     for (size_t j = 0; j < J && ok; j++) {
       ok = hipMemcpyAsync(din + b[j], src + b[j], b[j + 1] - b[j], hipMemcpyHostToDevice, e->cstream) == hipSuccess &&
            hipEventRecord(ev_in[j], e->cstream) == hipSuccess;
+      if (dbg) {
+        const double a = ms();
+        (void)hipEventSynchronize(ev_in[j]);
+        fprintf(stderr, "[bzg h2h] piece %zu (%llu B): upload queued %.2f done %.2f ms\n", j,
+                (unsigned long long)(b[j + 1] - b[j]), a, ms());
+      }
       std::lock_guard<std::mutex> g(mu);
       if (ok) uploaded = j + 1;
       else up_failed = true;
@@ -1169,6 +1180,7 @@ static int host_call_pipelined(Engine* e, const uint8_t* src, uint64_t n, unsign
         d = downs[i];
       }
       if (ok && d.len) ok = hipMemcpy(dst + d.off, dout + d.off, d.len, hipMemcpyDeviceToHost) == hipSuccess;
+      if (dbg) fprintf(stderr, "[bzg h2h] download %zu (%llu B) done %.2f ms\n", i, (unsigned long long)d.len, ms());
       if (!ok) {
         std::lock_guard<std::mutex> g(mu);
         down_failed = true;
@@ -1197,6 +1209,7 @@ static int host_call_pipelined(Engine* e, const uint8_t* src, uint64_t n, unsign
       }
       HIP_OK(hipStreamWaitEvent(e->stream, ev_in[j], 0));
       const bool last = j + 1 == J;
+      const double c0 = dbg ? ms() : 0.0;
       uint64_t ob = 0, cons = 0;
       bzg_stats one{};
       // the output is coded behind the previous segments' bytes (Engine::compress stages a
@@ -1215,6 +1228,8 @@ static int host_call_pipelined(Engine* e, const uint8_t* src, uint64_t n, unsign
       acc.mtf_symbols += one.mtf_symbols;
       acc.a5_roots += one.a5_roots;
       acc.a5_host += one.a5_host;
+      if (dbg) fprintf(stderr, "[bzg h2h] piece %zu: compress %.2f .. %.2f ms (%llu B in, %llu B out)\n", j, c0, ms(),
+                       (unsigned long long)cons, (unsigned long long)ob);
       if (done_out + ob > dst_cap) {
         rc = BZ_OUTBUFF_FULL;
         break;

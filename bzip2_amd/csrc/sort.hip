@@ -33,22 +33,25 @@ namespace bzg {
 namespace {
 
 constexpr int kT = 256;
-constexpr uint32_t kBig = 256;        // buckets larger than this are split by S1 byte passes
+constexpr uint32_t kBig = 512;        // buckets larger than this are split by S1 byte passes
 constexpr uint32_t kDTile = 4096;     // rotations per workgroup in a tiled S1 pass
 constexpr uint32_t kPerT = kDTile / kT;
 constexpr uint32_t kDBig = 16;        // S1 byte passes stop at this depth (then doubling)
 constexpr uint32_t kSG = 2048;      // S1 groups up to this size are packed into shared tiles
-// size classes: 0..5 go to S2 (2-8 .. 129-256), 6 / 7 to the next S1 pass (packed / tiled),
-// 8 (still big after kDBig characters) to the doubling fallback
-constexpr int kNCls = 8;
-constexpr uint32_t kClsMax[7] = {8, 16, 32, 64, 128, kBig, kSG};
-constexpr uint32_t kClsDeep = 8;
+// size classes: 0..6 go to S2 (2-8 .. 257-512), 7 / 8 to the next S1 pass (packed / tiled),
+// 9 (still big after kDBig characters) to the doubling fallback
+constexpr int kNCls = 9;
+constexpr int kS2Cls = 7;             // classes sorted by S2
+constexpr uint32_t kClsPacked = 7, kClsTiled = 8;
+constexpr uint32_t kClsMax[8] = {8, 16, 32, 64, 128, 256, kBig, kSG};
+constexpr uint32_t kClsDeep = 9;
 // S2 workgroups walk the (block-ordered) group lists XCD by XCD: each XCD's L2 then holds the
 // text and slots of its own few blocks instead of every block's
 __device__ __forceinline__ uint32_t s2_wg() { return xcd_remap(blockIdx.x, gridDim.x); }
 
 __host__ __device__ __forceinline__ uint32_t size_cls(uint32_t n) {
-  return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= kBig ? 5u : n <= kSG ? 6u : 7u;
+  return n <= 8 ? 0u : n <= 16 ? 1u : n <= 32 ? 2u : n <= 64 ? 3u : n <= 128 ? 4u : n <= 256 ? 5u : n <= kBig ? 6u
+         : n <= kSG ? 7u : 8u;
 }
 
 struct SortOut {
@@ -308,7 +311,7 @@ __global__ void __launch_bounds__(kT) k_s1_hist(const TileRec* __restrict__ TR, 
 __device__ __forceinline__ uint32_t bucket_cls(uint32_t total, uint32_t depth) {
   if (total < 2) return 0xffu;
   const uint32_t c = size_cls(total);
-  return (c >= 6 && depth >= kDBig) ? kClsDeep : c;
+  return (c >= kClsPacked && depth >= kDBig) ? kClsDeep : c;
 }
 
 // One workgroup per group: bucket totals and bases, per-tile offsets, and the number of
@@ -397,7 +400,8 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   for (int q = 0; q < 4; q++) cnt[q * kT + d] = 0;
   // (a cache that this pass empties is not stored: the next pass refills it from the text)
   const uint32_t myflag = (total == 1 ? 1u : 0u) |
-                          ((bucket_cls(total, grp_depth(gr) + 1) & ~1u) == 6u && tiled_next_cache(gr) ? 2u : 0u);
+                          (bucket_cls(total, grp_depth(gr) + 1) >= kClsPacked &&
+                           bucket_cls(total, grp_depth(gr) + 1) <= kClsTiled && tiled_next_cache(gr) ? 2u : 0u);
   uint32_t vv[kPerT], kk[kPerT];
   s1_load<false>(B, gr, U, lo, hi, vv, kk);
   __syncthreads();
@@ -618,27 +622,18 @@ __global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __re
     qq[i] = e - S.goff[j];
     vv[i] = ((fl & kGrpAlt) ? B.sa2 : B.sa)[S.gstart[j] + qq[i]];
   }
-  // keys: the cache words are loaded beside the slots (their addresses do not depend on the
-  // rotations); 4 characters of the text only where the cache is empty (identity groups, and
-  // every 4th pass), after the rotation has arrived
-#pragma unroll
-  for (int i = 0; i < (int)kPerTS; i++) {
-    if ((uint32_t)i >= rounds) break;
-    const uint32_t j = jj[i], fl = S.gfl[j];
-    kk[i] = ((fl & kGrpAlt) ? B.sk2 : B.sk)[S.gstart[j] + qq[i]];
-  }
+  // keys: the cache, or 4 characters of the text when the cache is empty (loading the cache
+  // words beside the slot loads instead measured no faster: profiles/r05_ab_*)
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {
     if ((uint32_t)i >= rounds) break;
     const uint32_t j = jj[i], fl = S.gfl[j], o = qq[i];
     if (fl & kGrpIdent) vv[i] = o;
     const bool fresh = (fl & kGrpIdent) || grp_cache(Grp{0, 0, 0, fl}) == 0;
-    qq[i] = 0xffffffffu;  // text position, or none
-    if (fresh) {
-      const uint32_t q = cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j]);
-      qq[i] = q;
-      kk[i] = ld_u32(B.text + S.gtoff[j] + q);
-    }
+    const uint32_t q = cyc_pos(vv[i], fl >> kGrpDepthShift, S.glen[j]);
+    qq[i] = fresh ? q : 0xffffffffu;  // text position, or none
+    kk[i] = ld_u32(fresh ? B.text + S.gtoff[j] + q
+                         : reinterpret_cast<const uint8_t*>(((fl & kGrpAlt) ? B.sk2 : B.sk) + S.gstart[j] + o));
   }
 #pragma unroll
   for (int i = 0; i < (int)kPerTS; i++) {
@@ -707,7 +702,7 @@ __global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __re
       const bool dst_alt = !(fl & kGrpIdent) && !(fl & kGrpAlt);
       // key caches only for buckets that stay in S1 (S2 and S3 read the text), and only when
       // this pass leaves a byte in them
-      if (bucket_cls(total, grp_depth(Grp{0, 0, 0, fl}) + 1) == 6u && s1_next_cache(Grp{0, 0, 0, fl}))
+      if (bucket_cls(total, grp_depth(Grp{0, 0, 0, fl}) + 1) == kClsPacked && s1_next_cache(Grp{0, 0, 0, fl}))
         (dst_alt ? B.sk2 : B.sk)[slot] = kk[i] << 8;
       if (total == 1) {
         if (dst_alt) B.sa[slot] = v;
@@ -1134,16 +1129,32 @@ __global__ void __launch_bounds__(kT) k_deep_compact2(const Grp* __restrict__ sl
 using BsortKey = uint64_t;
 constexpr BsortKey kPadKey = ~0ull;
 
+// Key layout by elements per wave kE: up to 256 elements, an 8-bit element index under 7
+// characters (first round) or an 8-bit run start, 6 characters and the index (later rounds);
+// 512 elements (class 257..512), 9-bit indices and run starts with 6 / 5 characters.
+template <int kE>
+struct KeyFmt {
+  static constexpr int kIb = kE > 256 ? 9 : 8;  // index / run-start bits
+  static constexpr int kC1 = kE > 256 ? 6 : 7;  // characters of a first-round key
+  static constexpr int kC2 = kE > 256 ? 5 : 6;  // characters of a later-round key
+  static_assert(kE <= 512, "keys index at most 512 elements");
+};
+template <int kE = 256>
 __device__ __forceinline__ BsortKey make_key1(uint32_t hi, uint32_t lo, uint32_t idx) {
-  return ((((uint64_t)hi << 32) | lo) & ~0xffull) | idx;
+  constexpr int kDrop = 64 - 8 * KeyFmt<kE>::kC1;  // low bits below the kept characters
+  return ((((uint64_t)hi << 32) | lo) & ~((1ull << kDrop) - 1ull)) | idx;
 }
+template <int kE = 256>
 __device__ __forceinline__ BsortKey make_key2(uint32_t rs, uint32_t hi, uint32_t lo, uint32_t idx) {
-  return ((uint64_t)rs << 56) | (((((uint64_t)hi << 32) | lo) >> 16) << 8) | idx;
+  constexpr int kIb = KeyFmt<kE>::kIb, kCb = 8 * KeyFmt<kE>::kC2;
+  return ((uint64_t)rs << (64 - kIb)) | (((((uint64_t)hi << 32) | lo) >> (64 - kCb)) << (64 - kIb - kCb)) | idx;
 }
 __device__ __forceinline__ bool key_valid(BsortKey k) { return k != kPadKey; }
-__device__ __forceinline__ uint32_t key_idx(BsortKey k) { return (uint32_t)k & 0xffu; }
+template <int kE = 256>
+__device__ __forceinline__ uint32_t key_idx(BsortKey k) { return (uint32_t)k & ((1u << KeyFmt<kE>::kIb) - 1u); }
 // same run start and characters (index ignored)
-__device__ __forceinline__ bool key_tied(BsortKey a, BsortKey b) { return (a >> 8) == (b >> 8); }
+template <int kE = 256>
+__device__ __forceinline__ bool key_tied(BsortKey a, BsortKey b) { return (a >> KeyFmt<kE>::kIb) == (b >> KeyFmt<kE>::kIb); }
 __device__ __forceinline__ bool key_less(BsortKey a, BsortKey b) { return a < b; }
 
 
@@ -1498,9 +1509,12 @@ __device__ void bsort_tail(const SortBufs& B, const SortOut& O, const Grp& g, ui
 
 // S2 run emission (classes with one group per wave): after kRounds rounds the runs still tied
 // are left as new groups.  Their rotations are stored at their slots (primary SA) and each run
-// becomes a record (depth:15 | run start:8 | size:9) in the group's own part of `rec` (from
+// becomes a record (depth:13 | run start:9 | size:10) in the group's own part of `rec` (from
 // half its first slot; a group of m has at most m / 2 runs), with per-class counts
 // ccnt[c * total + gbase + list index] for the class-major scan.  k_s2_emit builds the lists.
+__device__ __forceinline__ uint32_t s2_rec(uint32_t depth, uint32_t rs, uint32_t size) {
+  return (depth << 19) | (rs << 10) | size;
+}
 struct S2Emit {
   uint32_t* rec;
   uint32_t* ccnt;
@@ -1566,8 +1580,9 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       if (valid && q + 16 > U.len) text_words_wrap<4>(t, U.len, q, k4);
       Lv[w][idx] = vq[r];
       Lc[w][idx] = (uint8_t)(cq[r] >> 24);
-      Lx[w][idx] = ((uint64_t)((k4[1] << 24) | (k4[2] >> 8)) << 32) | ((k4[2] << 24) | (k4[3] >> 8));
-      K[r] = valid ? make_key1(k4[0], k4[1], idx) : kPadKey;
+      constexpr uint32_t kSh = 8 * (KeyFmt<kE>::kC1 - 4);  // the 8 characters after the first kC1
+      Lx[w][idx] = ((uint64_t)((k4[1] << kSh) | (k4[2] >> (32 - kSh))) << 32) | ((k4[2] << kSh) | (k4[3] >> (32 - kSh)));
+      K[r] = valid ? make_key1<kE>(k4[0], k4[1], idx) : kPadKey;
     }
   } else if constexpr (kBatch) {
     // all loads issued before any is used (3 aligned words and the BWT byte per rotation);
@@ -1589,7 +1604,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       if (valid && q + 8 > U.len) text_words_wrap<2>(t, U.len, q, k2);
       Lv[w][idx] = vq[r];
       Lc[w][idx] = (uint8_t)(cq[r] >> 24);
-      K[r] = valid ? make_key1(k2[0], k2[1], idx) : kPadKey;
+      K[r] = valid ? make_key1<kE>(k2[0], k2[1], idx) : kPadKey;
     }
   } else {
 #pragma unroll
@@ -1604,7 +1619,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       }
       Lv[w][idx] = vq[r];
       Lc[w][idx] = c;
-      K[r] = valid ? make_key1(hi, lo, idx) : kPadKey;
+      K[r] = valid ? make_key1<kE>(hi, lo, idx) : kPadKey;
     }
   }
   bool done[kPer];
@@ -1615,7 +1630,8 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   uint32_t maxrun = 0;  // longest tied run of the previous round (kSeg = 64)
   // BZG_DEBUG: waves entering each round, per class (dbg[8 + 8 * class + round]; round 7:
   // the rank-counting tail)
-  constexpr int kDbgCls = kSeg * kPer == 16 ? 1 : kSeg * kPer == 32 ? 2 : kSeg * kPer == 64 ? 3 : kSeg * kPer == 128 ? 4 : 5;
+  constexpr int kDbgCls = kSeg * kPer == 16 ? 1 : kSeg * kPer == 32 ? 2 : kSeg * kPer == 64 ? 3 : kSeg * kPer == 128 ? 4
+                         : kSeg * kPer == 256 ? 5 : 6;
   for (;;) {
     if (O.dbg && lane == 0) atomicAdd(&O.dbg[8 + 8 * kDbgCls + min(round, 6)], 1ull);
     if (O.dbg && round > 0 && kDbgCls >= 3) {  // later rounds: longest tied run and tied elements
@@ -1644,7 +1660,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         q = key_shfl_up1(K[kPer - 1]);
         if (sl == 0) q = ~K[r];  // no previous element
       }
-      tp[r] = key_valid(K[r]) && key_tied(q, K[r]);
+      tp[r] = key_valid(K[r]) && key_tied<kE>(q, K[r]);
     }
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
@@ -1671,7 +1687,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
       rsn[r] = max(rsn[r], pre);
-      const uint32_t idx = key_idx(K[r]);
+      const uint32_t idx = key_idx<kE>(K[r]);
       const bool valid = key_valid(K[r]);
       const bool tied = valid && (tp[r] || tn[r]);
       const uint32_t p = sl * kPer + r;
@@ -1688,7 +1704,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       any_tied |= tied;
     }
     if (__ballot(any_tied) == 0) break;
-    depth += round == 0 ? 7 : 6;  // tied runs are equal to this depth
+    depth += round == 0 ? KeyFmt<kE>::kC1 : KeyFmt<kE>::kC2;  // tied runs are equal to this depth
     if constexpr (kSeg == 64 && kPer <= 2) {  // (kPer 4: the registers would cost a wave per SIMD)
       bool split = false;  // the group is no longer one run
 #pragma unroll
@@ -1699,7 +1715,7 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
 #pragma unroll
         for (int r = 0; r < kPer; r++) {
           live[r] = key_valid(K[r]);
-          vv[r] = live[r] ? Lv[w][key_idx(K[r])] : 0u;
+          vv[r] = live[r] ? Lv[w][key_idx<kE>(K[r])] : 0u;
         }
         const uint32_t d2 = common_depth<kPer>(t, U.len, vv, live, depth, B.dwave);
         skipped |= d2 != depth;
@@ -1728,19 +1744,19 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
           for (int r = 0; r < kPer; r++) {
             if (!key_valid(K[r]) || done[r]) continue;
             const uint32_t p = sl * kPer + r;
-            B.sa[g.start + p] = Lv[w][key_idx(K[r])];
+            B.sa[g.start + p] = Lv[w][key_idx<kE>(K[r])];
             if (!tn[r]) {  // last member of its run
               const uint32_t size = p - rsn[r] + 1;
               if (depth >= B.dwave) {  // still tied after B.dwave characters: doubling fallback
                 O.deep[wave_append(O.n_deep, true)] = Grp{g.start + rsn[r], size, g.unit, grp_flags(0u, depth, 2u)};
               } else {
                 atomicAdd(&cc[size_cls(size)], 1u);
-                E.rec[g.start / 2 + atomicAdd(&cc[7], 1u)] = (depth << 17) | (rsn[r] << 9) | size;
+                E.rec[g.start / 2 + atomicAdd(&cc[7], 1u)] = s2_rec(depth, rsn[r], size);
               }
             }
           }
           wave_sync();
-          if (lane < 6) E.ccnt[(size_t)lane * E.total + E.gbase + bi] = cc[lane];
+          if (lane < (uint32_t)kS2Cls) E.ccnt[(size_t)lane * E.total + E.gbase + bi] = cc[lane];
           break;
         }
       } else {
@@ -1752,11 +1768,11 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
     // re-key the tied runs 8 characters deeper; unique elements keep their own position as run start
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
-      const uint32_t idx = key_idx(K[r]);
+      const uint32_t idx = key_idx<kE>(K[r]);
       if (!key_valid(K[r])) continue;
       const uint32_t p = sl * kPer + r;
       if (done[r]) {
-        K[r] = make_key2(p, 0, 0, idx);
+        K[r] = make_key2<kE>(p, 0, 0, idx);
       } else {
         uint32_t hi, lo;
         if (kPre && round == 1 && !skipped) {
@@ -1766,49 +1782,50 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
         } else {
           text_key8(t, U.len, cyc_pos(Lv[w][idx], depth, U.len), hi, lo);
         }
-        K[r] = make_key2(rsn[r], hi, lo, idx);
+        K[r] = make_key2<kE>(rsn[r], hi, lo, idx);
       }
     }
   }
 }
 
 // The records of the emitting k_bsort launches into the next class lists.  One thread per
-// group g of the concatenated classes 3..5 (gb[c]: index of class c's first group, c = 3..6).
+// group g of the concatenated classes 3..6 (gb[k]: index of class 3 + k's first group; gb[4]:
+// the total).
 struct S2Lists {
-  const Grp* cur[3];
-  uint32_t gb[4];
+  const Grp* cur[4];
+  uint32_t gb[5];
 };
 __global__ void k_s2_emit(S2Lists Ls, const uint32_t* __restrict__ rec, const uint32_t* __restrict__ cscan,
                           uint32_t total, ClsLists N) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= total) return;
-  uint32_t n = 0, pos[6];
+  uint32_t n = 0, pos[kS2Cls];
 #pragma unroll
-  for (int c = 0; c < 6; c++) {
+  for (int c = 0; c < kS2Cls; c++) {
     const uint32_t a = cscan[(size_t)c * total + g], e = cscan[(size_t)c * total + g + 1];
     pos[c] = a - cscan[(size_t)c * total];
     n += e - a;
   }
   if (n == 0) return;
-  const int k = g >= Ls.gb[2] ? 2 : g >= Ls.gb[1] ? 1 : 0;
+  const int k = g >= Ls.gb[3] ? 3 : g >= Ls.gb[2] ? 2 : g >= Ls.gb[1] ? 1 : 0;
   const Grp gr = Ls.cur[k][g - Ls.gb[k]];
   const uint32_t* gr_rec = rec + gr.start / 2;
   for (uint32_t x = 0; x < n; x++) {
     const uint32_t r = gr_rec[x];
-    const uint32_t size = r & 511u, rs = (r >> 9) & 255u, depth = r >> 17;
+    const uint32_t size = r & 1023u, rs = (r >> 10) & 511u, depth = r >> 19;
     const uint32_t c = size_cls(size);
     uint32_t p = 0;
 #pragma unroll
-    for (int q = 0; q < 6; q++)
+    for (int q = 0; q < kS2Cls; q++)
       if ((uint32_t)q == c) p = pos[q]++;
     N.l[c][p] = Grp{gr.start + rs, size, gr.unit, grp_flags(0u, depth, 0u)};
   }
 }
 
-// out[c] = size of class c in a class-major scan of 6 classes (c < 6).
+// out[c] = size of class c in a class-major scan of the S2 classes (c < kS2Cls).
 __global__ void k_s2_bounds(const uint32_t* __restrict__ cscan, uint32_t total, uint32_t* __restrict__ out) {
   const uint32_t c = threadIdx.x;
-  if (c < 6) out[c] = cscan[(size_t)(c + 1) * total] - cscan[(size_t)c * total];
+  if (c < (uint32_t)kS2Cls) out[c] = cscan[(size_t)(c + 1) * total] - cscan[(size_t)c * total];
 }
 
 // ---------------------------------------------------------------- S2 lists in block order
@@ -2329,8 +2346,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     ccap[c] = S / minsz + nb + 16;
     C.l[c] = ws.typed<Grp>("sort_cls" + std::to_string(c), ccap[c]);
   }
-  Grp* nxt6 = ws.typed<Grp>("sort_nxt6", ccap[6]);
-  Grp* nxt7 = ws.typed<Grp>("sort_nxt7", ccap[7]);
+  Grp* nxt6 = ws.typed<Grp>("sort_nxt6", ccap[kClsPacked]);  // (6 / 7 in names: packed / tiled)
+  Grp* nxt7 = ws.typed<Grp>("sort_nxt7", ccap[kClsTiled]);
   SortOut O{};
   O.bwt = bwt;
   O.rank0 = rank0;
@@ -2341,27 +2358,28 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     O.dbg = reinterpret_cast<unsigned long long*>(ws.u32("sort_dbg", 256));
     HIP_OK(hipMemsetAsync(O.dbg, 0, 1024, st));
   }
-  // counters: 0..7 class counts (init), 8..16 class bounds + total, 17 tiles, 18 packed total,
-  // 19 n_deep, 20 min depth
+  // counters: 0..8 class counts (init), 16 class-major scan total, 17 tiles, 18 packed total,
+  // 19 n_deep, 20 min depth, 21 / 22 deep pairs, 24..30 S2 class sizes, 32 / 33 pair splits,
+  // 40..49 class bounds + total
   uint32_t* cnt = ws.u32("sort_cnt", 64);  // counters: see below; 24..29 S2 class sizes
   O.n_deep = cnt + 19;
-  const size_t max_tiles = S / kDTile + ccap[7] + 16;
+  const size_t max_tiles = S / kDTile + ccap[kClsTiled] + 16;
   const size_t max_ptiles = S / kSG + 64;
-  const size_t max_tot = ccap[7] + max_ptiles;
+  const size_t max_tot = ccap[kClsTiled] + max_ptiles;
   uint32_t* TP = ws.u32("sort_TP", max_tiles + 16);
   TileRec* TR = ws.typed<TileRec>("sort_TR", max_tiles + 16);
   uint32_t* hist = ws.u32("sort_hist", max_tiles * 256);
-  uint32_t* tot = ws.u32("sort_tot", ccap[7] * 256);
+  uint32_t* tot = ws.u32("sort_tot", ccap[kClsTiled] * 256);
   uint32_t* ccnt = ws.u32("sort_ccnt", kNCls * max_tot + 16);
-  uint32_t* P = ws.u32("sort_P", ccap[6] + 16);
-  Unit* gunits = ws.typed<Unit>("sort_gunits", ccap[6] + 16);  // the packed groups' units
+  uint32_t* P = ws.u32("sort_P", ccap[kClsPacked] + 16);
+  Unit* gunits = ws.typed<Unit>("sort_gunits", ccap[kClsPacked] + 16);  // the packed groups' units
   uint32_t* first = ws.u32("sort_first", max_ptiles);
   uint32_t* last = ws.u32("sort_last", max_ptiles);
   uint32_t* nrec = ws.u32("sort_nrec", max_ptiles);
   uint32_t* srec = ws.u32("sort_rec", S + 64);  // bucket records of the packed passes and of S2
   uint32_t* scratch =
-      ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[6])) + 64);
-  uint32_t hc[48];
+      ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[kClsPacked])) + 64);
+  uint32_t hc[64];
   auto read_counters = [&]() {
     HIP_OK(hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -2388,9 +2406,9 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   read_counters();
   uint32_t ncls[kNCls];
   for (int c = 0; c < kNCls; c++) ncls[c] = hc[c];
-  uint32_t n6 = ncls[6], n7 = ncls[7];
-  Grp* cur6 = C.l[6];
-  Grp* cur7 = C.l[7];
+  uint32_t n6 = ncls[kClsPacked], n7 = ncls[kClsTiled];
+  Grp* cur6 = C.l[kClsPacked];
+  Grp* cur7 = C.l[kClsTiled];
   int passes = 0;
   uint64_t s1_elems = 0;
   // ---- S1: byte passes over the buckets larger than kBig (tiled groups > kSG, packed ones <= kSG)
@@ -2434,13 +2452,13 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * nTot, cnt + 16, scratch, st);
-    k_cls_bounds<<<1, 64, 0, st>>>(ccnt, nTot, cnt + 16, cnt + 8);
+    k_cls_bounds<<<1, 64, 0, st>>>(ccnt, nTot, cnt + 16, cnt + 40);
     HIP_OK(hipGetLastError());
     ClsLists Cp = C;
-    for (int c = 0; c < 6; c++) Cp.base[c] = ncls[c];
-    Cp.l[6] = nxt6;
-    Cp.l[7] = nxt7;
-    Cp.base[6] = Cp.base[7] = 0;
+    for (int c = 0; c < kS2Cls; c++) Cp.base[c] = ncls[c];
+    Cp.l[kClsPacked] = nxt6;
+    Cp.l[kClsTiled] = nxt7;
+    Cp.base[kClsPacked] = Cp.base[kClsTiled] = 0;
     if (n7) {
       k_s1_scatter<<<ntl, kT, 0, st>>>(TR, B, O, hist, tot, ccnt, nTot, Cp);
       HIP_OK(hipGetLastError());
@@ -2452,30 +2470,30 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     read_counters();
-    for (int c = 0; c < 6; c++) ncls[c] += hc[8 + c + 1] - hc[8 + c];
-    n6 = hc[8 + 7] - hc[8 + 6];
-    n7 = hc[8 + 8] - hc[8 + 7];
+    for (int c = 0; c < kS2Cls; c++) ncls[c] += hc[40 + c + 1] - hc[40 + c];
+    n6 = hc[40 + kClsPacked + 1] - hc[40 + kClsPacked];
+    n7 = hc[40 + kClsTiled + 1] - hc[40 + kClsTiled];
     std::swap(cur6, nxt6);
     std::swap(cur7, nxt7);
   }
   // ---- S2: every size class
   if (debug)
-    fprintf(stderr, "[bzg sort S2] buckets by class: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", ncls[0],
-            ncls[1], ncls[2], ncls[3], ncls[4], ncls[5]);
+    fprintf(stderr, "[bzg sort S2] buckets by class: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u 257-512:%u\n",
+            ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5], ncls[6]);
   // bitonic rounds before the rank-counting tail (classes 1, 2) or before the still-tied runs
-  // are emitted as new groups (classes 3..5, one group per wave; the S2 loop repeats until
+  // are emitted as new groups (classes 3..6, one group per wave; the S2 loop repeats until
   // every list is empty)
-  constexpr int kR3 = 8, kR4 = 2, kR5 = 2;  // (profiles/r03_*, r04_*: 3 or 4 rounds for class 3 slower)
+  constexpr int kR3 = 8, kR4 = 2, kR5 = 2, kR6 = 2;  // (profiles/r03_*, r04_*: 3 or 4 rounds for class 3 slower)
   {
     ClsLists N{};
-    for (int c = 0; c < 6; c++) N.l[c] = ws.typed<Grp>("sort_s2n" + std::to_string(c), ccap[c]);
+    for (int c = 0; c < kS2Cls; c++) N.l[c] = ws.typed<Grp>("sort_s2n" + std::to_string(c), ccap[c]);
     {  // block order for the first S2 round (see k_unit_count)
       // A list of more than S / 32 groups (high-entropy input: millions of small
       // buckets, most of them settled by their first 16 characters) stays as it is: its
       // reorder would cost more than the L2 locality it buys.
       constexpr uint64_t reorder_div = 32;  // profiles/r04_ab_s2_reorder.txt
       uint32_t* ucnt = ws.u32("sort_ucnt", nb + 64);
-      for (int c = 0; c < 6; c++) {
+      for (int c = 0; c < kS2Cls; c++) {
         if (ncls[c] < 2) continue;
         if ((uint64_t)ncls[c] * reorder_div > S) continue;
         HIP_OK(hipMemsetAsync(ucnt, 0, 4 * (size_t)nb, st));
@@ -2487,18 +2505,18 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         std::swap(C.l[c], N.l[c]);
       }
     }
-    const size_t max_s2 = ccap[3] + ccap[4] + ccap[5];
+    const size_t max_s2 = ccap[3] + ccap[4] + ccap[5] + ccap[6];
     Grp* tiny2 = ws.typed<Grp>("sort_tiny2", ccap[0]);
     Grp* tiny8 = ws.typed<Grp>("sort_tiny8", ccap[0]);
-    uint32_t* ccnt2 = ws.u32("sort_s2cnt", 6 * max_s2 + 16);
-    uint32_t* scratch2 = ws.u32("sort_s2scan", scan_scratch_words(6 * max_s2 + 16) + 64);
+    uint32_t* ccnt2 = ws.u32("sort_s2cnt", kS2Cls * max_s2 + 16);
+    uint32_t* scratch2 = ws.u32("sort_s2scan", scan_scratch_words(kS2Cls * max_s2 + 16) + 64);
     int s2_iters = 0;
     for (;;) {
       ++s2_iters;
       if (debug)
-        fprintf(stderr, "[bzg sort S2] iter %d: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u\n", s2_iters,
-                ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5]);
-      for (int c = 0; c < 6; c++) check_list(C.l[c], ncls[c], "S2", s2_iters, c);
+        fprintf(stderr, "[bzg sort S2] iter %d: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u 257-512:%u\n",
+                s2_iters, ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5], ncls[6]);
+      for (int c = 0; c < kS2Cls; c++) check_list(C.l[c], ncls[c], "S2", s2_iters, c);
       if (ncls[0]) {
         HIP_OK(hipMemsetAsync(cnt + 32, 0, 8, st));
         k_split_pairs<<<ceil_div(ncls[0], kT * kSplitPer), kT, 0, st>>>(C.l[0], ncls[0], tiny2, tiny8, cnt + 32);
@@ -2540,23 +2558,26 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
                                                                              O.n_deep);
       }
       HIP_OK(hipGetLastError());
-      const uint32_t total = ncls[3] + ncls[4] + ncls[5];
+      const uint32_t total = ncls[3] + ncls[4] + ncls[5] + ncls[6];
       if (total == 0) break;
-      HIP_OK(hipMemsetAsync(ccnt2, 0, (6 * (size_t)total + 1) * 4, st));
+      HIP_OK(hipMemsetAsync(ccnt2, 0, (kS2Cls * (size_t)total + 1) * 4, st));
       S2Emit E{srec, ccnt2, total, 0};
       if (ncls[3]) k_bsort<64, 1, kR3, false, true><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O, E);
       E.gbase += ncls[3];
       if (ncls[4]) k_bsort<64, 2, kR4, true, true><<<ceil_div(ncls[4], kT / 64), kT, 0, st>>>(C.l[4], ncls[4], B, O, E);
       E.gbase += ncls[4];
       if (ncls[5]) k_bsort<64, 4, kR5, false, true><<<ceil_div(ncls[5], kT / 64), kT, 0, st>>>(C.l[5], ncls[5], B, O, E);
+      E.gbase += ncls[5];
+      if (ncls[6]) k_bsort<64, 8, kR6, false, true><<<ceil_div(ncls[6], kT / 64), kT, 0, st>>>(C.l[6], ncls[6], B, O, E);
       HIP_OK(hipGetLastError());
-      scan_u32(ScanOp::Sum, true, ccnt2, ccnt2, 6 * (size_t)total + 1, nullptr, scratch2, st);
-      S2Lists Ls{{C.l[3], C.l[4], C.l[5]}, {0, ncls[3], ncls[3] + ncls[4], total}};
+      scan_u32(ScanOp::Sum, true, ccnt2, ccnt2, kS2Cls * (size_t)total + 1, nullptr, scratch2, st);
+      S2Lists Ls{{C.l[3], C.l[4], C.l[5], C.l[6]},
+                 {0, ncls[3], ncls[3] + ncls[4], ncls[3] + ncls[4] + ncls[5], total}};
       k_s2_emit<<<grid(total), kT, 0, st>>>(Ls, srec, ccnt2, total, N);
       k_s2_bounds<<<1, 64, 0, st>>>(ccnt2, total, cnt + 24);
       HIP_OK(hipGetLastError());
       read_counters();
-      for (int c = 0; c < 6; c++) {
+      for (int c = 0; c < kS2Cls; c++) {
         ncls[c] = hc[24 + c];
         std::swap(C.l[c], N.l[c]);
       }
@@ -2566,14 +2587,14 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       unsigned long long d[64];
       HIP_OK(hipMemcpyAsync(d, O.dbg, sizeof(d), hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
-      for (int c = 1; c < 6; c++)
+      for (int c = 1; c < kS2Cls; c++)
         fprintf(stderr, "[bzg sort S2] class %d waves by round: %llu %llu %llu %llu %llu %llu %llu+ tail %llu\n", c,
                 d[8 + 8 * c], d[9 + 8 * c], d[10 + 8 * c], d[11 + 8 * c], d[12 + 8 * c], d[13 + 8 * c], d[14 + 8 * c],
                 d[15 + 8 * c]);
-      unsigned long long e[48];
+      unsigned long long e[64];
       HIP_OK(hipMemcpyAsync(e, O.dbg + 64, sizeof(e), hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
-      for (int c = 3; c < 6; c++) {
+      for (int c = 3; c < kS2Cls; c++) {
         const unsigned long long* x = e + 16 * (c - 3);
         fprintf(stderr, "[bzg sort S2] class %d later rounds: longest run <=4:%llu <=8:%llu <=16:%llu <=32:%llu <=64:%llu >64:%llu"
                 " | tied <=4:%llu <=8:%llu <=16:%llu <=32:%llu <=64:%llu >64:%llu\n", c, x[0], x[1], x[2], x[3], x[4], x[5],
