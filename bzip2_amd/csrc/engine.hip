@@ -1109,21 +1109,24 @@ int bzg_find_magics(const void* d_in, uint64_t n, uint64_t* out, uint64_t cap, u
   });
 }
 
-// Host buffers of large inputs: the input goes over in pieces of growing size (the first small,
-// so that compression starts early; then each twice the one before), on the engine's copy
-// stream from a copier thread, while the main thread compresses the pieces that have arrived as
-// consecutive segments of one stream (a non-final segment emits its complete blocks and the
-// rest is resubmitted with the next piece, exactly as bzg_compress_device cuts a large input into
+// Host buffers of large inputs: the input goes over in pieces, on the engine's copy stream from a
+// copier thread, while the main thread compresses the pieces that have arrived as consecutive
+// segments of one stream (a non-final segment emits its complete blocks and the rest is
+// resubmitted with the next piece, exactly as bzg_compress_device cuts a large input into
 // batches, so the bytes equal one call's); each segment's output goes back from a second thread
 // while the next one is compressed.  Only the first piece's upload and the last segment's
-// download are not overlapped.
+// download are not overlapped.  A call has a fixed cost of about 5 ms besides its ~50 ms per GB
+// (host synchronisations of the sort passes, narrow late passes), so pieces are few: the first
+// a fifth of the input (its compression covers the upload of the rest, which runs at ~50 GB/s),
+// the rest in one piece when it is at most four times the first (1 GB: 200 + 800 MB), else in
+// pieces doubling in size (h2h timeline: profiles/r05_h2h_*.txt).
 static constexpr uint64_t kPipeMin = 192ull << 20;  // smaller inputs: one upload, one call, one download
 static constexpr uint64_t kPipeFirst = 96ull << 20;
 
 static std::vector<uint64_t> pipe_pieces(uint64_t n) {
   std::vector<uint64_t> b{0};
-  uint64_t s = std::max<uint64_t>(kPipeFirst, n / 10);
-  while (n - b.back() >= 3 * s) {  // the remainder is at least 1.5 pieces of the next size
+  uint64_t s = std::max<uint64_t>(kPipeFirst, n / 5);
+  while (n - b.back() > 4 * s) {
     b.push_back(b.back() + s);
     s *= 2;
   }
@@ -1148,8 +1151,8 @@ static int host_call_pipelined(Engine* e, const uint8_t* src, uint64_t n, unsign
   std::vector<Down> downs;  // segment outputs to copy back, in order
   bool all_queued = false, down_failed = false;
   const int dev = e->device;
-  // BZG_DEBUG: host times (ms since the call) of each piece's upload, compression and download
-  static const bool dbg = getenv("BZG_DEBUG") != nullptr;
+  // BZG_H2H_DEBUG: host times (ms since the call) of each piece's upload, compression and download
+  static const bool dbg = getenv("BZG_H2H_DEBUG") != nullptr;
   const auto t0 = std::chrono::steady_clock::now();
   auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
   std::thread up([&] {

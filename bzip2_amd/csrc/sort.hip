@@ -129,7 +129,8 @@ __device__ __forceinline__ void text_words_wrap(const uint8_t* t, uint32_t len, 
 // elements before it uses any.
 template <int N>
 __device__ __forceinline__ void text_raw(const uint8_t* p, uint32_t (&x)[N + 1]) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+  // (pointer arithmetic, not an integer round trip, so the loads stay global_load, not flat)
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p - ((uintptr_t)p & 3u));
 #pragma unroll
   for (int i = 0; i <= N; i++) x[i] = w[i];
 }
@@ -144,7 +145,7 @@ __device__ __forceinline__ void text_words_of(const uint8_t* p, const uint32_t (
 __device__ __forceinline__ void text_key16(const uint8_t* t, uint32_t len, uint32_t q, uint32_t (&k)[4]) {
   if (q + 16 <= len) {
     const uintptr_t a = (uintptr_t)(t + q);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(t + q - (a & 3u));
     const uint32_t sh = (uint32_t)(a & 3u);  // byte shift
     const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
     k[0] = __builtin_bswap32(__builtin_amdgcn_alignbyte(x1, x0, sh));
@@ -790,7 +791,7 @@ __global__ void k_cls_bounds(const uint32_t* __restrict__ cscan, uint32_t nTot, 
 __device__ __forceinline__ void text_key8(const uint8_t* t, uint32_t len, uint32_t q, uint32_t& hi, uint32_t& lo) {
   if (q + 8 <= len) {
     const uintptr_t a = (uintptr_t)(t + q);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(t + q - (a & 3u));
     const uint32_t sh = (uint32_t)(a & 3u);
     const uint32_t x0 = w[0], x1 = w[1], x2 = w[2];
     hi = __builtin_bswap32(__builtin_amdgcn_alignbyte(x1, x0, sh));
