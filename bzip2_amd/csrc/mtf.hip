@@ -77,10 +77,11 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
                                             uint32_t* __restrict__ siglen) {
   const ChunkRef r = chunk_ref(boff, cbase);
   if (!r.valid) return;
-  // the signature leaves four bytes per store (a store per new symbol was most of the kernel's
-  // time on high-entropy input: ~250 scattered byte stores per chunk)
-  uint32_t* out = reinterpret_cast<uint32_t*>(sig + (size_t)r.gidx * 256);
-  uint32_t cnt = 0, acc = 0;
+  // the signature leaves sixteen bytes per store (a store per new symbol was most of the
+  // kernel's time on high-entropy input: ~250 scattered byte stores per chunk; four bytes per
+  // store still left ~63 per chunk)
+  uint4* out = reinterpret_cast<uint4*>(sig + (size_t)r.gidx * 256);
+  uint32_t cnt = 0, acc[4] = {0, 0, 0, 0};
   uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // seen bytes, in registers
   const uint32_t a_lo = r.lo & ~15u;
   uint32_t a = (r.hi - 1) & ~15u;  // word being processed (walking down to a_lo)
@@ -112,10 +113,12 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
           s1 |= qq == 1 ? bit : 0ull;
           s2 |= qq == 2 ? bit : 0ull;
           s3 |= qq == 3 ? bit : 0ull;
-          acc |= c << (8 * (cnt & 3u));
-          if ((++cnt & 3u) == 0) {
-            out[(cnt >> 2) - 1] = acc;
-            acc = 0;
+          const uint32_t wi = (cnt >> 2) & 3u, sh = c << (8 * (cnt & 3u));
+#pragma unroll
+          for (uint32_t k = 0; k < 4; k++) acc[k] |= wi == k ? sh : 0u;
+          if ((++cnt & 15u) == 0) {
+            out[(cnt >> 4) - 1] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+            acc[0] = acc[1] = acc[2] = acc[3] = 0;
           }
         }
       }
@@ -123,7 +126,7 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
     if (a <= a_lo) break;
     a -= 16;
   }
-  if (cnt & 3u) out[cnt >> 2] = acc;
+  if (cnt & 15u) out[cnt >> 4] = make_uint4(acc[0], acc[1], acc[2], acc[3]);  // (bytes past cnt: unused)
   siglen[r.gidx] = cnt;
 }
 
