@@ -793,8 +793,7 @@ uint64_t code_emit(Workspace& ws, const std::vector<CodePart>& parts, int level,
     HIP_OK(hipGetLastError());
   }
   uint64_t hch[2];
-  HIP_OK(hipMemcpyAsync(hch, chain, 16, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  ws.read_small(hch, chain, 16, st);
   const uint64_t total_bits = hch[0];
   const uint32_t comb_h = (uint32_t)hch[1];
   const uint64_t end_bits = total_bits + (final_batch ? 80 : 0);

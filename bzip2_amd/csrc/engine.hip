@@ -31,6 +31,74 @@ namespace bzg {
 Workspace::~Workspace() {
   release_all();
   if (handoff_) (void)hipEventDestroy(handoff_);
+  if (mbox_) (void)hipHostFree(mbox_);
+}
+
+// read_small: the words of up to four pieces to pinned host memory, then the flag (release at
+// system scope after every word is visible)
+constexpr uint32_t kMboxWords = 8192;
+struct MboxPieces {
+  const uint32_t* src[4];
+  uint32_t nw[4], at[4];
+};
+__global__ void __launch_bounds__(256) k_mbox(MboxPieces P, uint32_t* dst, uint32_t* flag, uint32_t seq) {
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    for (uint32_t i = threadIdx.x; i < P.nw[k]; i += 256) dst[P.at[k] + i] = P.src[k][i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void Workspace::read_small(void* dst, const void* dev_src, size_t bytes, hipStream_t st) {
+  read_small({SmallRead{dst, dev_src, bytes}}, st);
+}
+
+void Workspace::read_small(std::initializer_list<SmallRead> reads, hipStream_t st) {
+  MboxPieces P{};
+  uint32_t total = 0;
+  bool fast = reads.size() <= 4;
+  int k = 0;
+  for (const SmallRead& r : reads) {
+    const size_t nw = (r.bytes + 3) / 4;
+    fast = fast && (reinterpret_cast<uintptr_t>(r.src) & 3u) == 0 && total + nw <= kMboxWords;
+    if (k < 4) {
+      P.src[k] = static_cast<const uint32_t*>(r.src);
+      P.nw[k] = (uint32_t)nw;
+      P.at[k] = total;
+    }
+    total += (uint32_t)std::min<size_t>(nw, kMboxWords + 1);
+    k++;
+  }
+  if (!fast) {
+    for (const SmallRead& r : reads) HIP_OK(hipMemcpyAsync(r.dst, r.src, r.bytes, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    return;
+  }
+  if (!mbox_) {
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&mbox_), (kMboxWords + 16) * 4, hipHostMallocCoherent));
+    HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&mbox_dev_), mbox_, 0));
+    mbox_[kMboxWords] = 0;
+  }
+  const uint32_t seq = ++mseq_ == 0 ? ++mseq_ : mseq_;
+  k_mbox<<<1, 256, 0, st>>>(P, mbox_dev_, mbox_dev_ + kMboxWords, seq);
+  HIP_OK(hipGetLastError());
+  uint32_t* flag = mbox_ + kMboxWords;
+  for (uint64_t spins = 1;; spins++) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
+    if ((spins & 1023) == 0) {  // a fault or an error on the stream ends the wait
+      const hipError_t e = hipStreamQuery(st);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
+        for (const SmallRead& r : reads) HIP_OK(hipMemcpy(r.dst, r.src, r.bytes, hipMemcpyDeviceToHost));  // (not expected)
+        return;
+      }
+      if (e != hipErrorNotReady) HIP_OK(e);
+    }
+    __builtin_ia32_pause();
+  }
+  k = 0;
+  for (const SmallRead& r : reads) std::memcpy(r.dst, mbox_ + P.at[k++], r.bytes);
 }
 
 void Workspace::set_stream(hipStream_t s) {
@@ -148,6 +216,7 @@ struct Engine {
   Workspace ws;
   std::vector<std::unique_ptr<Workspace>> pws;  // one per part of a batch
   std::vector<hipEvent_t> psorted;              // per part: its sort is done
+  hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // batch(): MTF start, tables start, tables end
   hipEvent_t ev[6];
   hipEvent_t ev_rle;
 
@@ -232,11 +301,9 @@ struct Engine {
     float mtf_ms = 0, tab_ms = 0, last_post = 0;
     uint64_t sort_iters = 0, sort_unsorted = 0;
     if (nb > 0) {
-      HIP_OK(hipMemcpyAsync(hboff.data(), r.boff, 4 * (nb + 1), hipMemcpyDeviceToHost, s));
-      HIP_OK(hipMemcpyAsync(hper.data(), r.period, 4 * nb, hipMemcpyDeviceToHost, s));
-      HIP_OK(hipMemcpyAsync(hbq.data(), r.bq, 4 * nb, hipMemcpyDeviceToHost, s));
-      HIP_OK(hipMemcpyAsync(hqp.data(), r.qper, 4 * nb, hipMemcpyDeviceToHost, s));
-      HIP_OK(hipStreamSynchronize(s));
+      ws.read_small({{hboff.data(), r.boff, 4ull * (nb + 1)}, {hper.data(), r.period, 4ull * nb}, {hbq.data(), r.bq, 4ull * nb},
+                     {hqp.data(), r.qper, 4ull * nb}},
+                    s);
       uint8_t* bwt = ws.u8("bwt", hboff[nb] + 16);
       uint32_t* rank0 = ws.u32("rank0", nb + 2);
       static const bool one_stream = getenv("BZG_ONE_STREAM") != nullptr;  // per-kernel profiling
@@ -274,12 +341,19 @@ struct Engine {
       std::vector<std::promise<void>> sorted(K);
       std::vector<std::future<void>> sorted_f;
       for (auto& x : sorted) sorted_f.push_back(x.get_future());
+      // raised right after a part's promise is settled: the main thread spins on it rather
+      // than sleeping in the future (a wake-up took ~50 us of idle device per part)
+      std::unique_ptr<std::atomic<int>[]> settled(new std::atomic<int>[K]);
+      for (uint32_t p = 0; p < K; p++) settled[p].store(0);
       const int dev = device;
       auto sorter = [&, dev](int t) {
         try {
           HIP_OK(hipSetDevice(dev));  // the current device is per host thread
         } catch (...) {
-          for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) sorted[p].set_exception(std::current_exception());
+          for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) {
+            sorted[p].set_exception(std::current_exception());
+            settled[p].store(1, std::memory_order_release);
+          }
           return;
         }
         hipStream_t ss = S == 1 ? s : sstream[t];
@@ -287,6 +361,7 @@ struct Engine {
         for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) {
           if (failed) {
             sorted[p].set_exception(std::make_exception_ptr(HipFailure(hipErrorUnknown)));
+            settled[p].store(1, std::memory_order_release);
             continue;
           }
           try {
@@ -301,25 +376,27 @@ struct Engine {
             failed = true;
             sorted[p].set_exception(std::current_exception());
           }
+          settled[p].store(1, std::memory_order_release);
         }
       };
       // the timing events exist before any sorter thread starts, so every exit path below
       // joins the threads
-      hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-      HIP_OK(hipEventCreate(&e0));
-      HIP_OK(hipEventCreate(&e1));
-      HIP_OK(hipEventCreate(&e2));
+      for (hipEvent_t& e : tev)
+        if (!e) HIP_OK(hipEventCreate(&e));
+      hipEvent_t e0 = tev[0], e1 = tev[1], e2 = tev[2];
       std::vector<std::thread> th;
       std::exception_ptr err;
       try {
-        if (S > 1)
-          for (int t = 0; t < S; t++) th.emplace_back(sorter, t);
-        else
-          sorter(0);
+        // this thread sorts the first stream's parts itself (one thread fewer to start, and it
+        // does not sit idle)
+        for (int t = 1; t < S; t++) th.emplace_back(sorter, t);
+        sorter(0);
         // measured (profiles/r03_pipeline_sweep.txt): MTF and tables beside the later sorts
         // slow both more than they overlap; they run once over the whole batch after every
         // part is sorted
         for (uint32_t p = 0; p < K; p++) {
+          if (S > 1)
+            while (!settled[p].load(std::memory_order_acquire)) __builtin_ia32_pause();
           sorted_f[p].get();
           HIP_OK(hipStreamWaitEvent(s, psorted[p], 0));
         }
@@ -340,19 +417,11 @@ struct Engine {
         mtf_stage(ws, r, bwt, nb, hboff[nb], P.m, s, &hboff);
         HIP_OK(hipEventRecord(e1, s));
         code_tables(ws, r, P.m, nb, P.t, s, split_tables() ? sstream[0] : nullptr);
-        HIP_OK(hipEventRecord(e2, s));
-        HIP_OK(hipEventSynchronize(e2));
-        for (uint32_t p = 0; p < nparts; p++) copyrank_check(parts[p].a5);
-        (void)hipEventElapsedTime(&mtf_ms, e0, e1);
-        (void)hipEventElapsedTime(&tab_ms, e1, e2);
-        last_post = mtf_ms + tab_ms;
+        HIP_OK(hipEventRecord(e2, s));  // (timings and the A5 check once the batch is done, below)
       } catch (...) {
         err = std::current_exception();
       }
       for (auto& x : th) x.join();
-      (void)hipEventDestroy(e0);
-      (void)hipEventDestroy(e1);
-      (void)hipEventDestroy(e2);
       if (err) std::rethrow_exception(err);
       for (uint32_t p = 0; p < nparts; p++) {
         const Part& P = parts[p];
@@ -370,7 +439,19 @@ struct Engine {
     for (uint32_t p = 0; p < K; p++) cp.push_back(CodePart{&parts[p].r, &parts[p].m, &parts[p].t, origptr + parts[p].b0, parts[p].r.nblocks});
     *out_bytes = code_emit(ws, cp, level, trailer, c, d_out, out_cap, s);
     HIP_OK(hipEventRecord(ev[4], s));
-    HIP_OK(hipEventSynchronize(ev[4]));
+    // the batch's end: the MTF symbol counts (a statistic) come back through the spinning
+    // small read, which is also the wait for the batch (a sleeping event wait cost ~40 us)
+    std::vector<uint32_t> nm(nb);
+    if (nb > 0 && K == 1 && parts[0].r.nblocks == nb)
+      ws.read_small(nm.data(), parts[0].m.nmtf, 4ull * nb, s);
+    else
+      HIP_OK(hipEventSynchronize(ev[4]));
+    if (nb > 0) {
+      for (uint32_t p = 0; p < nparts; p++) copyrank_check(parts[p].a5);
+      (void)hipEventElapsedTime(&mtf_ms, tev[0], tev[1]);
+      (void)hipEventElapsedTime(&tab_ms, tev[1], tev[2]);
+      last_post = mtf_ms + tab_ms;
+    }
     st->combined_crc = c.combined_crc;
     st->carry_bits = c.carry_bits;
     st->carry_byte = c.carry_byte;
@@ -397,13 +478,7 @@ struct Engine {
       last.a5_roots += (uint32_t)parts[p].a5.need.size();
       last.a5_host += parts[p].a5.n_host;
     }
-    for (uint32_t p = 0; p < K; p++) {
-      const Part& P = parts[p];
-      if (!P.r.nblocks) continue;
-      std::vector<uint32_t> nm(P.r.nblocks);
-      HIP_OK(hipMemcpy(nm.data(), P.m.nmtf, 4 * P.r.nblocks, hipMemcpyDeviceToHost));
-      for (uint32_t x : nm) last.mtf_symbols += x;
-    }
+    for (uint32_t x : nm) last.mtf_symbols += x;
   }
 
   // bzg_compress_device's contract: inputs larger than kMaxBatch are cut into batches; the

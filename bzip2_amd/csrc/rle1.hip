@@ -752,6 +752,10 @@ __global__ void __launch_bounds__(64) k_segment_fill(const uint32_t* __restrict_
 // Block offsets from k_segment_fill's cuts (written at boff + 1): boff[0] = 0; a final batch
 // closes its last block at m, a non-final one leaves the block after the last cut open (it
 // restarts the next batch from its input start).
+__global__ void k_set_word(uint32_t* __restrict__ p, uint32_t v) {
+  if (threadIdx.x == 0) p[0] = v;
+}
+
 __global__ void k_segment_finish(const uint32_t* __restrict__ m_ptr, const uint32_t* __restrict__ res,
                                  int final_batch, uint32_t* __restrict__ boff, uint32_t* __restrict__ nblocks) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -1118,9 +1122,7 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   k_segment_finish<<<1, 64, 0, st>>>(mtot, mtot + 12, final_batch ? 1 : 0, boff, nbl);
   HIP_OK(hipGetLastError());
   uint32_t hv[2];
-  HIP_OK(hipMemcpyAsync(hv, mtot, 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(hv + 1, nbl, 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  ws.read_small({{hv, mtot, 4}, {hv + 1, nbl, 4}}, st);
   if (hv[1] == 0xffffffffu) throw HipFailure(hipErrorUnknown);
   res.m = hv[0];
   res.nblocks = hv[1];
@@ -1133,9 +1135,8 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
       HIP_OK(hipGetLastError());
     }
     if (final_batch) {
-      const uint32_t nn = (uint32_t)n;
-      HIP_OK(hipMemcpyAsync(binst + res.nblocks, &nn, 4, hipMemcpyHostToDevice, st));
-      HIP_OK(hipStreamSynchronize(st));
+      k_set_word<<<1, 64, 0, st>>>(binst + res.nblocks, (uint32_t)n);
+      HIP_OK(hipGetLastError());
     }
   }
   if (res.nblocks == 0) {  // non-final batch with no complete block: consume nothing
@@ -1145,8 +1146,7 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   // binst[nblocks] is n for a final batch, else the input start of the incomplete block
   // that opens the next batch (a chunk start, so RLE1 restarts there with fresh state).
   std::vector<uint32_t> hbi(res.nblocks + 1);
-  HIP_OK(hipMemcpyAsync(hbi.data(), binst, 4ull * (res.nblocks + 1), hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
+  ws.read_small(hbi.data(), binst, 4ull * (res.nblocks + 1), st);
   res.consumed = final_batch ? n : hbi[res.nblocks];
 
   const int B = (int)res.nblocks;

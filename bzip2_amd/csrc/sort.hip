@@ -2381,10 +2381,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* scratch =
       ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[kClsPacked])) + 64);
   uint32_t hc[64];
-  auto read_counters = [&]() {
-    HIP_OK(hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-  };
+  auto read_counters = [&]() { ws.read_small(hc, cnt, sizeof(hc), st); };
   auto grid = [](uint64_t n) { return (unsigned)std::max<uint64_t>(1, ceil_div64(n, kT)); };
   static const bool debug = getenv("BZG_DEBUG") != nullptr;
   static const bool check = getenv("BZG_CHECK") != nullptr;
@@ -2523,8 +2520,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         k_split_pairs<<<ceil_div(ncls[0], kT * kSplitPer), kT, 0, st>>>(C.l[0], ncls[0], tiny2, tiny8, cnt + 32);
         HIP_OK(hipGetLastError());
         uint32_t hn[2];
-        HIP_OK(hipMemcpyAsync(hn, cnt + 32, 8, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
+        ws.read_small(hn, cnt + 32, 8, st);
         if (hn[0]) {
           HIP_OK(hipMemsetAsync(O.tdeep, 0, sizeof(Grp) * hn[0], st));
           k_tiny<2><<<ceil_div(hn[0], 32 * (kT / 64)), kT, 0, st>>>(tiny2, hn[0], B, O);
@@ -2680,8 +2676,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       k_pair_end<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, E, h0, ordat, R, cnt + 22);
       {  // (R holds the long ones until k_pair_resolve refills it; waves past the count exit)
         uint32_t nlong = 0;
-        HIP_OK(hipMemcpyAsync(&nlong, cnt + 22, 4, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
+        ws.read_small(&nlong, cnt + 22, 4, st);
         if (nlong) k_pair_long<<<ceil_div(nlong, kT / 64), kT, 0, st>>>(R, cnt + 22, B, h0, ordat);
       }
       k_pair_resolve<<<grid(n_deep), kT, 0, st>>>(L0, n_deep, B, O, E, F, uof, tbase, ordat, R, cnt + 21);

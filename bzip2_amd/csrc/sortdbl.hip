@@ -519,8 +519,7 @@ void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0
     HIP_OK(hipGetLastError());
     scan_u32(ScanOp::Sum, true, sz, sz, nL0, tot0, scr, st);
     uint32_t t32 = 0;
-    HIP_OK(hipMemcpyAsync(&t32, tot0, 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    ws.read_small(&t32, tot0, 4, st);
     T = t32;
   }
   const size_t lcap = T / 2 + nL0 + 16;
@@ -544,10 +543,7 @@ void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0
   HIP_OK(hipMemcpyAsync(L, L0, sizeof(Grp) * nL0, hipMemcpyDeviceToDevice, st));
   // counters: 0 total(scan), 1 n_large, 2 n_small, 3 n_next(L'), 4 n_large2, 5 n_equal, 6 tiles
   uint32_t hc[8];
-  auto read_counters = [&]() {
-    HIP_OK(hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-  };
+  auto read_counters = [&]() { ws.read_small(hc, cnt, sizeof(hc), st); };
   auto grid = [](uint64_t n) { return (unsigned)std::max<uint64_t>(1, ceil_div64(n, kT)); };
   const size_t tile_lds = sizeof(TileLds);
   static_assert(4 * sizeof(TileLds) <= 160 * 1024, "four tile-sort workgroups must fit one CU's LDS");

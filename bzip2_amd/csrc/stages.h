@@ -6,6 +6,7 @@
 #pragma once
 #include <exception>
 #include <functional>
+#include <initializer_list>
 #include <map>
 #include <string>
 #include <thread>
@@ -40,6 +41,20 @@ class Workspace {
   // stream wait for the work queued so far on the old one, so a later free on the new stream
   // is ordered after every earlier use of the buffers.
   void set_stream(hipStream_t s);
+  // Copies `bytes` (4-byte aligned, small: the sort's list sizes between passes) from device
+  // memory to `dst` once the work queued on `st` so far is done.  A one-workgroup kernel
+  // writes them into pinned host memory and raises a flag there that this thread spins on: no
+  // copy-engine transfer and no sleeping wait, so the device idles a few microseconds per
+  // read instead of ~35 (profiles/r05_gaps_*).  Larger reads take hipMemcpyAsync + a stream
+  // synchronisation.
+  void read_small(void* dst, const void* dev_src, size_t bytes, hipStream_t st);
+  // the same for up to four pieces at once
+  struct SmallRead {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  void read_small(std::initializer_list<SmallRead> reads, hipStream_t st);
 
  private:
   struct Buf {
@@ -54,6 +69,9 @@ class Workspace {
   size_t total_ = 0;
   uint32_t* crc_ = nullptr;
   uint32_t* xp2_ = nullptr;
+  uint32_t* mbox_ = nullptr;  // pinned host words for read_small, the flag after them
+  uint32_t* mbox_dev_ = nullptr;
+  uint32_t mseq_ = 0;
 };
 
 // ---- stage A1/A2 ---------------------------------------------------------------------
