@@ -439,18 +439,58 @@ __global__ void __launch_bounds__(kT) k_final(uint32_t b0, const uint32_t* __res
 // Bit offset of every block and the running combined CRC (compress.c:826-828), continuing
 // from the previous part of the batch: chain[0] = start bit, chain[1] = combined CRC in; the
 // part's end replaces them (parts are chained in stream order on one stream).
-__global__ void k_offsets(const uint32_t* __restrict__ info, const uint32_t* __restrict__ bcrc, uint32_t nb,
-                          uint64_t* __restrict__ chain, uint64_t* __restrict__ boffbits) {
-  if (threadIdx.x != 0) return;
-  uint64_t pos = chain[0];
-  uint32_t comb = (uint32_t)chain[1];
-  for (uint32_t b = 0; b < nb; b++) {
+// Bit offsets of the blocks (an exclusive sum of their bit lengths from chain[0]) and the
+// combined CRC (compress.c:826-828: c = rotl(c, 1) ^ bcrc[b] per block, i.e. rotl(c0, nb) xor
+// the xor of rotl(bcrc[b], nb - 1 - b)), one workgroup: a serial walk of ~1100 blocks was
+// ~175 us of dependent loads on the critical path.
+constexpr uint32_t kOffT = 1024;
+__global__ void __launch_bounds__(kOffT) k_offsets(const uint32_t* __restrict__ info, const uint32_t* __restrict__ bcrc,
+                                                   uint32_t nb, uint64_t* __restrict__ chain,
+                                                   uint64_t* __restrict__ boffbits) {
+  __shared__ uint64_t wsum[kOffT / 64];
+  __shared__ uint32_t wx[kOffT / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint32_t per = ceil_div(nb, kOffT), b0 = min(nb, t * per), b1 = min(nb, b0 + per);
+  uint64_t mine = 0;
+  uint32_t x = 0;
+  for (uint32_t b = b0; b < b1; b++) {
+    mine += info[(size_t)b * 8 + 3];
+    const uint32_t r = (nb - 1 - b) & 31u, c = bcrc[b];
+    x ^= r ? (c << r) | (c >> (32 - r)) : c;
+  }
+  // exclusive sum over the threads (64-bit), xor over the workgroup
+  uint64_t incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(incl, o, 64);
+    if (lane >= (uint32_t)o) incl += y;
+  }
+  uint32_t xr = x;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) xr ^= (uint32_t)__shfl_xor((int)xr, o, 64);
+  if (lane == 63) wsum[w] = incl;
+  if (lane == 0) wx[w] = xr;
+  __syncthreads();
+  const uint64_t start = chain[0];
+  uint64_t pre = start;
+  for (uint32_t k = 0; k < w; k++) pre += wsum[k];
+  uint64_t pos = pre + incl - mine;
+  for (uint32_t b = b0; b < b1; b++) {
     boffbits[b] = pos;
     pos += info[(size_t)b * 8 + 3];
-    comb = ((comb << 1) | (comb >> 31)) ^ bcrc[b];
   }
-  chain[0] = pos;
-  chain[1] = comb;
+  __syncthreads();  // every thread has read chain[0]
+  if (t == kOffT - 1) {
+    uint64_t tot = start;
+    uint32_t xa = 0;
+    for (uint32_t k = 0; k < kOffT / 64; k++) {
+      tot += wsum[k];
+      xa ^= wx[k];
+    }
+    const uint32_t c0 = (uint32_t)chain[1], r = nb & 31u;
+    chain[0] = tot;
+    chain[1] = (r ? (c0 << r) | (c0 >> (32 - r)) : c0) ^ xa;
+  }
 }
 
 __global__ void k_chain_init(uint64_t* __restrict__ chain, uint64_t start_bit, uint32_t comb) {
@@ -789,7 +829,7 @@ uint64_t code_emit(Workspace& ws, const std::vector<CodePart>& parts, int level,
   HIP_OK(hipGetLastError());
   for (const CodePart& p : parts) {
     if (p.nb == 0) continue;
-    k_offsets<<<1, 64, 0, st>>>(p.t->info, p.r->bcrc, p.nb, chain, p.t->bbits);
+    k_offsets<<<1, kOffT, 0, st>>>(p.t->info, p.r->bcrc, p.nb, chain, p.t->bbits);
     HIP_OK(hipGetLastError());
   }
   uint64_t hch[2];
