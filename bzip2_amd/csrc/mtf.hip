@@ -77,11 +77,12 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
                                             uint32_t* __restrict__ siglen) {
   const ChunkRef r = chunk_ref(boff, cbase);
   if (!r.valid) return;
-  // the signature leaves sixteen bytes per store (a store per new symbol was most of the
+  // the signature leaves eight bytes per store (a store per new symbol was most of the
   // kernel's time on high-entropy input: ~250 scattered byte stores per chunk; four bytes per
-  // store still left ~63 per chunk)
-  uint4* out = reinterpret_cast<uint4*>(sig + (size_t)r.gidx * 256);
-  uint32_t cnt = 0, acc[4] = {0, 0, 0, 0};
+  // store left ~63; sixteen cost text more in selects than they saved: profiles/r05_ab_sig*)
+  uint2* out = reinterpret_cast<uint2*>(sig + (size_t)r.gidx * 256);
+  uint64_t acc = 0;
+  uint32_t cnt = 0;
   uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // seen bytes, in registers
   const uint32_t a_lo = r.lo & ~15u;
   uint32_t a = (r.hi - 1) & ~15u;  // word being processed (walking down to a_lo)
@@ -113,12 +114,10 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
           s1 |= qq == 1 ? bit : 0ull;
           s2 |= qq == 2 ? bit : 0ull;
           s3 |= qq == 3 ? bit : 0ull;
-          const uint32_t wi = (cnt >> 2) & 3u, sh = c << (8 * (cnt & 3u));
-#pragma unroll
-          for (uint32_t k = 0; k < 4; k++) acc[k] |= wi == k ? sh : 0u;
-          if ((++cnt & 15u) == 0) {
-            out[(cnt >> 4) - 1] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-            acc[0] = acc[1] = acc[2] = acc[3] = 0;
+          acc |= (uint64_t)c << (8 * (cnt & 7u));
+          if ((++cnt & 7u) == 0) {
+            out[(cnt >> 3) - 1] = make_uint2((uint32_t)acc, (uint32_t)(acc >> 32));
+            acc = 0;
           }
         }
       }
@@ -126,7 +125,7 @@ __global__ void __launch_bounds__(kT) k_sig(const uint8_t* __restrict__ L, const
     if (a <= a_lo) break;
     a -= 16;
   }
-  if (cnt & 15u) out[cnt >> 4] = make_uint4(acc[0], acc[1], acc[2], acc[3]);  // (bytes past cnt: unused)
+  if (cnt & 7u) out[cnt >> 3] = make_uint2((uint32_t)acc, (uint32_t)(acc >> 32));  // (bytes past cnt: unused)
   siglen[r.gidx] = cnt;
 }
 

@@ -29,6 +29,12 @@ def tables(kind, n, seed=1):
 
 
 def main():
+    rng = np.random.default_rng(7)
+    for a in (8, 32, 64, 128, 258):  # latency against the alphabet size (no rescale: near-equal counts)
+        t = [[int(x) for x in rng.poisson(580, a)] for _ in range(48)]
+        B.code_lengths(t)
+        B.code_lengths(t)
+        print(f"alpha {a}: 48 tables", flush=True)
     for kind in ("prng", "text"):
         for n in (48, 480, 4800):
             t = tables(kind, n)
