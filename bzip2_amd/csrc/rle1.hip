@@ -329,17 +329,40 @@ __device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t ti
   load16(x, n, base, v);
   const RunBits rb = run_bits(x, n, base, v);
   // per-byte chunk info only for threads holding a run of 4+ (the carry scan only when the
-  // tile has one): the others emit their bytes unchanged
-  ByteInfo bi[kPer];
-  if (__syncthreads_or(rb.longrun)) {
-    const uint32_t before = run_before(rb.last1 ? rb.last1 - 1u : 0u, carry[tile], sh, thr);
-    if (rb.longrun) byte_info_from(x, n, base, v, before, bi);
+  // tile has one): the others emit their bytes unchanged.  Those threads walk their bytes twice
+  // (count, then emit) rather than keeping per-byte info: an array of it held k_emit at 113
+  // VGPRs (4 waves per SIMD) for the ~1% of threads that need it.
+  uint32_t before = 0;
+  if (__syncthreads_or(rb.longrun)) before = run_before(rb.last1 ? rb.last1 - 1u : 0u, carry[tile], sh, thr);
+  uint8_t prev0 = 0, next_after = 0;
+  uint32_t r0 = 0;
+  if (rb.longrun) {
+    prev0 = (base > 0 && base - 1 < n) ? x[base - 1] : 0;
+    next_after = (base + kPer < n) ? x[base + kPer] : 0;
+    r0 = ((uint32_t)base - before) % 255u;  // chunk offset of the thread's first byte if it continues a run
   }
+  // f(k, r, last, e) for the thread's bytes below n: r = chunk offset (0..254), last = the chunk
+  // ends here, e = output bytes
+  auto walk = [&](auto f) {
+    uint8_t prev = prev0;
+    uint32_t r = r0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint64_t i = base + k;
+      if (i >= n) break;
+      if (i == 0 || v[k] != prev) r = 0;
+      else if (k > 0) r = r == 254u ? 0u : r + 1u;
+      prev = v[k];
+      const uint8_t nx = (k + 1 < kPer) ? v[k + 1] : next_after;
+      const bool last = (i + 1 >= n) || (nx != v[k]) || (r == 254u);
+      const uint32_t e = r <= 2u ? 1u : (r == 3u ? 1u + (last ? 1u : 0u) : (last ? 1u : 0u));
+      f(k, i, r, last, e);
+    }
+  };
   uint32_t s = rb.nvalid;
   if (rb.longrun) {
     s = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) s += bi[k].e;
+    walk([&](int, uint64_t, uint32_t, bool, uint32_t e) { s += e; });
   }
   uint32_t tot;
   uint32_t incl = block_incl_sum(s, sh, &tot);
@@ -361,27 +384,23 @@ __device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t ti
         if ((uint32_t)k < rb.nvalid) ob[lp + k] = v[k];
     }
   } else {
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-      const uint64_t i = base + k;
-      if (i >= n) break;
-      const ByteInfo b = bi[k];
-      if (i + 1 == n) *last_len1 = (b.r == 0) ? 1u : 0u;
-      if (b.r == 0) {
+    walk([&](int k, uint64_t i, uint32_t r, bool last, uint32_t e) {
+      if (i + 1 == n) *last_len1 = (r == 0) ? 1u : 0u;
+      if (r == 0) {
         const uint32_t w = pos >> 5;
         if (w == w0) bits0 |= 1u << (pos & 31);
         else bits1 |= 1u << (pos & 31);
       }
       const uint32_t lp = pos - t0 + lofs;
       if (out == nullptr) {  // chunk map only (seg_map_stage): no block bytes
-      } else if (b.r <= 3) {
+      } else if (r <= 3) {
         ob[lp] = v[k];
-        if (b.r == 3 && b.last) ob[lp + 1] = 0;
-      } else if (b.last) {
-        ob[lp] = (uint8_t)(b.r - 3);
+        if (r == 3 && last) ob[lp + 1] = 0;
+      } else if (last) {
+        ob[lp] = (uint8_t)(r - 3);
       }
-      pos += b.e;
-    }
+      pos += e;
+    });
   }
   if (bits0) atomicOr(&cb[w0 - (t0 >> 5)], bits0);
   if (bits1) atomicOr(&cb[w0 + 1 - (t0 >> 5)], bits1);
