@@ -70,6 +70,47 @@ __device__ __forceinline__ RunBits run_bits(const uint8_t* __restrict__ x, uint6
   return r;
 }
 
+// The same from the thread's bytes as little-endian words (w: zero past n), pw = the word of
+// the 4 bytes before the thread (base >= 4 and base <= n, else unused).
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[4], int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xffu; }
+__device__ __forceinline__ void load16w(const uint8_t* __restrict__ x, uint64_t n, uint64_t base, uint32_t (&w)[4],
+                                        uint32_t& pw) {
+  pw = (base >= 4 && base <= n) ? *reinterpret_cast<const uint32_t*>(x + base - 4) : 0u;
+  if (base + kPer <= n) {
+    const uint4 q = *reinterpret_cast<const uint4*>(x + base);
+    w[0] = q.x, w[1] = q.y, w[2] = q.z, w[3] = q.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint32_t a = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) a |= (base + 4 * j + b < n ? (uint32_t)x[base + 4 * j + b] : 0u) << (8 * b);
+      w[j] = a;
+    }
+  }
+}
+__device__ __forceinline__ RunBits run_bits_words(uint64_t n, uint64_t base, const uint32_t (&w)[4], uint32_t pw) {
+  uint32_t a3 = (pw >> 8) & 0xffu, a2 = (pw >> 16) & 0xffu, a1 = pw >> 24;  // x[i-3], x[i-2], x[i-1]
+  RunBits r{0u, 0u, base < n ? (uint32_t)min<uint64_t>(kPer, n - base) : 0u, false};
+  uint32_t lng = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const uint64_t i = base + k;
+    const uint32_t c = byte_of(w, k);
+    const bool ok = i < n;
+    if (ok && (i == 0 || c != a1)) {
+      r.starts |= 1u << k;
+      r.last1 = (uint32_t)i + 1u;
+    }
+    lng |= (ok && i >= 3 && c == a1 && c == a2 && c == a3) ? 1u : 0u;
+    a3 = a2;
+    a2 = a1;
+    a1 = c;
+  }
+  r.longrun = lng != 0;
+  return r;
+}
+
 // SWAR form of run_bits for a thread of a full interior tile (base >= 16, base + 16 < n):
 // w = its 16 bytes as little-endian words, pw = the word before them.  Byte k of the thread
 // starts a run iff it differs from the byte before; a run of 4 ends at it iff it equals the 3
@@ -319,15 +360,18 @@ __device__ __forceinline__ void byte_info(const uint8_t* __restrict__ x, uint64_
 #define BZG_EMIT_BOUNDS __launch_bounds__(kT)
 #endif
 // k_emit for one tile that needs the per-byte rules.  ow / cb: the tile's LDS staging (cb zeroed).
+// The thread's 16 bytes are loaded again here (an L2 hit): keeping the words k_emit loaded
+// for its fast path alive into this path held the kernel at 86 VGPRs (5 waves per SIMD) against
+// 76 (6): RLE1 2.96 -> 2.80 ms per GB (profiles/r05_ab_emit.txt).
 __device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t tile, const uint32_t* __restrict__ carry,
                           const uint32_t* __restrict__ out_base, uint8_t* __restrict__ out,
                           uint32_t* __restrict__ cbits, uint32_t* __restrict__ last_len1, uint32_t* sh, uint32_t* thr,
                           uint32_t* ow, uint32_t* cb) {
   uint8_t* ob = reinterpret_cast<uint8_t*>(ow);
   const uint64_t base = tile * kTile + (uint64_t)threadIdx.x * kPer;
-  uint8_t v[kPer];
-  load16(x, n, base, v);
-  const RunBits rb = run_bits(x, n, base, v);
+  uint32_t w[4], pw;
+  load16w(x, n, base, w, pw);
+  const RunBits rb = run_bits_words(n, base, w, pw);
   // per-byte chunk info only for threads holding a run of 4+ (the carry scan only when the
   // tile has one): the others emit their bytes unchanged.  Those threads walk their bytes twice
   // (count, then emit) rather than keeping per-byte info: an array of it held k_emit at 113
@@ -337,7 +381,7 @@ __device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t ti
   uint8_t prev0 = 0, next_after = 0;
   uint32_t r0 = 0;
   if (rb.longrun) {
-    prev0 = (base > 0 && base - 1 < n) ? x[base - 1] : 0;
+    prev0 = (uint8_t)(pw >> 24);  // (0 at base 0, whose first byte starts a run anyway)
     next_after = (base + kPer < n) ? x[base + kPer] : 0;
     r0 = ((uint32_t)base - before) % 255u;  // chunk offset of the thread's first byte if it continues a run
   }
@@ -350,11 +394,12 @@ __device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t ti
     for (int k = 0; k < kPer; k++) {
       const uint64_t i = base + k;
       if (i >= n) break;
-      if (i == 0 || v[k] != prev) r = 0;
+      const uint8_t c = (uint8_t)byte_of(w, k);
+      if (i == 0 || c != prev) r = 0;
       else if (k > 0) r = r == 254u ? 0u : r + 1u;
-      prev = v[k];
-      const uint8_t nx = (k + 1 < kPer) ? v[k + 1] : next_after;
-      const bool last = (i + 1 >= n) || (nx != v[k]) || (r == 254u);
+      prev = c;
+      const uint8_t nx = (k + 1 < kPer) ? (uint8_t)byte_of(w, k + 1) : next_after;
+      const bool last = (i + 1 >= n) || (nx != c) || (r == 254u);
       const uint32_t e = r <= 2u ? 1u : (r == 3u ? 1u + (last ? 1u : 0u) : (last ? 1u : 0u));
       f(k, i, r, last, e);
     }
@@ -378,10 +423,24 @@ __device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t ti
     bits1 = sh5 ? rb.starts >> (32u - sh5) : 0u;
     if (base < n && n - base <= kPer) *last_len1 = (rb.starts >> (n - 1 - base)) & 1u;
     if (out != nullptr) {
-      const uint32_t lp = pos - t0 + lofs;
+      const uint32_t lp = pos - t0 + lofs, a = lp & 3u;
+      if (rb.nvalid == (uint32_t)kPer && a == 0) {
+        uint32_t* o = ow + (lp >> 2);
 #pragma unroll
-      for (int k = 0; k < kPer; k++)
-        if ((uint32_t)k < rb.nvalid) ob[lp + k] = v[k];
+        for (int j = 0; j < 4; j++) o[j] = w[j];
+      } else if (rb.nvalid == (uint32_t)kPer) {
+        // three whole LDS words in the middle, the bytes of the two edge words (shared with the
+        // neighbouring threads) one by one
+        uint32_t* o = ow + (lp >> 2);
+        for (uint32_t k = 0; k < 4u - a; k++) ob[lp + k] = (uint8_t)byte_of(w, (int)k);
+#pragma unroll
+        for (int j = 1; j < 4; j++) o[j] = __builtin_amdgcn_alignbyte(w[j], w[j - 1], 4u - a);
+        for (uint32_t k = 16u - a; k < 16u; k++) ob[lp + k] = (uint8_t)(w[3] >> (8 * (k & 3u)));
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPer; k++)
+          if ((uint32_t)k < rb.nvalid) ob[lp + k] = (uint8_t)byte_of(w, k);
+      }
     }
   } else {
     walk([&](int k, uint64_t i, uint32_t r, bool last, uint32_t e) {
@@ -394,7 +453,7 @@ __device__ void emit_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t ti
       const uint32_t lp = pos - t0 + lofs;
       if (out == nullptr) {  // chunk map only (seg_map_stage): no block bytes
       } else if (r <= 3) {
-        ob[lp] = v[k];
+        ob[lp] = (uint8_t)byte_of(w, k);
         if (r == 3 && last) ob[lp + 1] = 0;
       } else if (last) {
         ob[lp] = (uint8_t)(r - 3);
