@@ -145,7 +145,9 @@ __device__ __forceinline__ RunBitsW run_bits_w(const uint32_t (&w)[4], uint32_t 
 // tile's first run start on, h = the bytes before it (they continue the run that starts at the
 // carried run start), ends = that run ends at the tile's byte h - 1.  k_rle_fix adds the h
 // bytes' output once the carries are known (closed form).  tinfo = S | h << 16 | ends << 31.
-constexpr uint32_t kRleG = 1;  // tiles per workgroup of the two RLE1 passes (4 with all loads in flight: +0.5 ms)
+// tiles per workgroup of the two RLE1 passes (2 / 4 with all loads in flight: RLE1 +0.36 /
+// +0.59 ms per GB, profiles/r05_ab_rle_g.txt)
+constexpr uint32_t kRleG = 1;
 
 __device__ __forceinline__ bool rle_interior(uint64_t tile, uint64_t n) {
   return tile > 0 && (tile + 1) * kTile < n;
@@ -165,12 +167,14 @@ __device__ __forceinline__ bool tile_in_run(const uint8_t* __restrict__ x, uint6
 __device__ __forceinline__ uint64_t run_emitted(uint64_t x);
 
 // k_rle_count for one tile that needs the per-byte rules (first, last or run-holding tiles).
+// Only threads holding a run of 4 walk their bytes; the others count theirs from the run-start
+// bits.  (The bytes are loaded again, as in emit_tile.)
 __device__ void rle_count_tile(const uint8_t* __restrict__ x, uint64_t n, uint64_t tile, uint32_t* __restrict__ tmax,
                                uint32_t* __restrict__ tinfo, uint32_t* sh, uint32_t* thr) {
   const uint64_t ts = tile * kTile, base = ts + (uint64_t)threadIdx.x * kPer;
-  uint8_t v[kPer];
-  load16(x, n, base, v);
-  const RunBits rb = run_bits(x, n, base, v);
+  uint32_t w[4], pw;
+  load16w(x, n, base, w, pw);
+  const RunBits rb = run_bits_words(n, base, w, pw);
   const uint32_t len = (uint32_t)min<uint64_t>(kTile, n - ts);
   const bool general = __syncthreads_or(rb.longrun);
   const uint32_t incl = block_incl_max(rb.last1, sh);
@@ -182,23 +186,33 @@ __device__ void rle_count_tile(const uint8_t* __restrict__ x, uint64_t n, uint64
   thr[threadIdx.x] = incl;
   __syncthreads();
   uint32_t m1 = threadIdx.x ? thr[threadIdx.x - 1] : 0u;  // 1 + run start of the byte (0: before the tile)
-  const uint8_t next_after = (base + kPer < n) ? x[base + kPer] : 0;
   uint32_t s = 0, h = 0;
+  if (!rb.longrun) {
+    // bytes before the tile's first run start continue the carried run (h); the rest emit once
+    const uint32_t k0 = m1 ? 0u : (rb.starts ? (uint32_t)__builtin_ctz(rb.starts) : (uint32_t)kPer);
+    h = min(k0, rb.nvalid);
+    s = rb.nvalid - h;
+  } else {
+    const uint8_t next_after = (base + kPer < n) ? x[base + kPer] : 0;
+    uint32_t r = m1 ? ((uint32_t)base - (m1 - 1u)) % 255u : 0u;  // chunk offset carried into byte 0
 #pragma unroll
-  for (int k = 0; k < kPer; k++) {
-    const uint64_t i = base + k;
-    if (i >= n) break;
-    if ((rb.starts >> k) & 1u) m1 = (uint32_t)i + 1u;
-    if (m1 == 0) {
-      h++;
-    } else if (!rb.longrun) {
-      s++;
-    } else {
-      uint32_t r = (uint32_t)i - (m1 - 1u);
-      if (r >= 255u) r %= 255u;
-      const uint8_t nx = (k + 1 < kPer) ? v[k + 1] : next_after;
-      const bool last = (i + 1 >= n) || (nx != v[k]) || (r == 254);
-      s += r <= 2 ? 1u : (r == 3 ? 1u + (last ? 1u : 0u) : (last ? 1u : 0u));
+    for (int k = 0; k < kPer; k++) {
+      const uint64_t i = base + k;
+      if (i >= n) break;
+      const uint8_t c = (uint8_t)byte_of(w, k);
+      if ((rb.starts >> k) & 1u) {
+        m1 = (uint32_t)i + 1u;
+        r = 0;
+      } else if (k > 0) {
+        r = r == 254u ? 0u : r + 1u;
+      }
+      if (m1 == 0) {
+        h++;
+      } else {
+        const uint8_t nx = (k + 1 < kPer) ? (uint8_t)byte_of(w, k + 1) : next_after;
+        const bool last = (i + 1 >= n) || (nx != c) || (r == 254u);
+        s += r <= 2u ? 1u : (r == 3u ? 1u + (last ? 1u : 0u) : (last ? 1u : 0u));
+      }
     }
   }
   uint32_t tot;
