@@ -116,13 +116,23 @@ __device__ __forceinline__ uint32_t text_key4(const uint8_t* t, uint32_t len, ui
 
 // Characters q .. q + 4N - 1 of the cyclic unit text as big-endian words, one at a time
 // (the wrap-around path; rare).
+// (a rolled loop with an incremental index: unrolled, its 4N modulo reductions and byte loads
+// set the register peak of the S2 sorts although it runs only for keys that wrap)
 template <int N>
 __device__ __forceinline__ void text_words_wrap(const uint8_t* t, uint32_t len, uint32_t q, uint32_t (&k)[N]) {
-  for (int w = 0; w < N; w++) {
-    uint32_t x = 0;
-    for (uint32_t i = 0; i < 4; i++) x = (x << 8) | t[(q + 4 * w + i) % len];
-    k[w] = x;
+  uint32_t acc[N];
+#pragma unroll
+  for (int w = 0; w < N; w++) acc[w] = 0;
+  uint32_t p = q;
+#pragma unroll 1
+  for (uint32_t j = 0; j < 4u * N; j++) {
+    const uint32_t c = t[p];
+    p = p + 1 == len ? 0u : p + 1;
+#pragma unroll
+    for (int w = 0; w < N; w++) acc[w] = (j >> 2) == (uint32_t)w ? (acc[w] << 8) | c : acc[w];
   }
+#pragma unroll
+  for (int w = 0; w < N; w++) k[w] = acc[w];
 }
 // The N + 1 aligned words covering characters p .. p + 4N - 1 (loads only; text_words_of
 // turns them into big-endian words).  Split so that a caller issues the loads of all its
@@ -1564,21 +1574,30 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
   if constexpr (kPre) {
     // one round trip for two rounds: 16 characters per rotation, the 8 after the first 7
     // kept in LDS for the second round's keys (almost every wave of these classes has one)
-    uint32_t raw[kPer][5], cq[kPer];
+    // (4 aligned words hold at least 13 characters from any start: the kC1 + kC2 the two rounds
+    // use; a fifth word per rotation held class 257..512 at 4 waves per SIMD)
+    uint32_t raw[kPer][4], cq[kPer];
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
       cq[r] = cyc_pos(vq[r], depth, U.len);
-      text_raw<4>(t + cq[r], raw[r]);
+      text_raw<3>(t + cq[r], raw[r]);
       cq[r] |= (uint32_t)t[vq[r] == 0 ? U.len - 1 : vq[r] - 1] << 24;
     }
+    static_assert(KeyFmt<kE>::kC1 + KeyFmt<kE>::kC2 <= 13, "four aligned words per rotation");
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
       const uint32_t p = sl * kPer + r, idx = lane * kPer + r;
       const bool valid = p < m;
       const uint32_t q = cq[r] & 0xffffffu;
       uint32_t k4[4];
-      text_words_of<4>(t + q, raw[r], k4);
-      if (valid && q + 16 > U.len) text_words_wrap<4>(t, U.len, q, k4);
+      {
+        uint32_t k3[3];
+        text_words_of<3>(t + q, raw[r], k3);
+        k4[0] = k3[0], k4[1] = k3[1], k4[2] = k3[2];
+        // characters 12 .. 15 - (start & 3) of the last word (the rest are not used)
+        k4[3] = __builtin_bswap32(__builtin_amdgcn_alignbyte(0u, raw[r][3], (uint32_t)((uintptr_t)(t + q) & 3u)));
+      }
+      if (valid && q + 13 > U.len) text_words_wrap<4>(t, U.len, q, k4);
       Lv[w][idx] = vq[r];
       Lc[w][idx] = (uint8_t)(cq[r] >> 24);
       constexpr uint32_t kSh = 8 * (KeyFmt<kE>::kC1 - 4);  // the 8 characters after the first kC1
