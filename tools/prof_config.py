@@ -1,5 +1,5 @@
 """One BASELINE config on the device for profiling (development tool):
-python tools/prof_config.py single|random|repeat [steps]
+python tools/prof_config.py single|random|repeat|text [steps] [decode]
 single: 4 GiB of byte 0x61 (config 4); random: 4 GiB of PRNG bytes (config 5); repeat: 1e9 B
 of the bench text with 25% long repeats.  Each step is one bzg_compress_device call at -9."""
 import os
@@ -25,11 +25,21 @@ def main():
         d = torch.randint(0, 256, (1 << 32,), dtype=torch.uint8, device="cuda", generator=g)
     else:
         d = torch.frombuffer(bytearray(datagen.text(1_000_000_000, bench.rank_seed(0))), dtype=torch.uint8).to("cuda")
-        bench.add_repeats(d, 0.25)
+        if kind == "repeat":
+            bench.add_repeats(d, 0.25)
     n = d.numel()
     cap = B.bound(n)
     out = torch.empty(cap, dtype=torch.uint8, device="cuda")
     ms, nb, st = bench.time_device(d, n, 9, out, cap, steps=steps)
+    if len(sys.argv) > 3 and sys.argv[3] == "decode":  # then decode the stream `steps` times
+        dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        sp = torch.cuda.current_stream().cuda_stream
+        for _ in range(steps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rc, got = B.decompress_device(out.data_ptr(), nb, dec.data_ptr(), n + 64, stream_ptr=sp)
+            torch.cuda.synchronize()
+            print("decode", rc, got, f"{1e3 * (time.perf_counter() - t0):.2f} ms", flush=True)
     print(kind, n, f"{ms:.3f} ms", f"{n / ms / 1e3:.1f} MB/s", {k: round(st[k + '_ms'], 3) for k in ("rle1", "bwt", "mtf", "code")},
           flush=True)
 
