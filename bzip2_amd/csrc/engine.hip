@@ -219,6 +219,7 @@ struct Engine {
   hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // batch(): MTF start, tables start, tables end
   hipEvent_t ev[6];
   hipEvent_t ev_rle;
+  hipEvent_t ev_crc_in = nullptr, ev_crc_out = nullptr;  // block CRCs on the idle sort stream
 
   explicit Engine(int dev) : device(dev) {
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -226,6 +227,8 @@ struct Engine {
     HIP_OK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     for (auto& e : ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipEventCreateWithFlags(&ev_rle, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_crc_in, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_crc_out, hipEventDisableTiming));
     ws.set_stream(stream);
   }
 
@@ -291,7 +294,10 @@ struct Engine {
     ws.set_stream(s);
     HIP_OK(hipEventRecord(ev[0], s));
     Rle1Result r;
-    rle1_stage(ws, d_in, n, level, end_seg, tail_merge, r, s);
+    // the block CRCs run on the last sort stream (idle at the default two sort streams; with
+    // three it only queues behind that stream's sorts) and overlap the sort
+    hipStream_t crc_st = sstream[kSortStreams - 1];  // (profiles/r05_ab_crc_side.txt)
+    rle1_stage(ws, d_in, n, level, end_seg, tail_merge, r, s, crc_st, ev_crc_in, ev_crc_out);
     HIP_OK(hipEventRecord(ev[1], s));
     const uint32_t nb = r.nblocks;
     uint32_t* origptr = ws.u32("origptr", nb + 2);
@@ -437,6 +443,7 @@ struct Engine {
     c.header_done = st->header_done;
     std::vector<CodePart> cp;
     for (uint32_t p = 0; p < K; p++) cp.push_back(CodePart{&parts[p].r, &parts[p].m, &parts[p].t, origptr + parts[p].b0, parts[p].r.nblocks});
+    if (crc_st && r.nblocks) HIP_OK(hipStreamWaitEvent(s, ev_crc_out, 0));  // bcrc: the packing's input
     *out_bytes = code_emit(ws, cp, level, trailer, c, d_out, out_cap, s);
     HIP_OK(hipEventRecord(ev[4], s));
     // the batch's end: the MTF symbol counts (a statistic) come back through the spinning

@@ -1173,7 +1173,8 @@ __global__ void __launch_bounds__(kT) k_qperiod(const uint8_t* __restrict__ blk,
 
 // ------------------------------------------------------------------------------------
 void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool final_batch,
-                bool tail_merge, Rle1Result& res, hipStream_t st) {
+                bool tail_merge, Rle1Result& res, hipStream_t st, hipStream_t crc_st, hipEvent_t crc_in,
+                hipEvent_t crc_out) {
   const uint32_t nblock_max = 100000u * (uint32_t)level - 19u;
   res.nblocks = 0;
   res.consumed = 0;
@@ -1249,10 +1250,20 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   for (int b = 0; b < B; b++) maxin = std::max(maxin, hbi[b + 1] - hbi[b]);
   const uint32_t split = (uint32_t)std::min<uint64_t>(kCrcSplitMax, std::max<uint64_t>(kCrcSplit, ceil_div64(maxin, 1u << 19)));
   uint32_t* cpart = ws.u32("crc_part", (size_t)(B + 2) * split);
-  k_block_crc<<<dim3(split, B), kT, 0, st>>>(d_in, binst, ws.crc_table(), ws.xpow2_table(), split, cpart, tinfo, n);
+  // the block CRCs are read only by the packing: on a side stream they overlap the sort
+  const uint32_t* ctab = ws.crc_table();
+  const uint32_t* xtab = ws.xpow2_table();
+  hipStream_t cs = st;
+  if (crc_st && crc_in && crc_out) {
+    HIP_OK(hipEventRecord(crc_in, st));
+    HIP_OK(hipStreamWaitEvent(crc_st, crc_in, 0));
+    cs = crc_st;
+  }
+  k_block_crc<<<dim3(split, B), kT, 0, cs>>>(d_in, binst, ctab, xtab, split, cpart, tinfo, n);
   HIP_OK(hipGetLastError());
-  k_crc_combine<<<B, 64, 0, st>>>(binst, cpart, ws.xpow2_table(), B, split, bcrc);
+  k_crc_combine<<<B, 64, 0, cs>>>(binst, cpart, xtab, B, split, bcrc);
   HIP_OK(hipGetLastError());
+  if (cs != st) HIP_OK(hipEventRecord(crc_out, cs));
   res.bcrc = bcrc;
   res.blk = blk;
   res.boff = boff;
