@@ -420,6 +420,7 @@ struct Engine {
         P.r = r;
         P.hboff = hboff;
         P.w = &ws;
+        HIP_OK(hipStreamWaitEvent(s, ev_crc_out, 0));  // in-use maps and block CRCs (side stream)
         mtf_stage(ws, r, bwt, nb, hboff[nb], P.m, s, &hboff);
         HIP_OK(hipEventRecord(e1, s));
         code_tables(ws, r, P.m, nb, P.t, s, split_tables() ? sstream[0] : nullptr);
@@ -443,7 +444,6 @@ struct Engine {
     c.header_done = st->header_done;
     std::vector<CodePart> cp;
     for (uint32_t p = 0; p < K; p++) cp.push_back(CodePart{&parts[p].r, &parts[p].m, &parts[p].t, origptr + parts[p].b0, parts[p].r.nblocks});
-    if (crc_st && r.nblocks) HIP_OK(hipStreamWaitEvent(s, ev_crc_out, 0));  // bcrc: the packing's input
     *out_bytes = code_emit(ws, cp, level, trailer, c, d_out, out_cap, s);
     HIP_OK(hipEventRecord(ev[4], s));
     // the batch's end: the MTF symbol counts (a statistic) come back through the spinning

@@ -1263,12 +1263,12 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   HIP_OK(hipGetLastError());
   k_crc_combine<<<B, 64, 0, cs>>>(binst, cpart, xtab, B, split, bcrc);
   HIP_OK(hipGetLastError());
-  if (cs != st) HIP_OK(hipEventRecord(crc_out, cs));
   res.bcrc = bcrc;
   res.blk = blk;
   res.boff = boff;
   res.binst = binst;
-  block_info_stage(ws, res, st);
+  block_info_stage(ws, res, st, cs);
+  if (cs != st) HIP_OK(hipEventRecord(crc_out, cs));
 }
 
 // ---- one region of a sharded stream ------------------------------------
@@ -1336,16 +1336,18 @@ void seg_walk_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, u
   last_fill = hres[2];
 }
 
-void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st) {
+void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st, hipStream_t side) {
   const uint32_t B = res.nblocks;
   if (B == 0) return;
   res.inuse = ws.u32("inuse", (size_t)(B + 2) * 8);
   res.ninuse = ws.u32("ninuse", B + 2);
   res.period = ws.u32("period", B + 2);
-  HIP_OK(hipMemsetAsync(res.inuse, 0, (size_t)B * 8 * 4, st));
-  k_in_use<<<dim3(kInUseSplit, B), kT, 0, st>>>(res.blk, res.boff, res.inuse);
+  // in-use maps: read by MTF and the tables, not the sort (side: rle1_stage's CRC stream)
+  hipStream_t iu = side ? side : st;
+  HIP_OK(hipMemsetAsync(res.inuse, 0, (size_t)B * 8 * 4, iu));
+  k_in_use<<<dim3(kInUseSplit, B), kT, 0, iu>>>(res.blk, res.boff, res.inuse);
   HIP_OK(hipGetLastError());
-  k_ninuse<<<ceil_div(B, kT), kT, 0, st>>>(res.inuse, B, res.ninuse);
+  k_ninuse<<<ceil_div(B, kT), kT, 0, iu>>>(res.inuse, B, res.ninuse);
   HIP_OK(hipGetLastError());
   k_period<<<B, kT, 0, st>>>(res.blk, res.boff, res.period);
   HIP_OK(hipGetLastError());

@@ -90,14 +90,15 @@ struct Rle1Result {
   uint32_t* bq = nullptr;       // B* offsets of each periodic block's root (origptr.hip)
   uint32_t* qper = nullptr;     // smallest period of a quasi-periodic block (qsa.h), else 0
 };
-// crc_st / crc_in / crc_out (optional): the block CRCs run on crc_st, which waits for crc_in
-// (recorded on st once their inputs are ready); crc_out is recorded after them, and bcrc may be
-// read only by work ordered after it (the sort and MTF do not read it).
+// crc_st / crc_in / crc_out (optional): the block CRCs and the in-use maps run on crc_st, which
+// waits for crc_in (recorded on st once their inputs are ready); crc_out is recorded after them,
+// and bcrc / inuse / ninuse may be read only by work ordered after it (the sort reads neither).
 void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool final_batch,
                 bool tail_merge, Rle1Result& res, hipStream_t st, hipStream_t crc_st = nullptr,
                 hipEvent_t crc_in = nullptr, hipEvent_t crc_out = nullptr);
 // in-use maps, nInUse and primitive periods of res.nblocks blocks given res.blk / res.boff
-void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st);
+// (side: the in-use maps go there; only MTF and the tables read them)
+void block_info_stage(Workspace& ws, Rle1Result& res, hipStream_t st, hipStream_t side = nullptr);
 // bit offsets of the block-header / end-of-stream magics of a .bz2 stream, sorted, as
 // 2 * offset + kind (magic.hip)
 uint64_t find_magics_stage(const uint8_t* d_in, uint64_t n, std::vector<uint64_t>& found, hipStream_t st);
