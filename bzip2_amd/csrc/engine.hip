@@ -1207,7 +1207,7 @@ static constexpr uint64_t kPipeFirst = 96ull << 20;
 
 static std::vector<uint64_t> pipe_pieces(uint64_t n) {
   std::vector<uint64_t> b{0};
-  uint64_t s = std::max<uint64_t>(kPipeFirst, n / 5);
+  uint64_t s = std::max<uint64_t>(kPipeFirst, n / 5);  // (n/4, n/8, 3 pieces: slower, profiles/r05_h2h_split.txt)
   while (n - b.back() > 4 * s) {
     b.push_back(b.back() + s);
     s *= 2;
