@@ -236,12 +236,25 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
     __syncthreads();
     const uint32_t g = g0 + threadIdx.x;
     if (g < nsel) {
-      const uint16_t* c = S.chunk + threadIdx.x * kGroupSize;
+      // the group's 50 symbols in 25 registers, read as pairs (a group starts 100 bytes after the
+      // last: 4-byte aligned, and 25 words apart keeps the lanes on distinct banks), once for
+      // both the cost and the counting loops
+      const uint32_t* cw = reinterpret_cast<const uint32_t*>(S.chunk + threadIdx.x * kGroupSize);
       const uint32_t n = min((uint32_t)kGroupSize, nmtf - g * kGroupSize);
+      uint32_t sym[kGroupSize / 2];
+#pragma unroll
+      for (int k = 0; k < (int)kGroupSize / 2; k++) sym[k] = cw[k];
+      auto sym_at = [&](int i) { return (sym[i >> 1] >> (16 * (i & 1))) & 0xffffu; };
       // 50 lengths <= 17: every 10-bit field sum stays below 1024
       uint64_t acc = 0;
-#pragma unroll 10
-      for (uint32_t i = 0; i < n; i++) acc += S.lenp[c[i]];
+      if (n == kGroupSize) {
+#pragma unroll
+        for (int i = 0; i < (int)kGroupSize; i++) acc += S.lenp[sym_at(i)];
+      } else {
+#pragma unroll
+        for (int i = 0; i < (int)kGroupSize; i++)
+          if ((uint32_t)i < n) acc += S.lenp[sym_at(i)];
+      }
       uint32_t cost[kNGroups];
 #pragma unroll
       for (int t = 0; t < kNGroups; t++) cost[t] = (uint32_t)(acc >> (10 * t)) & 1023u;
@@ -262,18 +275,20 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
         // counted in registers first, so few lanes of a wave hit the same LDS counter
         // (four byte counters in one word: a group has at most 50 symbols)
         uint32_t f4 = 0;
-#pragma unroll 10
-        for (uint32_t i = 0; i < n; i++) {
-          const uint32_t v = c[i];
-          if (v > 3) atomicAdd(&S.rfreq[bt][v * 2 + (threadIdx.x & 1u)], 1u);
-          else f4 += 1u << (8 * v);
+        uint32_t* rfb = &S.rfreq[bt][threadIdx.x & 1u];
+#pragma unroll
+        for (int i = 0; i < (int)kGroupSize; i++) {
+          const uint32_t v = sym_at(i);
+          if ((uint32_t)i < n) {
+            if (v > 3) atomicAdd(&rfb[v * 2], 1u);
+            else f4 += 1u << (8 * v);
+          }
         }
         const uint32_t f0 = f4 & 255u, f1 = (f4 >> 8) & 255u, f2 = (f4 >> 16) & 255u, f3 = f4 >> 24;
-        const uint32_t cp = threadIdx.x & 1u;
-        if (f0) atomicAdd(&S.rfreq[bt][0 + cp], f0);
-        if (f1) atomicAdd(&S.rfreq[bt][2 + cp], f1);
-        if (f2) atomicAdd(&S.rfreq[bt][4 + cp], f2);
-        if (f3) atomicAdd(&S.rfreq[bt][6 + cp], f3);
+        if (f0) atomicAdd(&rfb[0], f0);
+        if (f1) atomicAdd(&rfb[2], f1);
+        if (f2) atomicAdd(&rfb[4], f2);
+        if (f3) atomicAdd(&rfb[6], f3);
       }
     }
   }
