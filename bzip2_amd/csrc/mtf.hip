@@ -518,15 +518,18 @@ __global__ void __launch_bounds__(64) k_rle2_plan(const uint32_t* __restrict__ b
 // first occurrence at initial position p has rank m + p - #{used positions < p}.  The symbols
 // stream from the BWT column 16 at a time (every lane of the quad loads the same 16 bytes, one
 // group ahead); the ranks of 16 steps leave as one 16-byte store; the zero-run summary is kept
-// on the way.  Per-chunk LDS: last occurrence (u16) and initial position (u8) of every byte.
+// on the way.  Per-chunk LDS: one u16 per byte, its last step or (before its first occurrence)
+// 0x8000 | its initial position: 32 KB per workgroup, and at most 128 VGPRs (a few spills per
+// 16 steps), so 4 waves share a SIMD instead of 3 (config 5 MTF 63.0 -> 57.6 ms,
+// profiles/r05_ab_mtfq_pack.txt).
 constexpr uint32_t kQChunks = kT / 4;
-__global__ void __launch_bounds__(kT) k_mtf_q(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
+__global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4))) k_mtf_q(const uint8_t* __restrict__ L, const uint32_t* __restrict__ boff,
                                               const uint32_t* __restrict__ cbase, const uint32_t* __restrict__ init,
                                               const uint32_t* __restrict__ hi_list, const uint32_t* __restrict__ n_hi,
                                               uint8_t* __restrict__ ranks, uint32_t* __restrict__ lead,
                                               uint32_t* __restrict__ trail, uint32_t* __restrict__ inner) {
-  __shared__ uint32_t lastw[kQChunks][128];  // u16 per byte
-  __shared__ uint32_t p0w[kQChunks][64];     // u8 per byte
+  // u16 per byte: its last step, or (never seen in the chunk) 0x8000 | its initial position
+  __shared__ uint32_t lastw[kQChunks][128];
   const uint32_t nh = *n_hi;
   if (blockIdx.x * kQChunks >= nh) return;
   const uint32_t q = threadIdx.x & 3u, ci = threadIdx.x >> 2;
@@ -540,8 +543,8 @@ __global__ void __launch_bounds__(kT) k_mtf_q(const uint8_t* __restrict__ L, con
     g = cbase[b] + c;
   }
   uint16_t* last = reinterpret_cast<uint16_t*>(lastw[ci]);
-  uint8_t* p0 = reinterpret_cast<uint8_t*>(p0w[ci]);
   for (uint32_t k = q; k < 128; k += 4) lastw[ci][k] = 0xffffffffu;
+  __builtin_amdgcn_wave_barrier();
   // initial positions, smallest first: lane r writes its 64 positions high to low in round
   // 3 - r, so the lowest lane writes last (past nInUse the list is unspecified)
   {
@@ -555,7 +558,7 @@ __global__ void __launch_bounds__(kT) k_mtf_q(const uint8_t* __restrict__ L, con
     for (uint32_t r = 0; r < 4; r++) {
       if (q == 3 - r) {
 #pragma unroll
-        for (int k = 63; k >= 0; k--) p0[(w[k >> 2] >> (8 * (k & 3))) & 0xffu] = (uint8_t)(64 * q + k);
+        for (int k = 63; k >= 0; k--) last[(w[k >> 2] >> (8 * (k & 3))) & 0xffu] = (uint16_t)(0x8000u | (64 * q + k));
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -593,8 +596,8 @@ __global__ void __launch_bounds__(kT) k_mtf_q(const uint8_t* __restrict__ L, con
       const uint32_t j = j16 + u;
       const bool act = j < len;
       const uint32_t c = (cw[u >> 2] >> (8 * (u & 3))) & 0xffu;
-      const uint32_t t = last[c], p = p0[c];
-      const bool first = t == 0xffffu;
+      const uint32_t t = last[c], p = t & 0xffu;
+      const bool first = t >= 0x8000u;
       // this lane's part of #{markers <= t} and of #{used positions < p}
       const uint32_t tl = t >> 8, tw = (t >> 6) & 3u, tb = t & 63u;
       uint64_t mt = M[0];
