@@ -464,6 +464,36 @@ def decode_line(a, d_text, d_stream, nb, no_cpu):
     return line
 
 
+def small_call_lines(a, d_text, d_out, cap, no_cpu):
+    """BASELINE config 2 (enwik8: 1e8 B of the same text generator, -9, one MI355X, device
+    resident), bit-exact against the reference on the whole 100 MB; and the per-rank share of
+    BASELINE config 3 at N = 2, 4, 8 (one call on 500, 250, 125 MB of the config-3 input: the
+    compress phase of one rank under strong scaling), with the per-byte rate against 1 GB."""
+    res = {}
+    n2 = 100_000_000
+    ms, nb, st = time_device(d_text, n2, a.level, d_out, cap, steps=10, warmup=2)
+    line = line_for("enwik8", n2, a.level, ms, nb, st,
+                    f"BASELINE config 2: the first {n2} B of the enwik9-class synthetic text (tests/datagen.py "
+                    f"stands in for enwik8), -{a.level}, device resident")
+    line["parity"] = sample_parity(d_text, n2, a.level, no_cpu)
+    res["enwik8_100mb"] = line
+    shares = {}
+    t1g = None
+    for n in (1_000_000_000, 500_000_000, 250_000_000, 125_000_000):
+        if n > d_text.numel():
+            continue
+        ms, nb, st = time_device(d_text, n, a.level, d_out, cap, steps=5 if n >= 500_000_000 else 10, warmup=1)
+        if n == 1_000_000_000:
+            t1g = ms
+        shares[str(n)] = {"ms": round(ms, 3), "value": round(n / ms / 1e3, 2), "unit": "MB/s",
+                          "stages_ms": {k: round(st[k + "_ms"], 3) for k in ("rle1", "bwt", "mtf", "code")},
+                          **({"ms_per_gb_vs_1gb": round(ms * (1e9 / n) / t1g, 3)} if t1g else {})}
+    res["strong_shares"] = {"workload": "one bzg_compress_device call on the first n B of the config-3 input "
+                                        "(the compress phase of one rank of a strong-scaling run at N = 1e9 / n)",
+                            "shares": shares}
+    return res
+
+
 def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False, nb_text=0):
     """Secondary lines (never `value`): GPU decompression of the main stream, BASELINE configs 4
     and 5 at full size (4 GiB, device resident; bzg_compress_device cuts them into 1.5e9-byte
@@ -471,6 +501,8 @@ def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False, nb_text=0):
     res = {}
     if nb_text:
         res["decompress_text"] = decode_line(a, d_text, d_out_text, nb_text, no_cpu)
+    # (after the decode line: these calls overwrite the main stream in d_out_text)
+    res.update(small_call_lines(a, d_text, d_out_text, cap_text, no_cpu))
     n4 = 1 << 32
     level = 9
     d = torch.full((n4,), 0x61, dtype=torch.uint8, device="cuda")

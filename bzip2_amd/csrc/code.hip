@@ -7,6 +7,7 @@
 // per-table symbol frequencies gathered with LDS atomics; each table's heap Huffman runs on
 // one lane with the reference's exact tie order.  Packing computes every field's bit offset
 // with block-level scans and ORs 32-bit big-endian words into the (zeroed) output.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -142,7 +143,13 @@ __device__ __forceinline__ int n_groups(uint32_t nmtf) {  // compress.c:266-270
 //         k_huff: BZ2_hbMakeCodeLengths for every (block, table), one wave each };
 //   k_cf (final mode): payload bits of every group under the final tables;
 //   k_final: canonical codes, selector MTF, table and header bit counts.
-constexpr uint32_t kCfSlices = 2;  // workgroups per block in k_cf
+// Workgroups per block in k_cf and k_pack (gridDim.x): at least kCfSlices (kPackSlices) and
+// enough for about kSliceFill workgroups per launch, so that a call of few blocks (100 MB: 110
+// blocks, 55 per k_cf half) is not a chain of steps on a hundred workgroups.
+constexpr uint32_t kCfSlices = 2, kPackSlices = 1, kSliceMax = 8, kSliceFill = 768;
+inline uint32_t slices_for(uint32_t nb, uint32_t lo) {
+  return std::max(lo, std::min(kSliceMax, ceil_div(kSliceFill, std::max(nb, 1u))));
+}
 
 __global__ void k_init_tables(uint32_t b0, const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ freq_g,
                               const uint32_t* __restrict__ ninuse, uint8_t* __restrict__ lens_g,
@@ -196,7 +203,7 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
   const uint32_t nmtf = nmtf_g[b];
   const uint32_t nsel = ceil_div(nmtf, kGroupSize);
   const uint32_t nch = ceil_div(nsel, kT);
-  const uint32_t cps = ceil_div(nch, kCfSlices);
+  const uint32_t cps = ceil_div(nch, gridDim.x);
   const uint32_t c0 = blockIdx.x * cps, c1 = min(nch, c0 + cps);
   if (c0 >= c1) return;
   const int ng = n_groups(nmtf);
@@ -368,29 +375,65 @@ __global__ void __launch_bounds__(kT) k_final(uint32_t b0, const uint32_t* __res
     len[i / kMaxAlpha][i % kMaxAlpha] = lens_g[(size_t)b * kNGroups * kMaxAlpha + i];
   for (uint32_t g = threadIdx.x; g < nsel; g += kT) sel[g] = sel_g[(size_t)b * kMaxSelectors + g];
   __syncthreads();
-  // canonical codes: lane t of wave t
-  if ((threadIdx.x & 63) == 0 && (int)(threadIdx.x >> 6) < ng) {
-    for (int t = threadIdx.x >> 6; t < ng; t += kT / 64) {
+  // canonical codes (BZ2_hbAssignCodes, huffman.c:152-166), table t on wave t % 4 with all its
+  // lanes: the code of symbol v is base[len v] + the number of symbols before v with the same
+  // length, where base[min] = 0 and base[l + 1] = (base[l] + count[l]) << 1.  Symbols are taken
+  // 64 at a time in index order; equal lengths inside a group of 64 are ranked by ballots, the
+  // earlier groups through LDS counts.  (A serial lane-0 loop over 17 x 258 entries was about
+  // 180 us of the tail of every call.)
+  {
+    __shared__ uint32_t lcnt[kT / 64][kMaxCodeLen + 2];
+    __shared__ uint32_t lbase[kT / 64][kMaxCodeLen + 2];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    for (int t = (int)w; t < ng; t += kT / 64) {
+      if (lane < kMaxCodeLen + 2) lcnt[w][lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      uint32_t rk[5], bits = 0;
       int mn = 32, mx = 0;
-      for (int v = 0; v < alpha; v++) {
-        mn = min(mn, (int)len[t][v]);
-        mx = max(mx, (int)len[t][v]);
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        const int v = 64 * k + (int)lane;
+        const bool in = v < alpha;
+        const uint32_t l = in ? len[t][v] : 0u;
+        uint64_t m = __ballot(in);
+#pragma unroll
+        for (int bit = 0; bit < 5; bit++) {
+          const uint64_t bal = __ballot((l >> bit) & 1u);
+          m &= ((l >> bit) & 1u) ? bal : ~bal;
+        }
+        rk[k] = in ? lcnt[w][l] + (uint32_t)__popcll(m & lanemask_lt()) : 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (in && (m & lanemask_lt()) == 0) lcnt[w][l] += (uint32_t)__popcll(m);  // the first lane of each length
+        __builtin_amdgcn_wave_barrier();
+        if (in) {
+          mn = min(mn, (int)l);
+          mx = max(mx, (int)l);
+          const int p = v == 0 ? (int)l : (int)len[t][v - 1];
+          bits += 1 + 2 * (uint32_t)((int)l > p ? (int)l - p : p - (int)l);
+        }
       }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, __shfl_xor(mn, o, 64));
+        mx = max(mx, __shfl_xor(mx, o, 64));
+      }
+      bits = wave_sum(bits);
+      if (lane == 0) {
+        uint32_t c = 0;
+        for (int l = mn; l <= mx; l++) {
+          lbase[w][l] = c;
+          c = (c + lcnt[w][l]) << 1;
+        }
+        misc[8 + t] = bits + 5;
+      }
+      __builtin_amdgcn_wave_barrier();
       uint32_t* co = codes_g + ((size_t)b * kNGroups + t) * kMaxAlpha;
-      uint32_t c = 0;
-      for (int l = mn; l <= mx; l++) {
-        for (int v = 0; v < alpha; v++)
-          if (len[t][v] == l) co[v] = c++;
-        c <<= 1;
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        const int v = 64 * k + (int)lane;
+        if (v < alpha) co[v] = lbase[w][len[t][v]] + rk[k];
       }
-      int cur = len[t][0];
-      uint32_t bits = 5;
-      for (int v = 0; v < alpha; v++) {
-        const int l = len[t][v];
-        bits += 1 + 2 * (uint32_t)(l > cur ? l - cur : cur - l);
-        cur = l;
-      }
-      misc[8 + t] = bits;
+      __builtin_amdgcn_wave_barrier();
     }
   }
   // selector MTF in parallel: the MTF index of selector s at g is the number of tables used
@@ -545,7 +588,6 @@ struct BitWriter {
 // nbits up to 32 may overflow the accumulator when nacc > 32 after a put; put() keeps
 // nacc < 32 on exit, so a put of <= 32 bits never loses bits.
 
-constexpr uint32_t kPackSlices = 1;  // workgroups per block in k_pack
 
 // The step's bit buffer holds either the whole step (default) or a window of it: a smaller
 // buffer lets more workgroups share a CU, and a step with more bits (high-entropy input) is
@@ -572,7 +614,7 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
   __shared__ uint32_t code[kNGroups][kMaxAlpha];  // code | length << 24 (one LDS read per symbol)
   __shared__ uint32_t sh[8];
   __shared__ PackLds P;
-  // kPackSlices workgroups per block: slice 0 also writes the block header, tables and
+  // gridDim.x workgroups per block: slice 0 also writes the block header, tables and
   // selectors; slice s packs its share of the payload steps from the bit offset of its first
   // group (p_dat + the bits of the groups before it)
   const uint32_t b = blockIdx.y, slice = blockIdx.x;
@@ -676,7 +718,7 @@ __global__ void __launch_bounds__(kT) k_pack(const uint16_t* __restrict__ mtfv, 
   {
     const uint8_t* selo = sel_g + (size_t)b * kMaxSelectors;
     const uint16_t* gb = gbits_g + (size_t)b * kMaxSelectors;
-    const uint32_t nsteps = ceil_div(nsel, kT), sps = ceil_div(nsteps, kPackSlices);
+    const uint32_t nsteps = ceil_div(nsel, kT), sps = ceil_div(nsteps, gridDim.x);
     const uint32_t s0 = min(nsteps, slice * sps), s1 = min(nsteps, s0 + sps);
     uint64_t pos = p_dat;  // bit position of the step
     {
@@ -824,12 +866,12 @@ void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_
     k_init_tables<<<n, 64, 0, s>>>(b0, m.nmtf, m.freq, r.ninuse, t.lens, rf);
     HIP_OK(hipGetLastError());
     for (int it = 0; it < kIters; it++) {
-      k_cf<<<dim3(kCfSlices, n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 0);
+      k_cf<<<dim3(slices_for(n, kCfSlices), n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 0);
       HIP_OK(hipGetLastError());
       k_huff<<<n * kNGroups, 64, 0, s>>>(b0, m.nmtf, r.ninuse, rf, t.lens);
       HIP_OK(hipGetLastError());
     }
-    k_cf<<<dim3(kCfSlices, n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 1);
+    k_cf<<<dim3(slices_for(n, kCfSlices), n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 1);
     HIP_OK(hipGetLastError());
     k_final<<<n, kT, 0, s>>>(b0, m.nmtf, r.ninuse, r.inuse, t.lens, t.codes, t.sel, t.selmtf, t.info);
     HIP_OK(hipGetLastError());
@@ -866,7 +908,7 @@ uint64_t code_emit(Workspace& ws, const std::vector<CodePart>& parts, int level,
   for (const CodePart& p : parts) {
     if (p.nb == 0) continue;
     const CodeTables& t = *p.t;
-    k_pack<<<dim3(kPackSlices, p.nb), kT, 0, st>>>(p.m->mtfv, p.m->mtf_off, p.m->nmtf, p.r->inuse, p.r->bcrc, p.origptr,
+    k_pack<<<dim3(slices_for(p.nb, kPackSlices), p.nb), kT, 0, st>>>(p.m->mtfv, p.m->mtf_off, p.m->nmtf, p.r->inuse, p.r->bcrc, p.origptr,
                                                  t.lens, t.codes, t.sel, t.selmtf, t.gbits, t.info, t.bbits,
                                                  (uint32_t*)out);
     HIP_OK(hipGetLastError());

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define BZG_WAVE 64
 
@@ -47,6 +48,12 @@ constexpr int kNGroups = 6;
 constexpr int kGroupSize = 50;
 constexpr int kIters = 4;
 constexpr int kMaxSelectors = 2 + 900000 / kGroupSize;  // 18002
+
+// A tuning knob from the environment (host side; read once by the caller's static).
+inline long long env_ll(const char* name, long long dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoll(e) : dflt;
+}
 
 __host__ __device__ inline uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 __host__ __device__ inline uint64_t ceil_div64(uint64_t a, uint64_t b) { return (a + b - 1) / b; }

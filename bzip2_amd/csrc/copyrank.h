@@ -10,6 +10,10 @@ namespace bzg {
 
 struct CopyRankFailure {};
 
+// Largest number of B* offsets per root the device closed form (origptr.hip k_copyrank_cf)
+// evaluates; copy_rank_distinct applies the same cap so that it reports what the device does.
+constexpr int32_t kCopyRankQMax = 1024;
+
 // B* structure of the cyclic root w (|w| = p >= 2, primitive): number of B* offsets q.
 int32_t root_bstar_count(const uint8_t* w, int32_t p);
 

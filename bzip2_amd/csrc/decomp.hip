@@ -72,6 +72,9 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t l) {
+  return ((uint64_t)rdlane((uint32_t)(v >> 32), l) << 32) | rdlane((uint32_t)v, l);
+}
 
 // Big-endian 32-bit word w of the stream (bytes past the end read as zero).
 __device__ __forceinline__ uint32_t stream_word(const uint8_t* __restrict__ in, uint64_t nbytes, uint64_t w) {
@@ -277,77 +280,128 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
     __syncthreads();
   }
   // ---- symbols (decompress.c:444-664, the Huffman half; MTF and runs are phase 2)
+  // Group-parallel decoding.  The 50 symbols of a selector group share one table, so a window
+  // of kWin bit positions from the group's first symbol is decoded at EVERY position at once
+  // (64 lanes x 4: the length and symbol of the code that would start there), and the chain of
+  // real symbol starts 0 -> next(0) -> next(next(0)) ... is read off by pointer jumping (5
+  // rounds to build next^2 .. next^32, then 6 rounds in which lane i composes its i steps),
+  // instead of 50 dependent table lookups on one lane (that serial loop was 114 ms of a 166 ms
+  // decode of 1 GB of text: one wave per block, ~700 cycles per lookup).  A group whose codes
+  // run past the window continues in the next window.  Every symbol (EOB and run digits
+  // included) takes the next slot of its group; a symbol past the last selector's group is a
+  // data error (decompress.c GET_MTF_VAL), a code running past the stream end an unexpected EOF.
   {
+    constexpr uint32_t kWin = 256, kPerLane = kWin / 64, kRing = 256;
+    __shared__ uint32_t ring[kRing];         // stream words [rfill - kRing, rfill) at [w % kRing]
+    __shared__ uint16_t J[6][kWin + 1];      // J[b][q]: the start 2^b codes after q (kWin: outside)
+    __shared__ uint16_t nxa[kWin];           // q + length of the code at q (unclamped)
+    __shared__ uint16_t sq[kWin];            // symbol of the code at q
     const uint32_t eob = ninuse + 1;
     const uint8_t* ssrc = selbuf + (size_t)c * kSelCap;
     uint16_t* sdst = symbuf + (size_t)c * symstride;
-    uint32_t sreg = 0, gi = 0, gleft = 0, lbase = 0, symv = 0;
-    uint64_t wword = p >> 5;  // stream word held by lane 0 of cur
-    // raw (byte-swapped at use) so that the prefetch of nxt is not waited for until needed
-    uint32_t cur = stream_word_raw(in, nbytes, wword + lane);
-    uint32_t nxt = stream_word_raw(in, nbytes, wword + 64 + lane);
-    uint64_t bb = (uint64_t)bswap32(rdlane(cur, 0)) << (32 + (p & 31));  // MSB-aligned bit buffer
-    uint32_t nb = 32 - (uint32_t)(p & 31), wi = 1;
-    t_sym = clock64();
-    // every symbol (EOB and run digits included) takes the next slot of its 50-symbol group;
-    // a symbol past the last selector's group is a data error (decompress.c GET_MTF_VAL)
-    const uint64_t p0 = p;
-    const uint32_t left0 = (uint32_t)min<uint64_t>(nbits - p, 0x7fffffffull);
-    uint32_t left = left0;  // bits of the stream after the current position
-    auto emit = [&](uint32_t sym) {
-      symv = lane == (ns & 63) ? sym : symv;
-      ns++;
-      if ((ns & 63) == 0) sdst[ns - 64 + lane] = (uint16_t)symv;
-    };
-    for (;;) {
-      if (gleft == 0) {
-        if (gi == nsel) { status = BZ_DATA_ERROR; break; }
-        if ((gi & 63) == 0) sreg = gi + lane < nsel ? ssrc[gi + lane] : 0u;
-        lbase = uni(rdlane(sreg, gi & 63) << kLutBits);
-        gi++;
-        gleft = kGroupSize;
-      }
-      if (nb < 32) {
-        bb |= (uint64_t)bswap32(rdlane(cur, wi)) << (32 - nb);
-        nb += 32;
-        if (++wi == 64) {
-          cur = nxt;
-          wword += 64;
-          nxt = stream_word_raw(in, nbytes, wword + 64 + lane);
-          wi = 0;
-        }
-      }
-      const uint32_t e = uni(lut[lbase + (uint32_t)(bb >> (64 - kLutBits))]);
-      uint32_t len, s0, s1 = 0;
-      bool two = false;
-      if ((e & 0x60u) == 0) {  // a code longer than the window: canonical limits per length
-                               // (the prefix passes limit[l] below the code's length only)
-        const uint32_t t = lbase >> kLutBits;
-        len = kLutBits + 1;
+    // the serial decoder's cap (more symbols than a block can hold): stop at the first multiple
+    // of 64 above nbmax
+    const uint32_t cap = 64u * (nbmax / 64u + 1u);
+    uint64_t rfill = p >> 5;
 #pragma unroll
-        for (int l = kLutBits + 1; l < kMaxDecLen; l++) len += (int32_t)(bb >> (64 - l)) > (int32_t)uni(limit[t][l]) ? 1u : 0u;
-        s0 = uni(perm[t][cbase[t][len] + (int32_t)(bb >> (64 - len))]);
-      } else {
-        s0 = (e >> 7) & 511u;
-        s1 = (e >> 16) & 511u;
-        two = (e & 0x60u) == 0x40u && gleft >= 2 && (e & 31u) <= left;  // both in this group
-        len = two ? (e & 31u) : (e >> 25);
+    for (uint32_t k = 0; k < kRing / 64; k++) ring[(rfill + 64 * k + lane) % kRing] = bswap32(stream_word_raw(in, nbytes, rfill + 64 * k + lane));
+    rfill += kRing;
+    uint32_t pre0 = stream_word_raw(in, nbytes, rfill + lane), pre1 = stream_word_raw(in, nbytes, rfill + 64 + lane);
+    if (lane < 6) J[lane][kWin] = (uint16_t)kWin;
+    t_sym = clock64();
+    uint64_t a = p;  // absolute bit of the next code
+    uint32_t gi = 0, sreg = 0;
+    bool stop = false;
+    while (!stop) {
+      if (gi == nsel) { status = BZ_DATA_ERROR; break; }
+      if ((gi & 63) == 0) sreg = gi + lane < nsel ? ssrc[gi + lane] : 0u;  // 64 selectors at a time
+      const uint32_t tb = uni(rdlane(sreg, gi & 63)) << kLutBits;
+      const uint32_t t = tb >> kLutBits;
+      gi++;
+      uint32_t need = kGroupSize;
+      while (need > 0) {
+        // the window's words (kWin + 32 bits) in the ring: the next 128 come from registers
+        while (((a + kWin + 32) >> 5) >= rfill) {
+          ring[(rfill + lane) % kRing] = bswap32(pre0);
+          ring[(rfill + 64 + lane) % kRing] = bswap32(pre1);
+          rfill += 128;
+          pre0 = stream_word_raw(in, nbytes, rfill + lane);
+          pre1 = stream_word_raw(in, nbytes, rfill + 64 + lane);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the code at every position of the window
+        uint32_t jq[kPerLane];
+#pragma unroll
+        for (uint32_t k = 0; k < kPerLane; k++) {
+          const uint32_t q = lane + 64 * k;
+          const uint64_t x = a + q;
+          const uint32_t w = (uint32_t)(x >> 5), sh = (uint32_t)(x & 31);
+          const uint32_t hi = ring[w % kRing], lo = ring[(w + 1) % kRing];
+          const uint32_t v = sh ? (hi << sh) | (lo >> (32 - sh)) : hi;
+          const uint32_t e = lut[tb + (v >> (32 - kLutBits))];
+          uint32_t len, s0;
+          if ((e & 0x60u) == 0) {  // longer than the table: canonical limits per length
+            len = kLutBits + 1;
+            for (int l = kLutBits + 1; l < kMaxDecLen; l++) len += (int32_t)(v >> (32 - l)) > limit[t][l] ? 1u : 0u;
+            s0 = perm[t][cbase[t][len] + (int32_t)(v >> (32 - len))];
+          } else {
+            len = e >> 25;
+            s0 = (e >> 7) & 511u;
+          }
+          nxa[q] = (uint16_t)(q + len);
+          sq[q] = (uint16_t)s0;
+          jq[k] = min(q + len, kWin);
+          J[0][q] = (uint16_t)jq[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        // next^(2^b) for b = 1..5
+#pragma unroll
+        for (uint32_t b = 1; b < 6; b++) {
+#pragma unroll
+          for (uint32_t k = 0; k < kPerLane; k++) jq[k] = J[b - 1][jq[k]];
+#pragma unroll
+          for (uint32_t k = 0; k < kPerLane; k++) J[b][lane + 64 * k] = (uint16_t)jq[k];
+          __builtin_amdgcn_wave_barrier();
+        }
+        // lane i: the start of the i-th code of the window
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 6; b++)
+          if ((lane >> b) & 1u) s = J[b][s];
+        const bool in_win = lane < need && s < kWin;
+        const uint32_t m = (uint32_t)__popcll(__ballot(in_win));  // codes of the group in this window
+        const uint32_t sym = in_win ? sq[s] : 0u;
+        const uint64_t endb = in_win ? a + nxa[s] : 0ull;
+        const uint64_t eofm = __ballot(in_win && endb > nbits), eobm = __ballot(in_win && sym == eob);
+        const uint32_t ieof = eofm ? (uint32_t)__builtin_ctzll(eofm) : 64u;
+        const uint32_t ieob = eobm ? (uint32_t)__builtin_ctzll(eobm) : 64u;
+        uint32_t cnt = min(m, min(ieof, ieob));  // codes emitted (an EOF code or EOB is not)
+        const bool capped = ns + cnt >= cap;
+        if (capped) cnt = cap - ns;
+        if (lane < cnt) sdst[ns + lane] = (uint16_t)sym;
+        ns += cnt;
+        if (capped) {
+          status = kStatusCap;
+          a = rdlane64(endb, cnt - 1);
+          stop = true;
+          break;
+        }
+        if (ieof < m && ieof <= ieob) {  // the stream ends inside this code
+          status = BZ_UNEXPECTED_EOF;
+          a = ieof ? rdlane64(endb, ieof - 1) : a;
+          stop = true;
+          break;
+        }
+        if (ieob < m) {  // end of block
+          a = rdlane64(endb, ieob);
+          stop = true;
+          break;
+        }
+        a = rdlane64(endb, m - 1);
+        need -= m;
       }
-      if (len > left) { status = BZ_UNEXPECTED_EOF; break; }
-      left -= len;
-      bb <<= len;
-      nb -= len;
-      gleft = uni(gleft - (two ? 2u : 1u));
-      if (s0 == eob) break;
-      emit(s0);
-      if (two) {
-        if (s1 == eob) break;
-        emit(s1);
-      }
-      if ((ns & ~63u) > nbmax) { status = kStatusCap; break; }
     }
-    p = p0 + (left0 - left);
-    if (lane < (ns & 63)) sdst[(ns & ~63u) + lane] = (uint16_t)symv;
+    p = a;
   }
 done:
   if (lane < 64) reinterpret_cast<uint32_t*>(seqbuf + (size_t)c * 256)[lane] = reinterpret_cast<const uint32_t*>(seq)[lane];

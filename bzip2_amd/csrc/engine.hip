@@ -84,8 +84,16 @@ void Workspace::read_small(std::initializer_list<SmallRead> reads, hipStream_t s
   k_mbox<<<1, 256, 0, st>>>(P, mbox_dev_, mbox_dev_ + kMboxWords, seq);
   HIP_OK(hipGetLastError());
   uint32_t* flag = mbox_ + kMboxWords;
+  // spin while the answer is expected within microseconds (the sort's list sizes); a wait
+  // longer than the spin budget (a whole batch still queued) blocks in the runtime instead of
+  // keeping a core busy beside the other host threads
+  constexpr uint64_t kSpinBudget = 1u << 15;  // about 1 ms
   for (uint64_t spins = 1;; spins++) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
+    if (spins == kSpinBudget) {
+      HIP_OK(hipStreamSynchronize(st));  // k_mbox is the stream's last operation
+      if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
+    }
     if ((spins & 1023) == 0) {  // a fault or an error on the stream ends the wait
       const hipError_t e = hipStreamQuery(st);
       if (e == hipSuccess) {
@@ -297,6 +305,14 @@ struct Engine {
     // the block CRCs run on the last sort stream (idle at the default two sort streams; with
     // three it only queues behind that stream's sorts) and overlap the sort
     hipStream_t crc_st = sstream[kSortStreams - 1];  // (profiles/r05_ab_crc_side.txt)
+    // on an error path the CRC / in-use kernels may still be in flight on crc_st when the next
+    // call frees or regrows the workspace on s: wait for them before the exception leaves
+    struct SideJoin {
+      hipStream_t side;
+      ~SideJoin() {
+        if (std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(side);
+      }
+    } side_join{crc_st};
     rle1_stage(ws, d_in, n, level, end_seg, tail_merge, r, s, crc_st, ev_crc_in, ev_crc_out);
     HIP_OK(hipEventRecord(ev[1], s));
     const uint32_t nb = r.nblocks;

@@ -61,7 +61,7 @@ __device__ __forceinline__ uint32_t single_copy_rank(uint32_t p, uint32_t k) {
 // copyrank_cf.cpp: classes of pairwise different keys, the first alone in its bucket.  One
 // workgroup per listed root (q >= 2 B* offsets); out[b] = r, or -1 when the rule does not apply
 // (the host model decides).
-constexpr uint32_t kCT = 1024, kQMax = 1024;
+constexpr uint32_t kCT = 1024, kQMax = (uint32_t)kCopyRankQMax;
 __device__ __forceinline__ int lg32d(uint32_t v) { return v == 0 ? -1 : 31 - (int)__builtin_clz(v); }
 __global__ void __launch_bounds__(kCT) k_copyrank_cf(const uint8_t* __restrict__ blk, const uint32_t* __restrict__ boff,
                                                      const uint32_t* __restrict__ period, const uint32_t* __restrict__ bq,

@@ -1084,10 +1084,30 @@ __global__ void __launch_bounds__(kT) k_period(const uint8_t* __restrict__ blk, 
     sorted[r] = v;
   }
   __syncthreads();
+  // every divisor is first tested on the block's first 64 positions, all at once (one thread
+  // per divisor); only the survivors get the whole-block check, in ascending order.  An
+  // aperiodic block (all text) has none but n, so its dozens of divisors no longer cost a
+  // chain of whole-workgroup rounds each (a 100 MB call: 370 us of k_period).
+  __shared__ uint8_t cand[512];
+  for (uint32_t i = threadIdx.x; i < nd; i += kT) {
+    const uint32_t p = sorted[i];
+    bool ok = p < n;
+    const uint32_t m = ok ? min(64u, n - p) : 0u;
+    for (uint32_t j = 0; ok && j < m; j += 16) {
+      uint4 x, y;
+      __builtin_memcpy(&x, blk + lo + j, 16);
+      __builtin_memcpy(&y, blk + lo + j + p, 16);
+      const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+      for (uint32_t c = 0; c < 16 && j + c < m; c++) ok = ok && (((xs[c >> 2] ^ ys[c >> 2]) >> (8 * (c & 3))) & 0xffu) == 0;
+    }
+    cand[i] = ok ? 1 : 0;
+  }
+  __syncthreads();
   uint32_t result = n;
   for (uint32_t q = 0; q < nd; q++) {
     const uint32_t p = sorted[q];
     if (p >= n) break;
+    if (!cand[q]) continue;  // (uniform: every thread reads the same flag)
     if (threadIdx.x == 0) bad = 0;
     __syncthreads();
     // 16 bytes per thread and step (unaligned loads; the block buffer is padded), 64 KB per
@@ -1253,6 +1273,11 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   // the block CRCs are read only by the packing: on a side stream they overlap the sort
   const uint32_t* ctab = ws.crc_table();
   const uint32_t* xtab = ws.xpow2_table();
+  // every buffer the side stream touches (here and in block_info_stage) is allocated, on st,
+  // before crc_in is recorded: the stream-ordered allocator lets crc_st use memory only once it
+  // is ordered behind the allocation
+  (void)ws.u32("inuse", (size_t)(B + 2) * 8);
+  (void)ws.u32("ninuse", B + 2);
   hipStream_t cs = st;
   if (crc_st && crc_in && crc_out) {
     HIP_OK(hipEventRecord(crc_in, st));

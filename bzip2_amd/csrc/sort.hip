@@ -2509,8 +2509,13 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       // buckets, most of them settled by their first 16 characters) stays as it is: its
       // reorder would cost more than the L2 locality it buys.
       constexpr uint64_t reorder_div = 32;  // profiles/r04_ab_s2_reorder.txt
+      // A part of few blocks is skipped as well: its text and slots are few enough to stay in
+      // the caches in any order, and the reorder's 7 x 4 launches and its per-block atomics
+      // (few counters, heavily contended) cost a 50 MB part about 0.5 ms on its critical path.
+      static const uint64_t reorder_min_s = (uint64_t)env_ll("BZG_REORDER_MIN_S", 200000000ll);
       uint32_t* ucnt = ws.u32("sort_ucnt", nb + 64);
       for (int c = 0; c < kS2Cls; c++) {
+        if (S < reorder_min_s) break;
         if (ncls[c] < 2) continue;
         if ((uint64_t)ncls[c] * reorder_div > S) continue;
         HIP_OK(hipMemsetAsync(ucnt, 0, 4 * (size_t)nb, st));
