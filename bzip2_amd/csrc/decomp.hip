@@ -147,6 +147,13 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
   __shared__ uint8_t lens[kNGroups][kMaxAlpha];
   __shared__ uint32_t cnt[kMaxDecLen + 1];
   __shared__ uint8_t seq[256];
+  // windowed chain decoding of the selectors and the symbols (below): stream words in an LDS
+  // ring, a window of kWin bit positions decoded at every position, pointer-jump tables
+  constexpr uint32_t kWin = 256, kPerLane = kWin / 64, kRing = 256;
+  __shared__ uint32_t ring[kRing];         // stream words [rfill - kRing, rfill) at [w % kRing]
+  __shared__ uint16_t J[6][kWin + 1];      // J[b][q]: the start 2^b codes after q (kWin: outside)
+  __shared__ uint16_t nxa[kWin];           // q + length of the code at q (unclamped)
+  __shared__ uint16_t sq[kWin];            // symbol of the code at q (selectors: leading ones)
   const uint32_t c = blockIdx.x;
   if (c >= nc) return;
   const uint32_t lane = __lane_id();
@@ -157,6 +164,54 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
   BitWindow W;
   W.init(in, nbytes, p);
   uint32_t ninuse = 0, g = 0, nsel = 0, alpha = 0;
+  uint64_t rfill = 0;  // the ring holds stream words [rfill - kRing, rfill); the next 128 are in pre0 / pre1
+  uint32_t pre0 = 0, pre1 = 0;
+  auto ring_init = [&](uint64_t bit) {
+    rfill = bit >> 5;
+#pragma unroll
+    for (uint32_t k = 0; k < kRing / 64; k++)
+      ring[(rfill + 64 * k + lane) % kRing] = bswap32(stream_word_raw(in, nbytes, rfill + 64 * k + lane));
+    rfill += kRing;
+    pre0 = stream_word_raw(in, nbytes, rfill + lane);
+    pre1 = stream_word_raw(in, nbytes, rfill + 64 + lane);
+    if (lane < 6) J[lane][kWin] = (uint16_t)kWin;
+    __builtin_amdgcn_wave_barrier();
+  };
+  // bits up to `bit` (exclusive) readable from the ring; the window start must stay within the
+  // ring's last kRing - 128 words (windows are kWin + 32 bits, far below)
+  auto ring_ensure = [&](uint64_t bit) {
+    while (((bit + 31) >> 5) >= rfill) {
+      ring[(rfill + lane) % kRing] = bswap32(pre0);
+      ring[(rfill + 64 + lane) % kRing] = bswap32(pre1);
+      rfill += 128;
+      pre0 = stream_word_raw(in, nbytes, rfill + lane);
+      pre1 = stream_word_raw(in, nbytes, rfill + 64 + lane);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto ring_peek = [&](uint64_t x) -> uint32_t {  // the 32 bits at absolute bit x (ensured)
+    const uint32_t w = (uint32_t)(x >> 5), sh = (uint32_t)(x & 31);
+    const uint32_t hi = ring[w % kRing], lo = ring[(w + 1) % kRing];
+    return sh ? (hi << sh) | (lo >> (32 - sh)) : hi;
+  };
+  // the chain 0 -> J[0][0] -> ... through the window: J[1..5] by pointer jumping, then lane i
+  // composes its i steps; jq holds J[0] of this lane's positions on entry.  Returns s_lane.
+  auto chain_starts = [&](uint32_t (&jq)[kPerLane]) -> uint32_t {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t b = 1; b < 6; b++) {
+#pragma unroll
+      for (uint32_t k = 0; k < kPerLane; k++) jq[k] = J[b - 1][jq[k]];
+#pragma unroll
+      for (uint32_t k = 0; k < kPerLane; k++) J[b][lane + 64 * k] = (uint16_t)jq[k];
+      __builtin_amdgcn_wave_barrier();
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 6; b++)
+      if ((lane >> b) & 1u) s = J[b][s];
+    return s;
+  };
 
   // ---- block header (decompress.c:306-352): magic (found by the scan), CRC, rand bit, origPtr
   // the reference checks origPtr before it reads the 16 mapping bits (decompress.c:348-351)
@@ -188,38 +243,71 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
   g = W.get(p, 3);
   nsel = W.get(p, 15);
   if (g < 2 || g > 6 || nsel < 1 || nsel > kSelCap) { status = BZ_DATA_ERROR; goto done; }
+  // The unary codes are decoded as chains through windows of kWin bit positions (the leading
+  // 1 bits at every position at once, as for the symbols below), the MTF of the table numbers
+  // then runs over the window's codes in order (a serial loop per selector was most of the
+  // header's time: ~12,000 selectors per text block).
+  ring_init(p);
   {
     uint32_t pos = 0x543210u;  // MTF list of table numbers, 4 bits per entry
-    uint32_t sreg = 0;
     uint8_t* sdst = selbuf + (size_t)c * kSelCap;
-    for (uint32_t i = 0; i < nsel; i++) {
-      const uint32_t v = W.peek32(p);
-      const uint32_t o = (~v == 0u) ? 32u : (uint32_t)__builtin_clz(~v);  // leading 1 bits
-      const uint32_t need = o >= g ? g : o + 1;  // the g-th 1 bit is the error
-      if (p + need > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
-      if (o >= g) { status = BZ_DATA_ERROR; goto done; }
-      p += o + 1;
-      const uint32_t t = (pos >> (4 * o)) & 0xfu;
-      if (o) {
-        const uint32_t low = pos & ((1u << (4 * o)) - 1u);
-        pos = (pos & ~((1u << (4 * (o + 1))) - 1u)) | (low << 4) | t;
+    uint64_t a = p;
+    uint32_t i0 = 0;
+    while (i0 < nsel) {
+      ring_ensure(a + kWin + 32);
+      uint32_t jq[kPerLane];
+#pragma unroll
+      for (uint32_t k = 0; k < kPerLane; k++) {
+        const uint32_t q = lane + 64 * k;
+        const uint32_t v = ring_peek(a + q);
+        const uint32_t o = (~v == 0u) ? 32u : (uint32_t)__builtin_clz(~v);  // leading 1 bits
+        sq[q] = (uint16_t)o;
+        jq[k] = o >= g ? kWin : min(q + o + 1, kWin);  // (the g-th 1 bit is an error: the chain stops)
+        J[0][q] = (uint16_t)jq[k];
       }
-      if (lane == (i & 63)) sreg = t;
-      if ((i & 63) == 63 || i + 1 == nsel) {
-        const uint32_t b0 = i & ~63u;
-        if (b0 + lane <= i) sdst[b0 + lane] = (uint8_t)sreg;
+      const uint32_t s = chain_starts(jq);
+      const bool in_win = i0 + lane < nsel && s < kWin;
+      const uint32_t m = (uint32_t)__popcll(__ballot(in_win));
+      const uint32_t o = in_win ? sq[s] : 0u;
+      const uint64_t at = a + s;
+      const uint32_t need = o >= g ? g : o + 1;
+      const uint64_t eofm = __ballot(in_win && at + need > nbits), errm = __ballot(in_win && o >= g);
+      const uint32_t ieof = eofm ? (uint32_t)__builtin_ctzll(eofm) : 64u;
+      const uint32_t ierr = errm ? (uint32_t)__builtin_ctzll(errm) : 64u;
+      const uint32_t cnt = min(m, min(ieof, ierr));
+      uint32_t selv = 0;
+      for (uint32_t j = 0; j < cnt; j++) {
+        const uint32_t oj = rdlane(o, j);
+        const uint32_t t = (pos >> (4 * oj)) & 0xfu;
+        if (oj) {
+          const uint32_t low = pos & ((1u << (4 * oj)) - 1u);
+          pos = (pos & ~((1u << (4 * (oj + 1))) - 1u)) | (low << 4) | t;
+        }
+        selv = lane == j ? t : selv;
       }
+      if (lane < cnt) sdst[i0 + lane] = (uint8_t)selv;
+      if (cnt < m) {  // at code cnt: the stream ends (checked first), or its g-th 1 bit
+        p = rdlane64(at, cnt);
+        status = ieof <= ierr ? BZ_UNEXPECTED_EOF : BZ_DATA_ERROR;
+        goto done;
+      }
+      a = rdlane64(at + o + 1, m - 1);
+      i0 += m;
     }
+    p = a;
   }
   // ---- code lengths (decompress.c:412-425): 5-bit start, then per symbol 0 | 1(0:+1, 1:-1)
   for (uint32_t t = 0; t < g; t++) {
     if (p + 5 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
-    uint32_t curr = W.get(p, 5);
+    ring_ensure(p + 32);
+    uint32_t curr = ring_peek(p) >> 27;
+    p += 5;
     for (uint32_t s = 0; s < alpha; s++) {
       for (;;) {
         if (curr < 1 || curr > (uint32_t)kMaxDecLen) { status = BZ_DATA_ERROR; goto done; }
         if (p + 2 > nbits) { status = BZ_UNEXPECTED_EOF; goto done; }
-        const uint32_t two = W.peek32(p) >> 30;
+        ring_ensure(p + 32);
+        const uint32_t two = ring_peek(p) >> 30;
         if (!(two & 2u)) {
           p += 1;
           break;
@@ -291,23 +379,12 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
   // included) takes the next slot of its group; a symbol past the last selector's group is a
   // data error (decompress.c GET_MTF_VAL), a code running past the stream end an unexpected EOF.
   {
-    constexpr uint32_t kWin = 256, kPerLane = kWin / 64, kRing = 256;
-    __shared__ uint32_t ring[kRing];         // stream words [rfill - kRing, rfill) at [w % kRing]
-    __shared__ uint16_t J[6][kWin + 1];      // J[b][q]: the start 2^b codes after q (kWin: outside)
-    __shared__ uint16_t nxa[kWin];           // q + length of the code at q (unclamped)
-    __shared__ uint16_t sq[kWin];            // symbol of the code at q
     const uint32_t eob = ninuse + 1;
     const uint8_t* ssrc = selbuf + (size_t)c * kSelCap;
     uint16_t* sdst = symbuf + (size_t)c * symstride;
     // the serial decoder's cap (more symbols than a block can hold): stop at the first multiple
     // of 64 above nbmax
     const uint32_t cap = 64u * (nbmax / 64u + 1u);
-    uint64_t rfill = p >> 5;
-#pragma unroll
-    for (uint32_t k = 0; k < kRing / 64; k++) ring[(rfill + 64 * k + lane) % kRing] = bswap32(stream_word_raw(in, nbytes, rfill + 64 * k + lane));
-    rfill += kRing;
-    uint32_t pre0 = stream_word_raw(in, nbytes, rfill + lane), pre1 = stream_word_raw(in, nbytes, rfill + 64 + lane);
-    if (lane < 6) J[lane][kWin] = (uint16_t)kWin;
     t_sym = clock64();
     uint64_t a = p;  // absolute bit of the next code
     uint32_t gi = 0, sreg = 0;
@@ -320,24 +397,13 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
       gi++;
       uint32_t need = kGroupSize;
       while (need > 0) {
-        // the window's words (kWin + 32 bits) in the ring: the next 128 come from registers
-        while (((a + kWin + 32) >> 5) >= rfill) {
-          ring[(rfill + lane) % kRing] = bswap32(pre0);
-          ring[(rfill + 64 + lane) % kRing] = bswap32(pre1);
-          rfill += 128;
-          pre0 = stream_word_raw(in, nbytes, rfill + lane);
-          pre1 = stream_word_raw(in, nbytes, rfill + 64 + lane);
-        }
-        __builtin_amdgcn_wave_barrier();
+        ring_ensure(a + kWin + 32);
         // the code at every position of the window
         uint32_t jq[kPerLane];
 #pragma unroll
         for (uint32_t k = 0; k < kPerLane; k++) {
           const uint32_t q = lane + 64 * k;
-          const uint64_t x = a + q;
-          const uint32_t w = (uint32_t)(x >> 5), sh = (uint32_t)(x & 31);
-          const uint32_t hi = ring[w % kRing], lo = ring[(w + 1) % kRing];
-          const uint32_t v = sh ? (hi << sh) | (lo >> (32 - sh)) : hi;
+          const uint32_t v = ring_peek(a + q);
           const uint32_t e = lut[tb + (v >> (32 - kLutBits))];
           uint32_t len, s0;
           if ((e & 0x60u) == 0) {  // longer than the table: canonical limits per length
@@ -353,21 +419,7 @@ __global__ void __launch_bounds__(64) k_dec_huff(const uint8_t* __restrict__ in,
           jq[k] = min(q + len, kWin);
           J[0][q] = (uint16_t)jq[k];
         }
-        __builtin_amdgcn_wave_barrier();
-        // next^(2^b) for b = 1..5
-#pragma unroll
-        for (uint32_t b = 1; b < 6; b++) {
-#pragma unroll
-          for (uint32_t k = 0; k < kPerLane; k++) jq[k] = J[b - 1][jq[k]];
-#pragma unroll
-          for (uint32_t k = 0; k < kPerLane; k++) J[b][lane + 64 * k] = (uint16_t)jq[k];
-          __builtin_amdgcn_wave_barrier();
-        }
-        // lane i: the start of the i-th code of the window
-        uint32_t s = 0;
-#pragma unroll
-        for (uint32_t b = 0; b < 6; b++)
-          if ((lane >> b) & 1u) s = J[b][s];
+        const uint32_t s = chain_starts(jq);
         const bool in_win = lane < need && s < kWin;
         const uint32_t m = (uint32_t)__popcll(__ballot(in_win));  // codes of the group in this window
         const uint32_t sym = in_win ? sq[s] : 0u;
