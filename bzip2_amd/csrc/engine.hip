@@ -11,6 +11,7 @@
 #include <vector>
 #include <cstring>
 #include <exception>
+#include <functional>
 #include <future>
 #include <mutex>
 #include <thread>
@@ -224,19 +225,13 @@ struct Engine {
   Workspace ws;
   std::vector<std::unique_ptr<Workspace>> pws;  // one per part of a batch
   std::vector<hipEvent_t> psorted;              // per part: its sort is done
-  hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // batch(): MTF start, tables start, tables end
-  hipEvent_t ev[6];
-  hipEvent_t ev_rle;
-  hipEvent_t ev_crc_in = nullptr, ev_crc_out = nullptr;  // block CRCs on the idle sort stream
+  hipEvent_t ev_rle;  // the sort streams start after RLE1
 
   explicit Engine(int dev) : device(dev) {
     HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto& x : sstream) HIP_OK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-    for (auto& e : ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipEventCreateWithFlags(&ev_rle, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_crc_in, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_crc_out, hipEventDisableTiming));
     ws.set_stream(stream);
   }
 
@@ -244,11 +239,13 @@ struct Engine {
   // after the call, and later growth or release must not be ordered on it.
   void own_streams() {
     ws.set_stream(stream);
+    ws2.set_stream(stream);
     for (auto& w : pws) w->set_stream(stream);
   }
   void release_idle() {
     own_streams();
     ws.release_all();
+    ws2.release_all();
     for (auto& w : pws) w->release_all();
   }
 
@@ -287,21 +284,54 @@ struct Engine {
     return std::min(hi, std::max(lo, e ? atoi(e) : dflt));
   }
 
-  // Compress one batch.  Throws HipFailure on device errors, OutBuffFull when out_cap is short.
+  // ---- one batch, in two stages -------------------------------------------------------
+  // front: RLE1 and the block sorts (origPtr included); back: MTF, the table optimisation and
+  // the packing.  batch() runs both on the caller's stream.  A multi-batch input pipelines them
+  // (compress below): the back stage of batch j (its own workspace slot and streams) runs
+  // beside the front stage of batch j + 1, which needs only batch j's consumed input.
   //
   // The blocks are cut into parts.  Each part is sorted on one of the sort streams by its own
   // host thread (the sorter synchronises with the host between passes, so several parts keep
-  // the device busy); once every part is sorted, origPtr, MTF and the table optimisation run
-  // over the whole batch on the main stream, then the bit offsets and the packing.
-  void batch(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
-             uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
-    const int level = st->level;
-    const bool end_seg = flags & BZG_FLAG_END_SEGMENT;
-    const bool tail_merge = (flags & BZG_FLAG_TAIL_MERGE) && end_seg;
-    const bool trailer = (flags & BZG_FLAG_TRAILER) && end_seg;
-    ws.set_stream(s);
-    HIP_OK(hipEventRecord(ev[0], s));
+  // the device busy); origPtr of a part's blocks follows its sort on the same stream.
+  struct SlotEvents {  // timing and side-stream events of one workspace slot
+    hipEvent_t ev[6] = {};
+    hipEvent_t tev[3] = {};
+    hipEvent_t crc_in = nullptr, crc_out = nullptr;
+    hipEvent_t sorted = nullptr;  // the front stage is complete on every stream it used
+    void create() {
+      if (crc_in) return;
+      for (auto& e : ev) HIP_OK(hipEventCreate(&e));
+      for (auto& e : tev) HIP_OK(hipEventCreate(&e));
+      HIP_OK(hipEventCreateWithFlags(&crc_in, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&crc_out, hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
+    }
+  };
+  struct BatchCtx {
+    Workspace* w = nullptr;
+    SlotEvents* e = nullptr;
+    int level = 9;
+    bool end_seg = false, tail_merge = false, trailer = false;
     Rle1Result r;
+    uint32_t nb = 0, nparts = 0;
+    std::vector<uint32_t> hboff, hper, hbq, hqp;
+    std::unique_ptr<Part[]> parts;
+    uint32_t* origptr = nullptr;
+    uint8_t* bwt = nullptr;
+    uint64_t sort_iters = 0, sort_unsorted = 0;
+    uint64_t consumed = 0;
+  };
+
+  void front(BatchCtx& c, const uint8_t* d_in, uint64_t n, unsigned flags, int level, hipStream_t s) {
+    Workspace& W = *c.w;
+    SlotEvents& E = *c.e;
+    c.level = level;
+    c.end_seg = flags & BZG_FLAG_END_SEGMENT;
+    c.tail_merge = (flags & BZG_FLAG_TAIL_MERGE) && c.end_seg;
+    c.trailer = (flags & BZG_FLAG_TRAILER) && c.end_seg;
+    W.set_stream(s);
+    HIP_OK(hipEventRecord(E.ev[0], s));
+    Rle1Result& r = c.r;
     // the block CRCs run on the last sort stream (idle at the default two sort streams; with
     // three it only queues behind that stream's sorts) and overlap the sort
     hipStream_t crc_st = sstream[kSortStreams - 1];  // (profiles/r05_ab_crc_side.txt)
@@ -313,215 +343,258 @@ struct Engine {
         if (std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(side);
       }
     } side_join{crc_st};
-    rle1_stage(ws, d_in, n, level, end_seg, tail_merge, r, s, crc_st, ev_crc_in, ev_crc_out);
-    HIP_OK(hipEventRecord(ev[1], s));
-    const uint32_t nb = r.nblocks;
-    uint32_t* origptr = ws.u32("origptr", nb + 2);
-    std::vector<uint32_t> hboff(nb + 1), hper(nb), hbq(nb), hqp(nb);
-    std::unique_ptr<Part[]> parts;
-    uint32_t K = 0, nparts = 0;
-    float mtf_ms = 0, tab_ms = 0, last_post = 0;
-    uint64_t sort_iters = 0, sort_unsorted = 0;
-    if (nb > 0) {
-      ws.read_small({{hboff.data(), r.boff, 4ull * (nb + 1)}, {hper.data(), r.period, 4ull * nb}, {hbq.data(), r.bq, 4ull * nb},
-                     {hqp.data(), r.qper, 4ull * nb}},
-                    s);
-      uint8_t* bwt = ws.u8("bwt", hboff[nb] + 16);
-      uint32_t* rank0 = ws.u32("rank0", nb + 2);
-      static const bool one_stream = getenv("BZG_ONE_STREAM") != nullptr;  // per-kernel profiling
-      const int want = nb < 64 || one_stream ? 1 : cfg("BZG_PARTS", 2, 1, 16);
-      K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)want, nb / 16));
-      const int S = nb < 64 || one_stream ? 1 : std::min<int>((int)K, cfg("BZG_SORT_STREAMS", 2, 1, kSortStreams));
-      parts.reset(new Part[K]);
-      nparts = K;
-      for (uint32_t p = 0; p < K; p++) {
-        Part& P = parts[p];
-        P.b0 = (uint32_t)((uint64_t)nb * p / K);
-        P.b1 = (uint32_t)((uint64_t)nb * (p + 1) / K);
-        const uint32_t pn = P.b1 - P.b0, base = hboff[P.b0];
-        P.w = part_ws(p);
-        P.w->set_stream(s);
-        P.hboff.assign(hboff.begin() + P.b0, hboff.begin() + P.b1 + 1);
-        for (auto& x : P.hboff) x -= base;
-        P.hper.assign(hper.begin() + P.b0, hper.begin() + P.b1);
-        P.hbq.assign(hbq.begin() + P.b0, hbq.begin() + P.b1);
-        P.hqp.assign(hqp.begin() + P.b0, hqp.begin() + P.b1);
-        P.r = r;
-        P.r.nblocks = pn;
-        P.r.blk = r.blk + base;
-        P.r.boff = P.w->u32("part_boff", pn + 2);
-        HIP_OK(hipMemcpyAsync(P.r.boff, P.hboff.data(), 4ull * (pn + 1), hipMemcpyHostToDevice, s));
-        P.r.binst = nullptr;
-        P.r.bcrc = r.bcrc + P.b0;
-        P.r.inuse = r.inuse + 8ull * P.b0;
-        P.r.ninuse = r.ninuse + P.b0;
-        P.r.period = r.period + P.b0;
-        P.r.bq = r.bq + P.b0;
-        P.r.qper = r.qper + P.b0;
-      }
-      HIP_OK(hipEventRecord(ev_rle, s));  // the sort streams start after RLE1 and the views
-      std::vector<std::promise<void>> sorted(K);
-      std::vector<std::future<void>> sorted_f;
-      for (auto& x : sorted) sorted_f.push_back(x.get_future());
-      // raised right after a part's promise is settled: the main thread spins on it rather
-      // than sleeping in the future (a wake-up took ~50 us of idle device per part)
-      std::unique_ptr<std::atomic<int>[]> settled(new std::atomic<int>[K]);
-      for (uint32_t p = 0; p < K; p++) settled[p].store(0);
-      const int dev = device;
-      auto sorter = [&, dev](int t) {
-        try {
-          HIP_OK(hipSetDevice(dev));  // the current device is per host thread
-        } catch (...) {
-          for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) {
-            sorted[p].set_exception(std::current_exception());
-            settled[p].store(1, std::memory_order_release);
-          }
-          return;
-        }
-        hipStream_t ss = S == 1 ? s : sstream[t];
-        bool failed = false;
+    rle1_stage(W, d_in, n, level, c.end_seg, c.tail_merge, r, s, crc_st, E.crc_in, E.crc_out);
+    HIP_OK(hipEventRecord(E.ev[1], s));
+    c.consumed = c.end_seg ? n : r.consumed;
+    const uint32_t nb = c.nb = r.nblocks;
+    c.origptr = W.u32("origptr", nb + 2);
+    c.hboff.assign(nb + 1, 0u);
+    c.hper.assign(nb, 0u);
+    c.hbq.assign(nb, 0u);
+    c.hqp.assign(nb, 0u);
+    if (nb == 0) {
+      HIP_OK(hipEventRecord(E.sorted, s));
+      return;
+    }
+    W.read_small({{c.hboff.data(), r.boff, 4ull * (nb + 1)}, {c.hper.data(), r.period, 4ull * nb},
+                  {c.hbq.data(), r.bq, 4ull * nb}, {c.hqp.data(), r.qper, 4ull * nb}},
+                 s);
+    uint8_t* bwt = c.bwt = W.u8("bwt", c.hboff[nb] + 16);
+    uint32_t* rank0 = W.u32("rank0", nb + 2);
+    uint32_t* origptr = c.origptr;
+    static const bool one_stream = getenv("BZG_ONE_STREAM") != nullptr;  // per-kernel profiling
+    const int want = nb < 64 || one_stream ? 1 : cfg("BZG_PARTS", 2, 1, 16);
+    const uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)want, nb / 16));
+    const int S = nb < 64 || one_stream ? 1 : std::min<int>((int)K, cfg("BZG_SORT_STREAMS", 2, 1, kSortStreams));
+    c.parts.reset(new Part[K]);
+    c.nparts = K;
+    Part* parts = c.parts.get();
+    for (uint32_t p = 0; p < K; p++) {
+      Part& P = parts[p];
+      P.b0 = (uint32_t)((uint64_t)nb * p / K);
+      P.b1 = (uint32_t)((uint64_t)nb * (p + 1) / K);
+      const uint32_t pn = P.b1 - P.b0, base = c.hboff[P.b0];
+      P.w = part_ws(p);
+      P.w->set_stream(s);
+      P.hboff.assign(c.hboff.begin() + P.b0, c.hboff.begin() + P.b1 + 1);
+      for (auto& x : P.hboff) x -= base;
+      P.hper.assign(c.hper.begin() + P.b0, c.hper.begin() + P.b1);
+      P.hbq.assign(c.hbq.begin() + P.b0, c.hbq.begin() + P.b1);
+      P.hqp.assign(c.hqp.begin() + P.b0, c.hqp.begin() + P.b1);
+      P.r = r;
+      P.r.nblocks = pn;
+      P.r.blk = r.blk + base;
+      P.r.boff = P.w->u32("part_boff", pn + 2);
+      HIP_OK(hipMemcpyAsync(P.r.boff, P.hboff.data(), 4ull * (pn + 1), hipMemcpyHostToDevice, s));
+      P.r.binst = nullptr;
+      P.r.bcrc = r.bcrc + P.b0;
+      P.r.inuse = r.inuse + 8ull * P.b0;
+      P.r.ninuse = r.ninuse + P.b0;
+      P.r.period = r.period + P.b0;
+      P.r.bq = r.bq + P.b0;
+      P.r.qper = r.qper + P.b0;
+    }
+    HIP_OK(hipEventRecord(ev_rle, s));  // the sort streams start after RLE1 and the views
+    std::vector<std::promise<void>> sorted(K);
+    std::vector<std::future<void>> sorted_f;
+    for (auto& x : sorted) sorted_f.push_back(x.get_future());
+    // raised right after a part's promise is settled: the main thread spins on it rather
+    // than sleeping in the future (a wake-up took ~50 us of idle device per part)
+    std::unique_ptr<std::atomic<int>[]> settled(new std::atomic<int>[K]);
+    for (uint32_t p = 0; p < K; p++) settled[p].store(0);
+    const int dev = device;
+    auto sorter = [&, dev](int t) {
+      try {
+        HIP_OK(hipSetDevice(dev));  // the current device is per host thread
+      } catch (...) {
         for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) {
-          if (failed) {
-            sorted[p].set_exception(std::make_exception_ptr(HipFailure(hipErrorUnknown)));
-            settled[p].store(1, std::memory_order_release);
-            continue;
-          }
-          try {
-            Part& P = parts[p];
-            P.w->set_stream(ss);
-            if (ss != s) HIP_OK(hipStreamWaitEvent(ss, ev_rle, 0));
-            copyrank_begin(*P.w, P.r, P.hboff, P.hper, P.hbq, P.a5, ss);  // (side stream: overlaps the sort)
-            bwt_stage(*P.w, P.r, P.hboff, P.hper, bwt + hboff[P.b0], rank0 + P.b0, &P.ss, ss, P.hqp.data());
-            HIP_OK(hipEventRecord(psorted[p], ss));
-            sorted[p].set_value();
-          } catch (...) {
-            failed = true;
-            sorted[p].set_exception(std::current_exception());
-          }
+          sorted[p].set_exception(std::current_exception());
           settled[p].store(1, std::memory_order_release);
         }
-      };
-      // the timing events exist before any sorter thread starts, so every exit path below
-      // joins the threads
-      for (hipEvent_t& e : tev)
-        if (!e) HIP_OK(hipEventCreate(&e));
-      hipEvent_t e0 = tev[0], e1 = tev[1], e2 = tev[2];
-      std::vector<std::thread> th;
-      std::exception_ptr err;
-      try {
-        // this thread sorts the first stream's parts itself (one thread fewer to start, and it
-        // does not sit idle)
-        for (int t = 1; t < S; t++) th.emplace_back(sorter, t);
-        sorter(0);
-        // measured (profiles/r03_pipeline_sweep.txt): MTF and tables beside the later sorts
-        // slow both more than they overlap; they run once over the whole batch after every
-        // part is sorted
-        for (uint32_t p = 0; p < K; p++) {
-          if (S > 1)
-            while (!settled[p].load(std::memory_order_acquire)) __builtin_ia32_pause();
-          sorted_f[p].get();
-          HIP_OK(hipStreamWaitEvent(s, psorted[p], 0));
-        }
-        for (auto& x : th) x.join();
-        th.clear();
-        HIP_OK(hipEventRecord(e0, s));
-        for (uint32_t p = 0; p < K; p++) {
-          parts[p].w->set_stream(s);
-          copyrank_finish(*parts[p].w, parts[p].r, rank0 + parts[p].b0, origptr + parts[p].b0, parts[p].a5, s);
-        }
-        K = 1;  // one part over the whole batch from here on
-        Part& P = parts[0];
-        P.b0 = 0;
-        P.b1 = nb;
-        P.r = r;
-        P.hboff = hboff;
-        P.w = &ws;
-        HIP_OK(hipStreamWaitEvent(s, ev_crc_out, 0));  // in-use maps and block CRCs (side stream)
-        mtf_stage(ws, r, bwt, nb, hboff[nb], P.m, s, &hboff);
-        HIP_OK(hipEventRecord(e1, s));
-        code_tables(ws, r, P.m, nb, P.t, s, split_tables() ? sstream[0] : nullptr);
-        HIP_OK(hipEventRecord(e2, s));  // (timings and the A5 check once the batch is done, below)
-      } catch (...) {
-        err = std::current_exception();
+        return;
       }
-      for (auto& x : th) x.join();
-      if (err) std::rethrow_exception(err);
-      for (uint32_t p = 0; p < nparts; p++) {
-        const Part& P = parts[p];
-        sort_iters = std::max<uint64_t>(sort_iters, (uint64_t)P.ss.iterations);
-        sort_unsorted += P.ss.unsorted_elems;
+      hipStream_t ss = S == 1 ? s : sstream[t];
+      bool failed = false;
+      for (uint32_t p = (uint32_t)t; p < K; p += (uint32_t)S) {
+        if (failed) {
+          sorted[p].set_exception(std::make_exception_ptr(HipFailure(hipErrorUnknown)));
+          settled[p].store(1, std::memory_order_release);
+          continue;
+        }
+        try {
+          Part& P = parts[p];
+          P.w->set_stream(ss);
+          if (ss != s) HIP_OK(hipStreamWaitEvent(ss, ev_rle, 0));
+          copyrank_begin(*P.w, P.r, P.hboff, P.hper, P.hbq, P.a5, ss);  // (side stream: overlaps the sort)
+          bwt_stage(*P.w, P.r, P.hboff, P.hper, bwt + c.hboff[P.b0], rank0 + P.b0, &P.ss, ss, P.hqp.data());
+          copyrank_finish(*P.w, P.r, rank0 + P.b0, origptr + P.b0, P.a5, ss);
+          HIP_OK(hipEventRecord(psorted[p], ss));
+          sorted[p].set_value();
+        } catch (...) {
+          failed = true;
+          sorted[p].set_exception(std::current_exception());
+        }
+        settled[p].store(1, std::memory_order_release);
       }
+    };
+    std::vector<std::thread> th;
+    std::exception_ptr err;
+    try {
+      // this thread sorts the first stream's parts itself (one thread fewer to start, and it
+      // does not sit idle)
+      for (int t = 1; t < S; t++) th.emplace_back(sorter, t);
+      sorter(0);
+      for (uint32_t p = 0; p < K; p++) {
+        if (S > 1)
+          while (!settled[p].load(std::memory_order_acquire)) __builtin_ia32_pause();
+        sorted_f[p].get();
+        HIP_OK(hipStreamWaitEvent(s, psorted[p], 0));
+      }
+      HIP_OK(hipStreamWaitEvent(s, E.crc_out, 0));  // in-use maps and block CRCs (side stream)
+      HIP_OK(hipEventRecord(E.sorted, s));
+    } catch (...) {
+      err = std::current_exception();
     }
-    HIP_OK(hipEventRecord(ev[2], s));
-    StreamCarry c;
-    c.combined_crc = st->combined_crc;
-    c.carry_bits = st->carry_bits;
-    c.carry_byte = st->carry_byte;
-    c.header_done = st->header_done;
+    for (auto& x : th) x.join();
+    if (err) std::rethrow_exception(err);
+    for (uint32_t p = 0; p < K; p++) {
+      c.sort_iters = std::max<uint64_t>(c.sort_iters, (uint64_t)parts[p].ss.iterations);
+      c.sort_unsorted += parts[p].ss.unsorted_elems;
+    }
+  }
+
+  // MTF, tables and packing of a front-staged batch on stream s (s2: the second table stream,
+  // or null).  `before_emit` (optional) runs on this thread right before the packing, which
+  // needs the stream state the previous batch leaves.
+  void back(BatchCtx& c, bzg_stream_state* st, uint8_t* d_out, uint64_t out_cap, uint64_t* out_bytes, hipStream_t s,
+            hipStream_t s2, bzg_stats& last, const std::function<void()>& before_emit = nullptr) {
+    Workspace& W = *c.w;
+    SlotEvents& E = *c.e;
+    W.set_stream(s);
+    HIP_OK(hipStreamWaitEvent(s, E.sorted, 0));
+    const uint32_t nb = c.nb;
+    Part* parts = c.parts.get();
+    Part one;  // the whole batch from here on
+    float mtf_ms = 0, tab_ms = 0;
+    if (nb > 0) {
+      HIP_OK(hipEventRecord(E.tev[0], s));
+      one.b0 = 0;
+      one.b1 = nb;
+      one.r = c.r;
+      one.hboff = c.hboff;
+      one.w = &W;
+      mtf_stage(W, c.r, c.bwt, nb, c.hboff[nb], one.m, s, &c.hboff);
+      HIP_OK(hipEventRecord(E.tev[1], s));
+      code_tables(W, c.r, one.m, nb, one.t, s, s2);
+      HIP_OK(hipEventRecord(E.tev[2], s));  // (timings and the A5 check once the batch is done, below)
+    }
+    HIP_OK(hipEventRecord(E.ev[2], s));
+    if (before_emit) before_emit();
+    StreamCarry cy;
+    cy.combined_crc = st->combined_crc;
+    cy.carry_bits = st->carry_bits;
+    cy.carry_byte = st->carry_byte;
+    cy.header_done = st->header_done;
     std::vector<CodePart> cp;
-    for (uint32_t p = 0; p < K; p++) cp.push_back(CodePart{&parts[p].r, &parts[p].m, &parts[p].t, origptr + parts[p].b0, parts[p].r.nblocks});
-    *out_bytes = code_emit(ws, cp, level, trailer, c, d_out, out_cap, s);
-    HIP_OK(hipEventRecord(ev[4], s));
+    if (nb > 0) cp.push_back(CodePart{&one.r, &one.m, &one.t, c.origptr, nb});
+    *out_bytes = code_emit(W, cp, c.level, c.trailer, cy, d_out, out_cap, s);
+    HIP_OK(hipEventRecord(E.ev[4], s));
     // the batch's end: the MTF symbol counts (a statistic) come back through the spinning
     // small read, which is also the wait for the batch (a sleeping event wait cost ~40 us)
     std::vector<uint32_t> nm(nb);
-    if (nb > 0 && K == 1 && parts[0].r.nblocks == nb)
-      ws.read_small(nm.data(), parts[0].m.nmtf, 4ull * nb, s);
+    if (nb > 0)
+      W.read_small(nm.data(), one.m.nmtf, 4ull * nb, s);
     else
-      HIP_OK(hipEventSynchronize(ev[4]));
+      HIP_OK(hipEventSynchronize(E.ev[4]));
     if (nb > 0) {
-      for (uint32_t p = 0; p < nparts; p++) copyrank_check(parts[p].a5);
-      (void)hipEventElapsedTime(&mtf_ms, tev[0], tev[1]);
-      (void)hipEventElapsedTime(&tab_ms, tev[1], tev[2]);
-      last_post = mtf_ms + tab_ms;
+      for (uint32_t p = 0; p < c.nparts; p++) copyrank_check(parts[p].a5);
+      (void)hipEventElapsedTime(&mtf_ms, E.tev[0], E.tev[1]);
+      (void)hipEventElapsedTime(&tab_ms, E.tev[1], E.tev[2]);
     }
-    st->combined_crc = c.combined_crc;
-    st->carry_bits = c.carry_bits;
-    st->carry_byte = c.carry_byte;
-    st->header_done = c.header_done ? 1 : 0;
+    st->combined_crc = cy.combined_crc;
+    st->carry_bits = cy.carry_bits;
+    st->carry_byte = cy.carry_byte;
+    st->header_done = cy.header_done ? 1 : 0;
     st->blocks_done += nb;
-    *consumed = end_seg ? n : r.consumed;
     last = bzg_stats{};
     float pipe_ms = 0, emit_ms = 0;
-    (void)hipEventElapsedTime(&last.rle1_ms, ev[0], ev[1]);
-    (void)hipEventElapsedTime(&pipe_ms, ev[1], ev[2]);
-    (void)hipEventElapsedTime(&emit_ms, ev[2], ev[4]);
-    (void)hipEventElapsedTime(&last.total_ms, ev[0], ev[4]);
-    // with the parts overlapped, the BWT figure is the sort pipeline up to the last part's
-    // tables minus the post-sort work of that last part; MTF and tables are their own
-    // durations summed over the parts (they run beside the sorts of later parts)
+    (void)hipEventElapsedTime(&last.rle1_ms, E.ev[0], E.ev[1]);
+    (void)hipEventElapsedTime(&pipe_ms, E.ev[1], E.ev[2]);
+    (void)hipEventElapsedTime(&emit_ms, E.ev[2], E.ev[4]);
+    (void)hipEventElapsedTime(&last.total_ms, E.ev[0], E.ev[4]);
+    // the BWT figure is the sort pipeline up to the tables' end minus MTF and the tables
     last.mtf_ms = mtf_ms;
     last.code_ms = tab_ms + emit_ms;
-    last.bwt_ms = std::max(0.f, pipe_ms - last_post);
+    last.bwt_ms = std::max(0.f, pipe_ms - mtf_ms - tab_ms);
     last.nblocks = nb;
-    last.sort_iterations = (int)sort_iters;
-    last.rle_bytes = nb ? hboff[nb] : 0;
-    last.sort_unsorted = sort_unsorted;
-    for (uint32_t p = 0; p < nparts; p++) {
+    last.sort_iterations = (int)c.sort_iters;
+    last.rle_bytes = nb ? c.hboff[nb] : 0;
+    last.sort_unsorted = c.sort_unsorted;
+    for (uint32_t p = 0; p < c.nparts; p++) {
       last.a5_roots += (uint32_t)parts[p].a5.need.size();
       last.a5_host += parts[p].a5.n_host;
     }
     for (uint32_t x : nm) last.mtf_symbols += x;
   }
 
-  // bzg_compress_device's contract: inputs larger than kMaxBatch are cut into batches; the
+  // Compress one batch on stream s.  Throws HipFailure on device errors, OutBuffFull when
+  // out_cap is short.
+  SlotEvents slot_ev[2];
+  Workspace ws2;  // the second workspace slot of pipelined batches
+  void batch(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
+             uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
+    slot_ev[0].create();
+    BatchCtx c;
+    c.w = &ws;
+    c.e = &slot_ev[0];
+    front(c, d_in, n, flags, st->level, s);
+    back(c, st, d_out, out_cap, out_bytes, s, split_tables() ? sstream[0] : nullptr, last);
+    *consumed = c.consumed;
+  }
+
+  // bzg_compress_device's contract: inputs larger than max_batch() are cut into batches; the
   // non-final batches emit complete blocks and the rest is resubmitted.
   void compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
                 uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last);
+  void compress_pipelined(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
+                          uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last);
 };
 
-// Largest batch handled in one pass: keeps every block/slot offset in 32 bits.
-static constexpr uint64_t kMaxBatch = 1500ull * 1000 * 1000;
+// Largest batch handled in one pass: keeps every block/slot offset in 32 bits.  BZG_MAX_BATCH
+// lowers it (tests: several pipelined batches from a small input).
+static constexpr uint64_t kMaxBatchLimit = 1500ull * 1000 * 1000;
+static uint64_t max_batch() {
+  static const uint64_t v = std::min<uint64_t>(kMaxBatchLimit, (uint64_t)std::max(1000000ll, env_ll("BZG_MAX_BATCH", (long long)kMaxBatchLimit)));
+  return v;
+}
+
+static void add_stats(bzg_stats& acc, const bzg_stats& one) {
+  acc.rle1_ms += one.rle1_ms;
+  acc.bwt_ms += one.bwt_ms;
+  acc.mtf_ms += one.mtf_ms;
+  acc.code_ms += one.code_ms;
+  acc.total_ms += one.total_ms;
+  acc.nblocks += one.nblocks;
+  acc.sort_iterations = std::max(acc.sort_iterations, one.sort_iterations);
+  acc.rle_bytes += one.rle_bytes;
+  acc.sort_unsorted += one.sort_unsorted;
+  acc.mtf_symbols += one.mtf_symbols;
+  acc.a5_roots += one.a5_roots;
+  acc.a5_host += one.a5_host;
+}
 
 void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
+  static const bool pipe = cfg("BZG_BATCH_PIPE", 1, 0, 1) != 0;  // BZG_BATCH_PIPE=0: batches one after another
+  const uint64_t batch_max = max_batch();
+  if (pipe && n > batch_max) return compress_pipelined(d_in, n, flags, st, d_out, out_cap, out_bytes, consumed, s, last);
   ws.set_stream(s);
   uint64_t done_in = 0, done_out = 0;
   bzg_stats acc{};
   for (;;) {
     const uint64_t left = n - done_in;
-    const bool last_piece = left <= kMaxBatch;
-    const uint64_t take = last_piece ? left : kMaxBatch;
+    const bool last_piece = left <= batch_max;
+    const uint64_t take = last_piece ? left : batch_max;
     const unsigned f = last_piece ? flags : 0u;
     uint64_t ob = 0, cons = 0;
     bzg_stats one{};
@@ -533,7 +606,7 @@ void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_strea
     const bool misaligned = ((uintptr_t)dst & 3u) != 0;
     uint8_t* bdst = dst;
     if (misaligned) {
-      cap = std::min<uint64_t>(cap, take + take / 50 + (take / 100000 + 2) * 64 + 4096);  // bzg_bound(take)
+      cap = std::min<uint64_t>(cap, bzg_bound(take));
       bdst = ws.u8("batch_out", cap + 16);
     }
     batch(d_in + done_in, take, f, st, bdst, cap, &ob, &cons, s, one);
@@ -541,23 +614,113 @@ void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_strea
       HIP_OK(hipMemcpyAsync(dst, bdst, ob, hipMemcpyDeviceToDevice, s));
       HIP_OK(hipStreamSynchronize(s));
     }
-    acc.rle1_ms += one.rle1_ms;
-    acc.bwt_ms += one.bwt_ms;
-    acc.mtf_ms += one.mtf_ms;
-    acc.code_ms += one.code_ms;
-    acc.total_ms += one.total_ms;
-    acc.nblocks += one.nblocks;
-    acc.sort_iterations = std::max(acc.sort_iterations, one.sort_iterations);
-    acc.rle_bytes += one.rle_bytes;
-    acc.sort_unsorted += one.sort_unsorted;
-    acc.mtf_symbols += one.mtf_symbols;
-    acc.a5_roots += one.a5_roots;
-    acc.a5_host += one.a5_host;
+    add_stats(acc, one);
     done_in += cons;
     done_out += ob;
     if (last_piece) break;
-    if (cons == 0) throw HipFailure(hipErrorUnknown);  // cannot happen: kMaxBatch holds many blocks
+    if (cons == 0) throw HipFailure(hipErrorUnknown);  // cannot happen: a batch holds many blocks
   }
+  *out_bytes = done_out;
+  *consumed = done_in;
+  last = acc;
+}
+
+// Batches of a multi-batch input, pipelined over two workspace slots: the front stage (RLE1,
+// sorts) of batch j + 1 runs on the caller's stream and the sort streams while the back stage
+// (MTF, tables, packing) of batch j runs on its slot's own streams from a second host thread.
+// The back stages pack in batch order (each needs the stream state and the output position the
+// previous one leaves); the front stage of batch j + 2 reuses slot j % 2 once batch j is done.
+// MTF is VALU-bound and the sorts wait on gathers, so the two overlap well (4 GiB of PRNG bytes,
+// three batches: profiles/r06_*).  The bytes equal the sequential batches' (the same stages on
+// the same inputs).
+void Engine::compress_pipelined(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st,
+                                uint8_t* d_out, uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed,
+                                hipStream_t s, bzg_stats& last) {
+  for (int k = 0; k < 2; k++) slot_ev[k].create();
+  // The back stages run on the CRC side stream, one stream, no table split.  A process has 4
+  // hardware queues (GPU_MAX_HW_QUEUES) and streams share them round-robin in creation order:
+  // the caller's and the engine's own stream, the two sort streams and the CRC stream take all
+  // four, and a back stage on a fifth stream shared a sort stream's queue, so it ran behind the
+  // next batch's sorts instead of beside them (config 5: no gain at all).  On the CRC stream it
+  // only delays the next batch's block CRCs, which nothing before that batch's back stage reads.
+  hipStream_t bs = sstream[kSortStreams - 1];
+  const uint64_t batch_max = max_batch();
+  Workspace* slot_ws[2] = {&ws, &ws2};
+  ws.set_stream(s);
+  ws2.set_stream(s);
+  std::unique_ptr<BatchCtx> ctx[2];
+  std::thread backer;  // the back stage of the previous batch
+  std::exception_ptr back_err;
+  uint64_t done_in = 0, done_out = 0;
+  bzg_stats acc{};
+  std::mutex mu;
+  auto join_back = [&] {
+    if (backer.joinable()) backer.join();
+    if (back_err) std::rethrow_exception(back_err);
+  };
+  try {
+    for (uint32_t j = 0;; j++) {
+      const uint64_t left = n - done_in;
+      const bool last_piece = left <= batch_max;
+      const uint64_t take = last_piece ? left : batch_max;
+      const int k = (int)(j & 1);
+      // slot k was batch j - 2's: its back stage ended before batch j - 1's began (below)
+      ctx[k].reset(new BatchCtx);
+      BatchCtx& c = *ctx[k];
+      c.w = slot_ws[k];
+      c.e = &slot_ev[k];
+      front(c, d_in + done_in, take, last_piece ? flags : 0u, st->level, s);
+      if (!last_piece && c.consumed == 0) throw HipFailure(hipErrorUnknown);  // a batch holds many blocks
+      // the previous batch's back stage must have packed before this one packs: this thread
+      // waits for it here, then hands this batch's back stage to a new thread
+      join_back();
+      uint8_t* dst = d_out + done_out;
+      const uint64_t dcap = out_cap - done_out;
+      // the slot moves to the back stage's stream here, before the next front stage queues
+      // anything on s (a handoff made later from the back thread would order the back stage
+      // behind that work too)
+      c.w->set_stream(bs);
+      HIP_OK(hipStreamWaitEvent(bs, c.e->sorted, 0));
+      const uint64_t take_in = c.consumed;
+      done_in += take_in;
+      backer = std::thread([&, k, dst, dcap, take] {
+        try {
+          HIP_OK(hipSetDevice(device));
+          BatchCtx& b = *ctx[k];
+          const bool misaligned = ((uintptr_t)dst & 3u) != 0;
+          uint64_t cap = dcap;
+          uint8_t* bdst = dst;
+          if (misaligned) {
+            b.w->set_stream(bs);
+            cap = std::min<uint64_t>(cap, bzg_bound(take));
+            bdst = b.w->u8("batch_out", cap + 16);
+          }
+          uint64_t ob = 0;
+          bzg_stats one{};
+          back(b, st, bdst, cap, &ob, bs, nullptr, one);
+          if (misaligned && ob) {
+            HIP_OK(hipMemcpyAsync(dst, bdst, ob, hipMemcpyDeviceToDevice, bs));
+            HIP_OK(hipStreamSynchronize(bs));
+          }
+          std::lock_guard<std::mutex> g(mu);
+          add_stats(acc, one);
+          done_out += ob;
+        } catch (...) {
+          back_err = std::current_exception();
+        }
+      });
+      if (last_piece) break;
+    }
+    join_back();
+  } catch (...) {
+    if (backer.joinable()) backer.join();
+    (void)hipStreamSynchronize(bs);
+    throw;
+  }
+  // the slots' workspaces go back to the caller's stream order: later growth or release by the
+  // next call is ordered after the back streams' work (already complete: the back stages
+  // ended with a host wait)
+  ws2.set_stream(stream);
   *out_bytes = done_out;
   *consumed = done_in;
   last = acc;
@@ -1104,7 +1267,7 @@ static std::vector<int> multi_devices(uint64_t n) {
     devs.swap(kept);
   }
   // worth it only for inputs of several blocks per device; shards within one batch
-  if (devs.size() < 2 || n < (uint64_t)devs.size() * 4000000ull || n / devs.size() + 1 > kMaxBatch) devs.clear();
+  if (devs.size() < 2 || n < (uint64_t)devs.size() * 4000000ull || n / devs.size() + 1 > kMaxBatchLimit) devs.clear();
   return devs;
 }
 
@@ -1146,7 +1309,7 @@ int bzg_compress_device(const void* d_in, uint64_t n, unsigned flags, bzg_stream
 }
 
 int bzg_seg_map(const void* d_in, uint64_t n, int level, void* stream) {
-  if (level < 1 || level > 9 || (n && !d_in) || n > kMaxBatch) return BZ_PARAM_ERROR;
+  if (level < 1 || level > 9 || (n && !d_in) || n > kMaxBatchLimit) return BZ_PARAM_ERROR;
   if (pool().devices() <= 0) return BZ_CONFIG_ERROR;
   SegState& S = seg_state();
   std::lock_guard<std::mutex> g(S.mu);

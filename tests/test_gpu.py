@@ -14,6 +14,7 @@ from tests import datagen, oracles as O
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def gold(name):
@@ -779,6 +780,49 @@ def test_device_api_split_batches_unaligned_output():
     del d_in, out
     torch.cuda.empty_cache()
     assert got == expected(b"a" * n, 9)
+
+
+_PIPE_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+import bzip2_amd as B
+data = open(sys.argv[2], "rb").read()
+d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+cap = B.bound(len(data))
+out = torch.zeros(cap + 8, dtype=torch.uint8, device="cuda")
+nb, cons, _ = B.compress_device(d_in.data_ptr(), len(data), 9, out.data_ptr() + int(sys.argv[4]), cap)
+torch.cuda.synchronize()
+assert cons == len(data), cons
+open(sys.argv[3], "wb").write(out[int(sys.argv[4]):int(sys.argv[4]) + nb].cpu().numpy().tobytes())
+s = B.last_stats()
+print(s["nblocks"], flush=True)
+"""
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_device_api_pipelined_batches(tmp_path, offset):
+    """A multi-batch device call runs its batches as a pipeline (Engine::compress_pipelined: the
+    MTF / tables / packing of batch j beside the RLE1 and sorts of batch j + 1, two workspace
+    slots).  With the batch limit lowered to 12 MB (BZG_MAX_BATCH, in a child process: the limit
+    is read once per process), 40 MB of text is 4 batches; the stream must equal the
+    reference's and the sequential batches' (BZG_BATCH_PIPE=0), at an aligned and an odd output
+    pointer."""
+    import subprocess
+    import sys
+
+    data = datagen.text(40_000_000, 97)
+    src = tmp_path / "in.bin"
+    src.write_bytes(data)
+    outs = {}
+    for pipe in ("1", "0"):
+        dst = tmp_path / f"out{pipe}.bin"
+        env = dict(os.environ, BZG_MAX_BATCH="12000000", BZG_BATCH_PIPE=pipe)
+        r = subprocess.run([sys.executable, "-c", _PIPE_CHILD, ROOT, str(src), str(dst), str(offset)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[pipe] = dst.read_bytes()
+    assert outs["1"] == outs["0"]
+    assert outs["1"] == expected(data, 9)
 
 
 def test_device_api_continuation_batches():
