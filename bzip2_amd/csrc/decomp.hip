@@ -836,6 +836,11 @@ constexpr uint32_t kSplit2 = 64;
 constexpr uint32_t kMaxSplit2 = 900000 / kSplit2 + 2;
 constexpr uint32_t kWalkT = 256;
 constexpr uint16_t kNil = 0xffffu;
+// The segment pass also keeps the first kWalkKeep bytes of its segment (the emitted byte of a
+// step is in the same Q word as the next row), so the emit pass copies them instead of walking
+// the segment's random Q reads a second time; a segment longer than that (a few percent: the
+// mean is kSplit2) walks on from the row kept with it.
+constexpr uint32_t kWalkKeep = 256;
 
 struct WalkBlock {
   uint32_t n, o, ns, start;
@@ -852,20 +857,33 @@ struct WalkBlock {
 __global__ void __launch_bounds__(kWalkT) k_dec_walk_seg(const uint32_t* __restrict__ qbuf, const uint32_t* __restrict__ slot,
                                                          const DecRes* __restrict__ res, uint32_t nbmax,
                                                          const uint32_t* __restrict__ wgmap, uint32_t* __restrict__ seg_nx,
-                                                         uint32_t* __restrict__ seg_len) {
+                                                         uint32_t* __restrict__ seg_len, uint32_t* __restrict__ keep,
+                                                         uint32_t* __restrict__ keep_row) {
   const uint32_t m = wgmap[blockIdx.x];
   if (m == ~0u) return;
   const uint32_t b = m >> 8, s = (m & 255u) * kWalkT + threadIdx.x;
   const WalkBlock W(res[slot[b]]);
   if (s >= W.ns) return;
   const uint32_t* Q = qbuf + (size_t)b * nbmax;
-  uint32_t j = W.slot_of(s), len = 0;
+  const size_t si = (size_t)b * kMaxSplit2 + s;
+  uint32_t* K = keep + si * (kWalkKeep / 4);
+  uint32_t j = W.slot_of(s), len = 0, acc = 0;
   do {
-    j = Q[j] >> 8;
+    const uint32_t e = Q[j];
+    j = e >> 8;
+    if (len < kWalkKeep) {
+      acc |= (e & 0xffu) << (8 * (len & 3));
+      if ((len & 3) == 3) {
+        K[len >> 2] = acc;
+        acc = 0;
+      }
+    }
     len++;
+    if (len == kWalkKeep) keep_row[si] = j;
   } while (!W.is_split(j));
-  seg_nx[(size_t)b * kMaxSplit2 + s] = W.id_of(j);
-  seg_len[(size_t)b * kMaxSplit2 + s] = len;
+  if (len < kWalkKeep && (len & 3)) K[len >> 2] = acc;
+  seg_nx[si] = W.id_of(j);
+  seg_len[si] = len;
 }
 
 __global__ void __launch_bounds__(1024) k_dec_walk_rank(const uint32_t* __restrict__ slot, const DecRes* __restrict__ res,
@@ -928,6 +946,8 @@ __global__ void __launch_bounds__(kWalkT) k_dec_walk_emit(const uint32_t* __rest
                                                           const uint32_t* __restrict__ seg_off,
                                                           const uint32_t* __restrict__ cyc_in,
                                                           const uint32_t* __restrict__ rbits, uint32_t rperiod,
+                                                          const uint32_t* __restrict__ keep,
+                                                          const uint32_t* __restrict__ keep_row,
                                                           uint8_t* __restrict__ ybuf) {
   const uint32_t m = wgmap[blockIdx.x];
   if (m == ~0u) return;
@@ -935,21 +955,39 @@ __global__ void __launch_bounds__(kWalkT) k_dec_walk_emit(const uint32_t* __rest
   const uint32_t c = slot[b];
   const WalkBlock W(res[c]);
   if (s >= W.ns) return;
-  const uint32_t t0 = seg_off[(size_t)b * kMaxSplit2 + s], cyc = cyc_in[b];
+  const size_t si = (size_t)b * kMaxSplit2 + s;
+  const uint32_t t0 = seg_off[si], cyc = cyc_in[b];
   if (t0 >= cyc) return;
   const bool rnd = res[c].rand != 0;
-  const uint32_t len = min(seg_len[(size_t)b * kMaxSplit2 + s], cyc - t0);
-  const uint32_t* Q = qbuf + (size_t)b * nbmax;
+  const uint32_t len = min(seg_len[si], cyc - t0);
   uint8_t* Y = ybuf + (size_t)c * nbmax;
-  uint32_t j = W.slot_of(s), t = t0;
+  uint32_t t = t0;
   ByteSink sink;
   sink.init(Y + t0);
-  for (uint32_t k = 0; k < len; k++, t++) {
-    const uint32_t e = Q[j];
-    j = e >> 8;
-    uint32_t y = e & 0xffu;
-    if (rnd) y ^= rand_flip(rbits, rperiod, t);
-    sink.put(y);
+  // the bytes the segment pass kept, then (long segments) the walk from the row kept with them
+  const uint32_t* K = keep + si * (kWalkKeep / 4);
+  const uint32_t nk = min(len, kWalkKeep);
+  for (uint32_t k = 0; k < nk; k += 4) {
+    const uint32_t w = K[k >> 2];
+#pragma unroll
+    for (uint32_t x = 0; x < 4; x++) {
+      if (k + x >= nk) break;
+      uint32_t y = (w >> (8 * x)) & 0xffu;
+      if (rnd) y ^= rand_flip(rbits, rperiod, t);
+      sink.put(y);
+      t++;
+    }
+  }
+  if (len > kWalkKeep) {
+    const uint32_t* Q = qbuf + (size_t)b * nbmax;
+    uint32_t j = keep_row[si];
+    for (uint32_t k = kWalkKeep; k < len; k++, t++) {
+      const uint32_t e = Q[j];
+      j = e >> 8;
+      uint32_t y = e & 0xffu;
+      if (rnd) y ^= rand_flip(rbits, rperiod, t);
+      sink.put(y);
+    }
   }
   sink.finish();
 }
@@ -1372,14 +1410,16 @@ int decode_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, uint8_t* d_out,
           uint32_t* seg_nx = ws.u32("dec_segnx", (size_t)R * kMaxSplit2);
           uint32_t* seg_len = ws.u32("dec_seglen", (size_t)R * kMaxSplit2);
           uint32_t* seg_off = ws.u32("dec_segoff", (size_t)R * kMaxSplit2);
+          uint32_t* keep = ws.u32("dec_keep", (size_t)R * kMaxSplit2 * (kWalkKeep / 4));
+          uint32_t* keep_row = ws.u32("dec_keeprow", (size_t)R * kMaxSplit2);
           HIP_OK(hipMemcpyAsync(d_wgmap, wgmap.data(), 4 * wgmap.size(), hipMemcpyHostToDevice, st));
           const uint32_t nwg = (uint32_t)wgmap.size();
-          k_dec_walk_seg<<<nwg, kWalkT, 0, st>>>(qbuf, d_slot, d_res, nbmax, d_wgmap, seg_nx, seg_len);
+          k_dec_walk_seg<<<nwg, kWalkT, 0, st>>>(qbuf, d_slot, d_res, nbmax, d_wgmap, seg_nx, seg_len, keep, keep_row);
           HIP_OK(hipGetLastError());
           k_dec_walk_rank<<<R, 1024, 0, st>>>(d_slot, d_res, seg_nx, seg_len, seg_off, cyc);
           HIP_OK(hipGetLastError());
           k_dec_walk_emit<<<nwg, kWalkT, 0, st>>>(qbuf, d_slot, d_res, nbmax, d_wgmap, seg_len, seg_off, cyc,
-                                                   dw.rbits, dw.rperiod, lbuf);
+                                                   dw.rbits, dw.rperiod, keep, keep_row, lbuf);
           HIP_OK(hipGetLastError());
           k_dec_walk_repeat<<<dim3(64, R), 256, 0, st>>>(d_slot, d_res, nbmax, cyc, dw.rbits, dw.rperiod, lbuf);
           HIP_OK(hipGetLastError());
