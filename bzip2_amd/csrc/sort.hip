@@ -2356,8 +2356,12 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   B.sk2 = ws.u32("sort_sk2", S + 16);
   B.text = r.blk;
   B.units = units;
-  B.dwave = 256;  // S2 -> S3 handoff depth (profiles/r02_dwave_sweep.txt; 64 / 128 measured slower in round 4)
-  B.dwave_tiny = 256;
+  // S2 -> S3 handoff depth (profiles/r02_dwave_sweep.txt; 64 / 128 measured slower in round 4;
+  // BZG_DWAVE / BZG_DWAVE_TINY: A/B knobs)
+  static const uint32_t dwave = (uint32_t)std::max(32ll, env_ll("BZG_DWAVE", 256));
+  static const uint32_t dwave_tiny = (uint32_t)std::max(32ll, env_ll("BZG_DWAVE_TINY", 256));
+  B.dwave = dwave;
+  B.dwave_tiny = dwave_tiny;
   // class lists: a class-c bucket holds more than kClsMax[c-1] rotations
   ClsLists C{};
   size_t ccap[kNCls];
