@@ -556,8 +556,18 @@ struct Engine {
   // non-final batches emit complete blocks and the rest is resubmitted.
   void compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
                 uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last);
+  // Host-call hooks of the pipelined batches: `ends` (ascending input offsets, the last = n)
+  // cuts the batches at the pieces of a staged upload; wait_input(end) makes the caller's
+  // stream wait for the upload of [0, end); on_output(off, len) runs once a batch's coded
+  // bytes [off, off + len) of the output are final (on the back-stage thread, in batch order).
+  struct PipeHooks {
+    std::vector<uint64_t> ends;
+    std::function<void(uint64_t)> wait_input;
+    std::function<void(uint64_t, uint64_t)> on_output;
+  };
   void compress_pipelined(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
-                          uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last);
+                          uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last,
+                          const PipeHooks* hooks = nullptr);
 };
 
 // Largest batch handled in one pass: keeps every block/slot offset in 32 bits.  BZG_MAX_BATCH
@@ -635,7 +645,7 @@ void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_strea
 // the same inputs).
 void Engine::compress_pipelined(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st,
                                 uint8_t* d_out, uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed,
-                                hipStream_t s, bzg_stats& last) {
+                                hipStream_t s, bzg_stats& last, const PipeHooks* hooks) {
   for (int k = 0; k < 2; k++) slot_ev[k].create();
   // The back stages run on the CRC side stream, one stream, no table split.  A process has 4
   // hardware queues (GPU_MAX_HW_QUEUES) and streams share them round-robin in creation order:
@@ -652,6 +662,7 @@ void Engine::compress_pipelined(const uint8_t* d_in, uint64_t n, unsigned flags,
   std::thread backer;  // the back stage of the previous batch
   std::exception_ptr back_err;
   uint64_t done_in = 0, done_out = 0;
+  size_t piece = 0;  // hooks->ends[piece]: the end of the next input piece
   bzg_stats acc{};
   std::mutex mu;
   auto join_back = [&] {
@@ -660,9 +671,13 @@ void Engine::compress_pipelined(const uint8_t* d_in, uint64_t n, unsigned flags,
   };
   try {
     for (uint32_t j = 0;; j++) {
-      const uint64_t left = n - done_in;
-      const bool last_piece = left <= batch_max;
-      const uint64_t take = last_piece ? left : batch_max;
+      // a batch ends at the next piece end (the previous batch's leftover, less than a block,
+      // joins it) or after batch_max bytes
+      uint64_t end = std::min(n, done_in + batch_max);
+      if (hooks && piece < hooks->ends.size() && hooks->ends[piece] <= end) end = hooks->ends[piece++];
+      const bool last_piece = end == n;
+      const uint64_t take = end - done_in;
+      if (hooks && hooks->wait_input) hooks->wait_input(end);
       const int k = (int)(j & 1);
       // slot k was batch j - 2's: its back stage ended before batch j - 1's began (below)
       ctx[k].reset(new BatchCtx);
@@ -702,9 +717,14 @@ void Engine::compress_pipelined(const uint8_t* d_in, uint64_t n, unsigned flags,
             HIP_OK(hipMemcpyAsync(dst, bdst, ob, hipMemcpyDeviceToDevice, bs));
             HIP_OK(hipStreamSynchronize(bs));
           }
-          std::lock_guard<std::mutex> g(mu);
-          add_stats(acc, one);
-          done_out += ob;
+          uint64_t off;
+          {
+            std::lock_guard<std::mutex> g(mu);
+            add_stats(acc, one);
+            off = done_out;
+            done_out += ob;
+          }
+          if (hooks && hooks->on_output) hooks->on_output(off, ob);
         } catch (...) {
           back_err = std::current_exception();
         }
@@ -1375,17 +1395,36 @@ int bzg_find_magics(const void* d_in, uint64_t n, uint64_t* out, uint64_t cap, u
 // segments of one stream (a non-final segment emits its complete blocks and the rest is
 // resubmitted with the next piece, exactly as bzg_compress_device cuts a large input into
 // batches, so the bytes equal one call's); each segment's output goes back from a second thread
-// while the next one is compressed.  Only the first piece's upload and the last segment's
-// download are not overlapped.  A call has a fixed cost of about 5 ms besides its ~50 ms per GB
-// (host synchronisations of the sort passes, narrow late passes), so pieces are few: the first
-// a fifth of the input (its compression covers the upload of the rest, which runs at ~50 GB/s),
-// the rest in one piece when it is at most four times the first (1 GB: 200 + 800 MB), else in
-// pieces doubling in size (h2h timeline: profiles/r05_h2h_*.txt).
+// while the next one is compressed.  The pieces are the batches of Engine::compress_pipelined,
+// so a piece's back stage (MTF, tables, packing) runs beside the next piece's sorts.  Only the
+// first piece's upload and the last piece's back stage and download are not overlapped.  A
+// piece has a fixed cost (host synchronisations of the sort passes, narrow late passes; a
+// 100 MB call takes 7.5 ms against 4.8 ms at the 1 GB rate), so pieces are few: from 640 MiB,
+// 10% (its upload is the only wait), 30% and 40% (each upload is covered by the compression of
+// the piece before, at ~53 GB/s) and a last 20% (short back stage and download); below that,
+// a fifth and the rest (profiles/r06_h2h_plans.txt, r05_h2h_*.txt).
 static constexpr uint64_t kPipeMin = 192ull << 20;  // smaller inputs: one upload, one call, one download
 static constexpr uint64_t kPipeFirst = 96ull << 20;
+static constexpr uint64_t kPipe4 = 640ull << 20;  // from here: four pieces
 
 static std::vector<uint64_t> pipe_pieces(uint64_t n) {
   std::vector<uint64_t> b{0};
+  if (const char* plan = getenv("BZG_H2H_PLAN")) {  // A/B knob: leading piece sizes in MB, "100,300"
+    for (const char* q = plan; *q;) {
+      char* e = nullptr;
+      const unsigned long long mb = strtoull(q, &e, 10);
+      if (e == q) break;
+      if (mb && b.back() + (mb << 20) < n) b.push_back(b.back() + (mb << 20));
+      q = *e ? e + 1 : e;
+    }
+    b.push_back(n);
+    return b;
+  }
+  if (n >= kPipe4) {  // 10% + 30% + 40% + 20% (profiles/r06_h2h_plans.txt)
+    for (uint64_t f : {1u, 4u, 8u}) b.push_back(n / 10 * f);
+    b.push_back(n);
+    return b;
+  }
   uint64_t s = std::max<uint64_t>(kPipeFirst, n / 5);  // (n/4, n/8, 3 pieces: slower, profiles/r05_h2h_split.txt)
   while (n - b.back() > 4 * s) {
     b.push_back(b.back() + s);
@@ -1461,58 +1500,46 @@ static int host_call_pipelined(Engine* e, const uint8_t* src, uint64_t n, unsign
     down.join();
     for (auto& x : ev_in) (void)hipEventDestroy(x);
   };
-  uint64_t done_in = 0, done_out = 0;
-  bzg_stats acc{};
-  int rc = BZ_OK;
-  try {
-    for (size_t j = 0; j < J; j++) {
+  // The pieces are the batches of Engine::compress_pipelined: the front stage of a piece (its
+  // RLE1 and sorts) waits for its upload and runs beside the previous piece's back stage; each
+  // piece's coded bytes go to the download thread as soon as they are packed.
+  Engine::PipeHooks hk;
+  hk.ends.assign(b.begin() + 1, b.end());
+  size_t waited = 0;  // pieces the caller's stream already waits for
+  hk.wait_input = [&](uint64_t end) {
+    while (waited < J && b[waited] < end) {
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return uploaded > j || up_failed; });
-        if (uploaded <= j) throw HipFailure(hipErrorUnknown);
+        cv.wait(g, [&] { return uploaded > waited || up_failed; });
+        if (uploaded <= waited) throw HipFailure(hipErrorUnknown);
       }
-      HIP_OK(hipStreamWaitEvent(e->stream, ev_in[j], 0));
-      const bool last = j + 1 == J;
-      const double c0 = dbg ? ms() : 0.0;
-      uint64_t ob = 0, cons = 0;
-      bzg_stats one{};
-      // the output is coded behind the previous segments' bytes (Engine::compress stages a
-      // misaligned destination itself)
-      e->compress(din + done_in, b[j + 1] - done_in, last ? flags : 0u, st, dout + done_out, cap - done_out, &ob,
-                  &cons, e->stream, one);
-      acc.rle1_ms += one.rle1_ms;
-      acc.bwt_ms += one.bwt_ms;
-      acc.mtf_ms += one.mtf_ms;
-      acc.code_ms += one.code_ms;
-      acc.total_ms += one.total_ms;
-      acc.nblocks += one.nblocks;
-      acc.sort_iterations = std::max(acc.sort_iterations, one.sort_iterations);
-      acc.rle_bytes += one.rle_bytes;
-      acc.sort_unsorted += one.sort_unsorted;
-      acc.mtf_symbols += one.mtf_symbols;
-      acc.a5_roots += one.a5_roots;
-      acc.a5_host += one.a5_host;
-      if (dbg) fprintf(stderr, "[bzg h2h] piece %zu: compress %.2f .. %.2f ms (%llu B in, %llu B out)\n", j, c0, ms(),
-                       (unsigned long long)cons, (unsigned long long)ob);
-      if (done_out + ob > dst_cap) {
-        rc = BZ_OUTBUFF_FULL;
-        break;
-      }
-      {
-        std::lock_guard<std::mutex> g(mu);
-        downs.push_back(Down{done_out, ob});
-      }
-      cv.notify_all();
-      done_in += cons;
-      done_out += ob;
+      HIP_OK(hipStreamWaitEvent(e->stream, ev_in[waited], 0));
+      if (dbg) fprintf(stderr, "[bzg h2h] piece %zu: compression may start %.2f ms\n", waited, ms());
+      waited++;
     }
+  };
+  bool overflow = false;
+  hk.on_output = [&](uint64_t off, uint64_t len) {
+    if (dbg) fprintf(stderr, "[bzg h2h] coded [%llu, +%llu) ready %.2f ms\n", (unsigned long long)off,
+                     (unsigned long long)len, ms());
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (off + len > dst_cap) overflow = true;
+      else downs.push_back(Down{off, len});
+    }
+    cv.notify_all();
+  };
+  uint64_t done_in = 0, done_out = 0;
+  bzg_stats acc{};
+  try {
+    e->compress_pipelined(din, n, flags, st, dout, cap, &done_out, &done_in, e->stream, acc, &hk);
   } catch (...) {
     finish_threads();
     throw;
   }
   finish_threads();
   publish_stats(acc);
-  if (rc != BZ_OK) return rc;
+  if (overflow || done_out > dst_cap) return BZ_OUTBUFF_FULL;
   if (up_failed || down_failed) throw HipFailure(hipErrorUnknown);
   *dst_len = done_out;
   if (consumed) *consumed = done_in;

@@ -664,12 +664,16 @@ def test_multi_device_host_path(monkeypatch, level):
     assert B.buff_to_buff_compress(txt, level) == expected(txt, level)
 
 
-def test_host_pipelined_equals_device():
+@pytest.mark.parametrize("plan", [None, "100,100", "64,64,64"])
+def test_host_pipelined_equals_device(monkeypatch, plan):
     """BZ2_bzBuffToBuffCompress of a large host buffer runs as a pipeline (engine.hip
-    host_call_pipelined: uploads, segment compressions and downloads overlapped); its bytes
-    equal one device-resident call on the same input, and a short destination gives
-    BZ_OUTBUFF_FULL."""
+    host_call_pipelined: piece uploads, the pieces' front and back stages over two workspace
+    slots, downloads overlapped); its bytes equal one device-resident call on the same input,
+    for the default piece plan and for 3 and 4 pieces (BZG_H2H_PLAN), and a short destination
+    gives BZ_OUTBUFF_FULL."""
     torch = pytest.importorskip("torch")
+    if plan:
+        monkeypatch.setenv("BZG_H2H_PLAN", plan)
     data = datagen.text(300_000_000, 404) + datagen.random_bytes(20_000_000, 5) + b"z" * 30_000_000
     got = B.buff_to_buff_compress(data, 9)
     d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
