@@ -11,7 +11,7 @@ import sys
 
 
 # kernels whose global reads are coalesced sequential sweeps of 16 B per lane
-STREAMING = {"k_rle_count", "k_emit", "k_in_use", "k_block_crc", "k_tile_reduce", "k_find_magics"}
+STREAMING = {"k_rle_count", "k_emit", "k_in_use", "k_block_crc", "k_tile_reduce", "k_scan_1p", "k_find_magics"}
 
 
 def per_kernel(path):
