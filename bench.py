@@ -571,12 +571,15 @@ def host_to_host(data, a, cap):
         assert rc == B.BZ_OK, rc
 
     h2h_call()  # warm-up (host staging buffers)
-    t1 = time.perf_counter()
-    h2h_call()
-    h2h = time.perf_counter() - t1
+    times = []
+    for _ in range(3):  # one call is ~60 ms; PCIe and host-copy timing varies from call to call
+        t1 = time.perf_counter()
+        h2h_call()
+        times.append(time.perf_counter() - t1)
+    h2h = min(times)
     return {"value": round(a.bytes / h2h / 1e6, 2), "unit": "MB/s", "ms": round(h2h * 1e3, 3),
-            "out_bytes": int(dl.value),
-            "api": "BZ2_bzBuffToBuffCompress, pageable host buffers (H2D + kernels + D2H)"}
+            "ms_calls": [round(t * 1e3, 3) for t in times], "out_bytes": int(dl.value),
+            "api": "BZ2_bzBuffToBuffCompress, pageable host buffers (H2D + kernels + D2H), best of 3 warm calls"}
 
 
 def cpu_model() -> str:

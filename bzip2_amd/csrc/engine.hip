@@ -40,12 +40,12 @@ Workspace::~Workspace() {
 constexpr uint32_t kMboxWords = 8192;
 struct MboxPieces {
   const uint32_t* src[4];
-  uint32_t nw[4], at[4];
+  uint32_t nw[4], at[4], stride[4];
 };
 __global__ void __launch_bounds__(256) k_mbox(MboxPieces P, uint32_t* dst, uint32_t* flag, uint32_t seq) {
 #pragma unroll
   for (int k = 0; k < 4; k++)
-    for (uint32_t i = threadIdx.x; i < P.nw[k]; i += 256) dst[P.at[k] + i] = P.src[k][i];
+    for (uint32_t i = threadIdx.x; i < P.nw[k]; i += 256) dst[P.at[k] + i] = P.src[k][(size_t)i * P.stride[k]];
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -67,12 +67,23 @@ void Workspace::read_small(std::initializer_list<SmallRead> reads, hipStream_t s
       P.src[k] = static_cast<const uint32_t*>(r.src);
       P.nw[k] = (uint32_t)nw;
       P.at[k] = total;
+      P.stride[k] = std::max(r.stride, 1u);
     }
     total += (uint32_t)std::min<size_t>(nw, kMboxWords + 1);
     k++;
   }
+  // (a strided piece's words one copy each)
+  auto copy_async = [&](const SmallRead& r) {
+    if (r.stride <= 1) {
+      HIP_OK(hipMemcpyAsync(r.dst, r.src, r.bytes, hipMemcpyDeviceToHost, st));
+      return;
+    }
+    for (size_t i = 0; i < r.bytes / 4; i++)
+      HIP_OK(hipMemcpyAsync(static_cast<uint32_t*>(r.dst) + i, static_cast<const uint32_t*>(r.src) + i * r.stride, 4,
+                            hipMemcpyDeviceToHost, st));
+  };
   if (!fast) {
-    for (const SmallRead& r : reads) HIP_OK(hipMemcpyAsync(r.dst, r.src, r.bytes, hipMemcpyDeviceToHost, st));
+    for (const SmallRead& r : reads) copy_async(r);
     HIP_OK(hipStreamSynchronize(st));
     return;
   }
@@ -99,7 +110,8 @@ void Workspace::read_small(std::initializer_list<SmallRead> reads, hipStream_t s
       const hipError_t e = hipStreamQuery(st);
       if (e == hipSuccess) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
-        for (const SmallRead& r : reads) HIP_OK(hipMemcpy(r.dst, r.src, r.bytes, hipMemcpyDeviceToHost));  // (not expected)
+        for (const SmallRead& r : reads) copy_async(r);  // (not expected)
+        HIP_OK(hipStreamSynchronize(st));
         return;
       }
       if (e != hipErrorNotReady) HIP_OK(e);
@@ -149,7 +161,7 @@ void Workspace::release_all() {
   crc_ = xp2_ = nullptr;
 }
 
-void* Workspace::get(const std::string& name, size_t bytes) {
+void* Workspace::get(const std::string& name, size_t bytes, bool zero) {
   bytes = std::max<size_t>(bytes, 64);
   Buf& b = bufs_[name];
   if (b.bytes >= bytes) return b.p;
@@ -173,6 +185,7 @@ void* Workspace::get(const std::string& name, size_t bytes) {
   b.bytes = grow;
   b.async = async;
   total_ += grow;
+  if (zero) HIP_OK(stream_ ? hipMemsetAsync(p, 0, grow, stream_) : hipMemset(p, 0, grow));
   return b.p;
 }
 

@@ -1205,7 +1205,7 @@ void rle1_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, bool 
   uint32_t* tmax = ws.u32("rle_tmax", tiles + 64);
   uint32_t* tsum = ws.u32("rle_tsum", tiles + 64);
   uint32_t* tinfo = ws.u32("rle_tinfo", tiles + 64);
-  uint32_t* scratch = ws.u32("rle_scan", scan_scratch_words(tiles) + 64);
+  uint32_t* scratch = ws.u32z("rle_scan", scan_scratch_words(tiles) + 64);
   uint32_t* mtot = ws.u32("rle_m", 16);
   uint8_t* blk = ws.u8("blk", mcap + 64);
   uint32_t* cbits = ws.u32("rle_cbits", mcap / 32 + 64);
@@ -1307,7 +1307,7 @@ void seg_map_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, hipStream_t s
   uint32_t* tmax = ws.u32("seg_tmax", tiles + 64);
   uint32_t* tsum = ws.u32("seg_tsum", tiles + 64);
   uint32_t* tinfo = ws.u32("seg_tinfo", tiles + 64);
-  uint32_t* scratch = ws.u32("seg_scan", scan_scratch_words(tiles) + 64);
+  uint32_t* scratch = ws.u32z("seg_scan", scan_scratch_words(tiles) + 64);
   uint32_t* mtot = ws.u32("seg_m", 16);
   uint32_t* cbits = ws.u32("seg_cbits", mcap / 32 + 64);
   k_rle_count<<<ceil_div64(tiles, kRleG), kT, 0, st>>>(d_in, n, tiles, tmax, tinfo);

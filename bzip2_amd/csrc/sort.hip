@@ -59,8 +59,8 @@ struct SortOut {
   uint32_t* rank0;   // slot of rotation 0 relative to its unit
   Grp* deep;         // groups left for the doubling fallback
   uint32_t* n_deep;
-  Grp* tdeep;        // k_tiny<2>: the deep pair of bucket i at [i] (zeroed before; k_deep_compact appends them)
-  Grp* dslot;        // classes 9..32: group i's deep groups at [i * dm, + dnum[i]) (k_deep_compact2 appends them)
+  Grp* tdeep;        // k_tiny<2>: the deep pair of bucket i at [i] (size 0: none; k_deep_compact_all appends them)
+  Grp* dslot;        // classes 9..32: group i's deep groups at [i * dm, + dnum[i]) (k_deep_compact_all appends them)
   uint32_t* dnum;
   uint32_t dm;
   unsigned long long* dbg;  // BZG_DEBUG counters (null otherwise)
@@ -197,9 +197,21 @@ __global__ void k_init_units(const Unit* __restrict__ units, uint32_t nu, SortBu
   }
 }
 
-__global__ void k_group_tiles(const Grp* __restrict__ L, uint32_t n, uint32_t* __restrict__ cnt) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n) cnt[g] = ceil_div(L[g].size, kDTile);
+// One launch for both lists of an S1 pass: the tiled groups' tile counts (for the tile prefix
+// TP) at [0, n7), then, for the packed groups, their sizes (for the element prefix P) and
+// each group's unit beside it, so that a packed tile reads its groups and their units in one
+// round trip instead of two dependent ones.
+__global__ void k_group_prep(const Grp* __restrict__ L7, uint32_t n7, uint32_t* __restrict__ TP,
+                             const Grp* __restrict__ L6, uint32_t n6, const Unit* __restrict__ units,
+                             uint32_t* __restrict__ sizes, Unit* __restrict__ gunits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n7) {
+    TP[i] = ceil_div(L7[i].size, kDTile);
+  } else if (i - n7 < n6) {
+    const Grp gr = L6[i - n7];
+    sizes[i - n7] = gr.size;
+    gunits[i - n7] = units[gr.unit];
+  }
 }
 
 // One record per S1 tile (TP: exclusive scan of the groups' tile counts): the tile's group,
@@ -457,7 +469,7 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
       if (flag[kk[i] >> 24] & 2u) dstk[pos[i]] = kk[i] << 8;
     }
   }
-  // a bucket of one: this rotation is ordered (its primary-SA copy is made by k_s1_single,
+  // a bucket of one: this rotation is ordered (its primary-SA copy is made by s1_single,
   // since other workgroups may still read the primary SA in this pass)
 #pragma unroll
   for (int i = 0; i < (int)kPerT; i++)
@@ -482,11 +494,14 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
   }
 }
 
-__global__ void __launch_bounds__(kT) k_s1_single(const Grp* __restrict__ G, SortBufs B, const uint32_t* __restrict__ tot) {
+// The primary-SA copies of the buckets of one that a tiled pass left in the alternate SA
+// (one workgroup per tiled group; the launch is shared with s1s_emit, see k_s1_tail).
+__device__ __forceinline__ void s1_single(const Grp* __restrict__ G, SortBufs B, const uint32_t* __restrict__ tot,
+                                          uint32_t g) {
   __shared__ uint32_t sh[kT / 64];
-  const Grp gr = G[blockIdx.x];
+  const Grp gr = G[g];
   if ((gr.flags & kGrpIdent) || (gr.flags & kGrpAlt)) return;  // pass wrote the primary SA
-  const uint32_t total = tot[(size_t)blockIdx.x * 256 + threadIdx.x];
+  const uint32_t total = tot[(size_t)g * 256 + threadIdx.x];
   const uint32_t incl = block_incl_sum(total, sh, (uint32_t*)nullptr);
   const uint32_t s = gr.start + incl - total;
   if (total == 1) B.sa[s] = B.sa2[s];
@@ -502,25 +517,20 @@ __global__ void __launch_bounds__(kT) k_s1_single(const Grp* __restrict__ G, Sor
 constexpr uint32_t kSGrp = kSG / (kBig + 1) + 2;
 
 // tile index of item i = P[i] / kSG; mark the first item of each tile and one past its last.
-__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_t* __restrict__ first,
-                             uint32_t* __restrict__ last) {
+// Groups hold at most kSG rotations, so every window of kSG prefix positions holds a group
+// start but the last window(s) after the last start: those tiles (up to ceil(total / kSG),
+// total = *ptotal) are marked empty here.
+__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, const uint32_t* __restrict__ ptotal,
+                             uint32_t* __restrict__ first, uint32_t* __restrict__ last) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t t = P[i] / kSG;
   if (i == 0 || P[i - 1] / kSG != t) first[t] = i;
   if (i == n - 1 || P[i + 1] / kSG != t) last[t] = i + 1;
+  if (i == n - 1)
+    for (uint32_t e = t + 1; e < ceil_div(*ptotal, kSG); e++) first[e] = 0xffffffffu;
 }
 
-// Group sizes (for the tile prefix) and each group's unit beside it, so that a packed tile
-// reads its groups and their units in one round trip instead of two dependent ones.
-__global__ void k_group_sizes(const Grp* __restrict__ L, uint32_t n, const Unit* __restrict__ units,
-                              uint32_t* __restrict__ sizes, Unit* __restrict__ gunits) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n) return;
-  const Grp gr = L[g];
-  sizes[g] = gr.size;
-  gunits[g] = units[gr.unit];
-}
 
 // packed kernels: 512 threads x 8 elements (a tile holds < 2 kSG rotations; kSG on average,
 // so the element loops stop at the tile's last 512-element round)
@@ -592,7 +602,7 @@ struct S1sOwner {
 // the tile's buckets of two or more rotations as records (group:5 | start:13 | size:14,
 // tile-relative) in the tile's own part of `rec` (it starts at half the tile's first element
 // offset: a tile of n rotations has at most n / 2 such buckets), with the per-class counts for
-// the class-major scan.  k_s1s_emit turns the records into class-list entries.
+// the class-major scan.  s1s_emit (k_s1_tail) turns the records into class-list entries.
 // Element rounds past the tile's size are skipped (uniform branches); loads are issued for
 // all rounds before their values are used, from addresses selected without branches.
 __device__ __forceinline__ uint32_t rec_pack(uint32_t j, uint32_t start, uint32_t size) {
@@ -740,12 +750,23 @@ __global__ void __launch_bounds__(kTS) BZG_SGPR_LIMIT k_s1s_pass(const Grp* __re
 }
 
 // The records of k_s1s_pass into the class lists (class-major offsets from cscan) or the
-// deep list; one wave per tile.
-__global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, const uint32_t* __restrict__ first,
-                                                const uint32_t* __restrict__ last, const uint32_t* __restrict__ P,
-                                                uint32_t nT, SortOut O, const uint32_t* __restrict__ rec,
-                                                const uint32_t* __restrict__ nrec, const uint32_t* __restrict__ cscan,
-                                                uint32_t nTot, uint32_t ibase, ClsLists C) {
+// deep list; one wave per tile (workgroup wg of the emission).
+struct S1sEmitArgs {
+  const Grp* SG;
+  const uint32_t *first, *last, *P;
+  uint32_t nT;
+  const uint32_t *rec, *nrec;
+  uint32_t ibase;
+};
+__device__ __forceinline__ void s1s_emit(const S1sEmitArgs& A, SortOut O, const uint32_t* __restrict__ cscan,
+                                         uint32_t nTot, const ClsLists& C, uint32_t wg) {
+  const Grp* __restrict__ SG = A.SG;
+  const uint32_t* __restrict__ first = A.first;
+  const uint32_t* __restrict__ last = A.last;
+  const uint32_t* __restrict__ P = A.P;
+  const uint32_t* __restrict__ rec = A.rec;
+  const uint32_t* __restrict__ nrec = A.nrec;
+  const uint32_t nT = A.nT, ibase = A.ibase;
   __shared__ uint32_t Wg[kT / 64][4][kSGrp];
   __shared__ uint32_t Wcc[kT / 64][kNCls];
   const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
@@ -754,7 +775,7 @@ __global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, con
   uint32_t* gfl = Wg[wv][2];
   uint32_t* gunit = Wg[wv][3];
   uint32_t* cc = Wcc[wv];
-  const uint32_t t = blockIdx.x * (kT / 64) + wv;
+  const uint32_t t = wg * (kT / 64) + wv;
   if (t >= nT) return;
   const uint32_t i0 = first[t];
   if (i0 == 0xffffffffu) return;
@@ -787,13 +808,15 @@ __global__ void __launch_bounds__(kT) k_s1s_emit(const Grp* __restrict__ SG, con
   }
 }
 
-// out[c] = start of class c in the class-major scan (c < kNCls), out[kNCls] = total.
-__global__ void k_cls_bounds(const uint32_t* __restrict__ cscan, uint32_t nTot, const uint32_t* __restrict__ total,
-                             uint32_t* __restrict__ out) {
-  const uint32_t c = threadIdx.x;
-  if (c < (uint32_t)kNCls) out[c] = cscan[(size_t)c * nTot];
-  if (c == (uint32_t)kNCls) out[c] = *total;
+// The end of an S1 pass in one launch: workgroups [0, n7) make the tiled groups' primary-SA
+// copies (s1_single), the rest turn the packed tiles' records into list entries (s1s_emit).
+__global__ void __launch_bounds__(kT) k_s1_tail(const Grp* __restrict__ G7, uint32_t n7, SortBufs B,
+                                               const uint32_t* __restrict__ tot, S1sEmitArgs A, SortOut O,
+                                               const uint32_t* __restrict__ cscan, uint32_t nTot, ClsLists C) {
+  if (blockIdx.x < n7) s1_single(G7, B, tot, blockIdx.x);
+  else s1s_emit(A, O, cscan, nTot, C, blockIdx.x - n7);
 }
+
 
 // ---------------------------------------------------------------- S2
 
@@ -893,6 +916,8 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
   if (!__ballot(act)) return;
   if constexpr (kW == 8) {
     if (bi < n_tiny && el == 0) O.dnum[bi] = 0;  // (the deep branch counts the bucket's deep groups)
+  } else {
+    if (bi < n_tiny && el == 0) O.tdeep[bi] = Grp{0, 0, 0, 0};  // (the deep branch writes the pair's group)
   }
   Unit U{0, 1, 0, 1};
   if (act) U = B.units[unit];
@@ -1079,11 +1104,11 @@ __global__ void __launch_bounds__(kT) k_tiny(const Grp* __restrict__ tiny, uint3
 // one atomic per workgroup of 4096 entries (a single-address atomic per wave, 1.5 M of them
 // for long repeats, serialised to tens of ms).
 constexpr uint32_t kCompactPer = 16;
-__global__ void __launch_bounds__(kT) k_deep_compact(const Grp* __restrict__ in, uint32_t n, Grp* __restrict__ out,
-                                                     uint32_t* __restrict__ cnt) {
+__device__ __forceinline__ void deep_compact1(const Grp* __restrict__ in, uint32_t n, Grp* __restrict__ out,
+                                              uint32_t* __restrict__ cnt, uint32_t wg) {
   __shared__ uint32_t sh[kT / 64];
   __shared__ uint32_t base;
-  const uint32_t i0 = (blockIdx.x * kT + threadIdx.x) * kCompactPer;
+  const uint32_t i0 = (wg * kT + threadIdx.x) * kCompactPer;
   Grp g[kCompactPer];
   uint32_t k = 0;
 #pragma unroll
@@ -1103,12 +1128,12 @@ __global__ void __launch_bounds__(kT) k_deep_compact(const Grp* __restrict__ in,
 
 // Deep groups in per-item slots ([i * m, i * m + num[i])) appended to the deep list, one
 // atomic per workgroup.
-__global__ void __launch_bounds__(kT) k_deep_compact2(const Grp* __restrict__ slot, const uint32_t* __restrict__ num,
-                                                      uint32_t n, uint32_t m, Grp* __restrict__ out,
-                                                      uint32_t* __restrict__ cnt) {
+__device__ __forceinline__ void deep_compact2(const Grp* __restrict__ slot, const uint32_t* __restrict__ num,
+                                              uint32_t n, uint32_t m, Grp* __restrict__ out,
+                                              uint32_t* __restrict__ cnt, uint32_t wg) {
   __shared__ uint32_t sh[kT / 64];
   __shared__ uint32_t base;
-  const uint32_t i0 = (blockIdx.x * kT + threadIdx.x) * kCompactPer;
+  const uint32_t i0 = (wg * kT + threadIdx.x) * kCompactPer;
   uint32_t c[kCompactPer], k = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kCompactPer; j++) {
@@ -1122,6 +1147,26 @@ __global__ void __launch_bounds__(kT) k_deep_compact2(const Grp* __restrict__ sl
   uint32_t p = base + ex;
   for (uint32_t j = 0; j < kCompactPer; j++)
     for (uint32_t x = 0; x < c[j]; x++) out[p++] = slot[(size_t)(i0 + j) * m + x];
+}
+// The deep groups of one S2 iteration's small classes in one launch: the pair buckets'
+// slots (entries of size 0: none; DeepSrc::slot null) and the per-item slots of k_tiny<8> and
+// classes 9..32, each source taking its own range of workgroups.
+struct DeepSrc {
+  const Grp* slot;       // per-item slots [i * m, i * m + num[i]); null: `in` (size 0 = none)
+  const Grp* in;
+  const uint32_t* num;
+  uint32_t n, m, wg0;    // items, slots per item, first workgroup
+};
+struct DeepSrcs {
+  DeepSrc s[4];
+  uint32_t ns;
+};
+__global__ void __launch_bounds__(kT) k_deep_compact_all(DeepSrcs D, Grp* __restrict__ out, uint32_t* __restrict__ cnt) {
+  int k = 0;
+  while (k + 1 < (int)D.ns && blockIdx.x >= D.s[k + 1].wg0) k++;
+  const DeepSrc& S = D.s[k];
+  if (S.slot) deep_compact2(S.slot, S.num, S.n, S.m, out, cnt, blockIdx.x - S.wg0);
+  else deep_compact1(S.in, S.n, out, cnt, blockIdx.x - S.wg0);
 }
 
 // ---- buckets of 9..256 rotations: one segment of kSeg lanes x kPer registers per bucket
@@ -1723,7 +1768,12 @@ __global__ void __launch_bounds__(kT) BZG_SGPR_LIMIT k_bsort(const Grp* __restri
       done[r] = valid && !tied;
       any_tied |= tied;
     }
-    if (__ballot(any_tied) == 0) break;
+    if (__ballot(any_tied) == 0) {
+      if constexpr (kEmit) {  // no records: the group's class counts are 0
+        if (lane < (uint32_t)kS2Cls) E.ccnt[(size_t)lane * E.total + E.gbase + bi] = 0u;
+      }
+      break;
+    }
     depth += round == 0 ? KeyFmt<kE>::kC1 : KeyFmt<kE>::kC2;  // tied runs are equal to this depth
     if constexpr (kSeg == 64 && kPer <= 2) {  // (kPer 4: the registers would cost a wave per SIMD)
       bool split = false;  // the group is no longer one run
@@ -1816,8 +1866,9 @@ struct S2Lists {
   uint32_t gb[5];
 };
 __global__ void k_s2_emit(S2Lists Ls, const uint32_t* __restrict__ rec, const uint32_t* __restrict__ cscan,
-                          uint32_t total, ClsLists N) {
+                          uint32_t total, ClsLists N, uint32_t* __restrict__ zero2) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < 2) zero2[g] = 0;  // k_split_pairs' output counters, for the next iteration
   if (g >= total) return;
   uint32_t n = 0, pos[kS2Cls];
 #pragma unroll
@@ -1842,11 +1893,6 @@ __global__ void k_s2_emit(S2Lists Ls, const uint32_t* __restrict__ rec, const ui
   }
 }
 
-// out[c] = size of class c in a class-major scan of the S2 classes (c < kS2Cls).
-__global__ void k_s2_bounds(const uint32_t* __restrict__ cscan, uint32_t total, uint32_t* __restrict__ out) {
-  const uint32_t c = threadIdx.x;
-  if (c < (uint32_t)kS2Cls) out[c] = cscan[(size_t)(c + 1) * total] - cscan[(size_t)c * total];
-}
 
 // ---------------------------------------------------------------- S2 lists in block order
 // The S1 passes append S2 groups pass after pass, each pass sweeping every block, so a list
@@ -2383,8 +2429,8 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     HIP_OK(hipMemsetAsync(O.dbg, 0, 1024, st));
   }
   // counters: 0..8 class counts (init), 16 class-major scan total, 17 tiles, 18 packed total,
-  // 19 n_deep, 20 min depth, 21 / 22 deep pairs, 24..30 S2 class sizes, 32 / 33 pair splits,
-  // 40..49 class bounds + total
+  // 19 n_deep, 20 min depth, 21 / 22 deep pairs, 32 / 33 pair splits (hc 24..30: the S2 class
+  // sizes read back)
   uint32_t* cnt = ws.u32("sort_cnt", 64);  // counters: see below; 24..29 S2 class sizes
   O.n_deep = cnt + 19;
   const size_t max_tiles = S / kDTile + ccap[kClsTiled] + 16;
@@ -2402,7 +2448,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
   uint32_t* nrec = ws.u32("sort_nrec", max_ptiles);
   uint32_t* srec = ws.u32("sort_rec", S + 64);  // bucket records of the packed passes and of S2
   uint32_t* scratch =
-      ws.u32("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[kClsPacked])) + 64);
+      ws.u32z("sort_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(kNCls * max_tot, max_tiles), ccap[kClsPacked])) + 64);
   uint32_t hc[64];
   auto read_counters = [&]() { ws.read_small(hc, cnt, sizeof(hc), st); };
   auto grid = [](uint64_t n) { return (unsigned)std::max<uint64_t>(1, ceil_div64(n, kT)); };
@@ -2437,19 +2483,15 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     ++passes;
     check_list(cur6, n6, "S1 packed", passes, 6);
     check_list(cur7, n7, "S1 tiled", passes, 7);
+    k_group_prep<<<grid((uint64_t)n7 + n6), kT, 0, st>>>(cur7, n7, TP, cur6, n6, units, P, gunits);
+    HIP_OK(hipGetLastError());
     if (n7) {
-      k_group_tiles<<<grid(n7), kT, 0, st>>>(cur7, n7, TP);
-      HIP_OK(hipGetLastError());
       scan_u32(ScanOp::Sum, true, TP, TP, n7, cnt + 17, scratch, st);
       k_tile_owner<<<n7, 64, 0, st>>>(cur7, n7, TP, units, TR);
       HIP_OK(hipGetLastError());
     }
-    if (n6) {
-      k_group_sizes<<<grid(n6), kT, 0, st>>>(cur6, n6, units, P, gunits);
-      HIP_OK(hipGetLastError());
-      scan_u32(ScanOp::Sum, true, P, P, n6, cnt + 18, scratch, st);
-    }
-    read_counters();
+    if (n6) scan_u32(ScanOp::Sum, true, P, P, n6, cnt + 18, scratch, st);
+    ws.read_small(hc + 17, cnt + 17, 8, st);
     const uint32_t ntl = n7 ? hc[17] : 0;
     const uint32_t nT = n6 ? ceil_div(hc[18], kSG) : 0;
     // class-major scan over the tiled groups and the packed tiles (tile t at index n7 + t)
@@ -2460,8 +2502,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       s1_elems += n6 ? hc[18] : 0;
     }
     if (nT) {
-      HIP_OK(hipMemsetAsync(first, 0xff, (size_t)nT * 4, st));
-      k_tile_first<<<grid(n6), kT, 0, st>>>(P, n6, first, last);
+      k_tile_first<<<grid(n6), kT, 0, st>>>(P, n6, cnt + 18, first, last);
       HIP_OK(hipGetLastError());
       k_s1s_pass<<<nT, kTS, 0, st>>>(cur6, gunits, first, last, P, B, O, srec, nrec, ccnt, nTot, n7);
       HIP_OK(hipGetLastError());
@@ -2473,8 +2514,6 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       HIP_OK(hipGetLastError());
     }
     scan_u32(ScanOp::Sum, true, ccnt, ccnt, (size_t)kNCls * nTot, cnt + 16, scratch, st);
-    k_cls_bounds<<<1, 64, 0, st>>>(ccnt, nTot, cnt + 16, cnt + 40);
-    HIP_OK(hipGetLastError());
     ClsLists Cp = C;
     for (int c = 0; c < kS2Cls; c++) Cp.base[c] = ncls[c];
     Cp.l[kClsPacked] = nxt6;
@@ -2483,17 +2522,16 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     if (n7) {
       k_s1_scatter<<<ntl, kT, 0, st>>>(TR, B, O, hist, tot, ccnt, nTot, Cp);
       HIP_OK(hipGetLastError());
-      k_s1_single<<<n7, kT, 0, st>>>(cur7, B, tot);
-      HIP_OK(hipGetLastError());
     }
-    if (nT) {
-      k_s1s_emit<<<ceil_div(nT, kT / 64), kT, 0, st>>>(cur6, first, last, P, nT, O, srec, nrec, ccnt, nTot, n7, Cp);
-      HIP_OK(hipGetLastError());
-    }
-    read_counters();
-    for (int c = 0; c < kS2Cls; c++) ncls[c] += hc[40 + c + 1] - hc[40 + c];
-    n6 = hc[40 + kClsPacked + 1] - hc[40 + kClsPacked];
-    n7 = hc[40 + kClsTiled + 1] - hc[40 + kClsTiled];
+    k_s1_tail<<<n7 + ceil_div(nT, kT / 64), kT, 0, st>>>(cur7, n7, B, tot, S1sEmitArgs{cur6, first, last, P, nT, srec, nrec, n7},
+                                                         O, ccnt, nTot, Cp);
+    HIP_OK(hipGetLastError());
+    // the class bounds of the class-major scan: its entries at c * nTot (class starts) and its total
+    uint32_t bnd[kNCls + 1];
+    ws.read_small({{bnd, ccnt, 4ull * kNCls, nTot}, {bnd + kNCls, cnt + 16, 4}}, st);
+    for (int c = 0; c < kS2Cls; c++) ncls[c] += bnd[c + 1] - bnd[c];
+    n6 = bnd[kClsPacked + 1] - bnd[kClsPacked];
+    n7 = bnd[kClsTiled + 1] - bnd[kClsTiled];
     std::swap(cur6, nxt6);
     std::swap(cur7, nxt7);
   }
@@ -2535,7 +2573,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
     Grp* tiny2 = ws.typed<Grp>("sort_tiny2", ccap[0]);
     Grp* tiny8 = ws.typed<Grp>("sort_tiny8", ccap[0]);
     uint32_t* ccnt2 = ws.u32("sort_s2cnt", kS2Cls * max_s2 + 16);
-    uint32_t* scratch2 = ws.u32("sort_s2scan", scan_scratch_words(kS2Cls * max_s2 + 16) + 64);
+    uint32_t* scratch2 = ws.u32z("sort_s2scan", scan_scratch_words(kS2Cls * max_s2 + 16) + 64);
     int s2_iters = 0;
     for (;;) {
       ++s2_iters;
@@ -2543,16 +2581,22 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         fprintf(stderr, "[bzg sort S2] iter %d: 2-8:%u 9-16:%u 17-32:%u 33-64:%u 65-128:%u 129-256:%u 257-512:%u\n",
                 s2_iters, ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5], ncls[6]);
       for (int c = 0; c < kS2Cls; c++) check_list(C.l[c], ncls[c], "S2", s2_iters, c);
+      // the small classes' deep groups, appended by one k_deep_compact_all after all of them
+      DeepSrcs D{};
+      uint32_t dwg = 0;
+      auto add_deep = [&](const Grp* slot, const Grp* in, const uint32_t* num, uint32_t n, uint32_t m) {
+        D.s[D.ns++] = DeepSrc{slot, in, num, n, m, dwg};
+        dwg += ceil_div(n, kT * kCompactPer);
+      };
       if (ncls[0]) {
-        HIP_OK(hipMemsetAsync(cnt + 32, 0, 8, st));
+        // (cnt + 32, + 33: zero at the start and after every iteration's k_s2_emit)
         k_split_pairs<<<ceil_div(ncls[0], kT * kSplitPer), kT, 0, st>>>(C.l[0], ncls[0], tiny2, tiny8, cnt + 32);
         HIP_OK(hipGetLastError());
         uint32_t hn[2];
         ws.read_small(hn, cnt + 32, 8, st);
         if (hn[0]) {
-          HIP_OK(hipMemsetAsync(O.tdeep, 0, sizeof(Grp) * hn[0], st));
           k_tiny<2><<<ceil_div(hn[0], 32 * (kT / 64)), kT, 0, st>>>(tiny2, hn[0], B, O);
-          k_deep_compact<<<ceil_div(hn[0], kT * kCompactPer), kT, 0, st>>>(O.tdeep, hn[0], O.deep, O.n_deep);
+          add_deep(nullptr, O.tdeep, nullptr, hn[0], 0);
         }
         if (hn[1]) {
           SortOut O8 = O;
@@ -2560,8 +2604,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
           O8.dslot = ws.typed<Grp>("sort_dslot8", (size_t)hn[1] * 4);
           O8.dnum = ws.u32("sort_dnum8", hn[1]);
           k_tiny<8><<<ceil_div(hn[1], 8 * (kT / 64)), kT, 0, st>>>(tiny8, hn[1], B, O8);
-          k_deep_compact2<<<ceil_div(hn[1], kT * kCompactPer), kT, 0, st>>>(O8.dslot, O8.dnum, hn[1], 4u, O.deep,
-                                                                           O.n_deep);
+          add_deep(O8.dslot, nullptr, O8.dnum, hn[1], 4u);
         }
       }
       if (ncls[1]) {
@@ -2570,8 +2613,7 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         O1.dslot = ws.typed<Grp>("sort_dslot1", (size_t)ncls[1] * O1.dm);
         O1.dnum = ws.u32("sort_dnum1", ncls[1]);
         k_bsort<16, 1, 2, false><<<ceil_div(ncls[1], 4 * (kT / 64)), kT, 0, st>>>(C.l[1], ncls[1], B, O1);
-        k_deep_compact2<<<ceil_div(ncls[1], kT * kCompactPer), kT, 0, st>>>(O1.dslot, O1.dnum, ncls[1], O1.dm, O.deep,
-                                                                             O.n_deep);
+        add_deep(O1.dslot, nullptr, O1.dnum, ncls[1], O1.dm);
       }
       if (ncls[2]) {
         SortOut O2 = O;
@@ -2579,13 +2621,14 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
         O2.dslot = ws.typed<Grp>("sort_dslot2", (size_t)ncls[2] * O2.dm);
         O2.dnum = ws.u32("sort_dnum2", ncls[2]);
         k_bsort<32, 1, 2, false><<<ceil_div(ncls[2], 2 * (kT / 64)), kT, 0, st>>>(C.l[2], ncls[2], B, O2);
-        k_deep_compact2<<<ceil_div(ncls[2], kT * kCompactPer), kT, 0, st>>>(O2.dslot, O2.dnum, ncls[2], O2.dm, O.deep,
-                                                                             O.n_deep);
+        add_deep(O2.dslot, nullptr, O2.dnum, ncls[2], O2.dm);
       }
+      if (D.ns) k_deep_compact_all<<<dwg, kT, 0, st>>>(D, O.deep, O.n_deep);
       HIP_OK(hipGetLastError());
       const uint32_t total = ncls[3] + ncls[4] + ncls[5] + ncls[6];
       if (total == 0) break;
-      HIP_OK(hipMemsetAsync(ccnt2, 0, (kS2Cls * (size_t)total + 1) * 4, st));
+      // (every group of the emitting classes writes its kS2Cls counts; the scan's last input
+      // word does not affect its exclusive output)
       S2Emit E{srec, ccnt2, total, 0};
       if (ncls[3]) k_bsort<64, 1, kR3, false, true><<<ceil_div(ncls[3], kT / 64), kT, 0, st>>>(C.l[3], ncls[3], B, O, E);
       E.gbase += ncls[3];
@@ -2598,10 +2641,12 @@ void bwt_stage(Workspace& ws, const Rle1Result& r, const std::vector<uint32_t>& 
       scan_u32(ScanOp::Sum, true, ccnt2, ccnt2, kS2Cls * (size_t)total + 1, nullptr, scratch2, st);
       S2Lists Ls{{C.l[3], C.l[4], C.l[5], C.l[6]},
                  {0, ncls[3], ncls[3] + ncls[4], ncls[3] + ncls[4] + ncls[5], total}};
-      k_s2_emit<<<grid(total), kT, 0, st>>>(Ls, srec, ccnt2, total, N);
-      k_s2_bounds<<<1, 64, 0, st>>>(ccnt2, total, cnt + 24);
+      k_s2_emit<<<grid(total), kT, 0, st>>>(Ls, srec, ccnt2, total, N, cnt + 32);
       HIP_OK(hipGetLastError());
-      read_counters();
+      // class sizes of the next lists: the class-major scan's entries at c * total
+      uint32_t b2[kS2Cls + 1];
+      ws.read_small({{b2, ccnt2, 4ull * (kS2Cls + 1), total}}, st);
+      for (int c = 0; c < kS2Cls; c++) hc[24 + c] = b2[c + 1] - b2[c];
       for (int c = 0; c < kS2Cls; c++) {
         ncls[c] = hc[24 + c];
         std::swap(C.l[c], N.l[c]);

@@ -514,7 +514,7 @@ void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0
   {
     uint32_t* sz = ws.u32("dbl_P", (size_t)nL0 + 16);
     uint32_t* tot0 = ws.u32("dbl_T0", 16);
-    uint32_t* scr = ws.u32("dbl_scan", scan_scratch_words((size_t)nL0 + 16) + 64);
+    uint32_t* scr = ws.u32z("dbl_scan", scan_scratch_words((size_t)nL0 + 16) + 64);
     k_group_sizes<<<(unsigned)ceil_div64(nL0, kT), kT, 0, st>>>(L0, nL0, sz);
     HIP_OK(hipGetLastError());
     scan_u32(ScanOp::Sum, true, sz, sz, nL0, tot0, scr, st);
@@ -539,7 +539,7 @@ void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0
   uint32_t* hist = ws.u32("dbl_hist", max_dtiles * 256);
   uint32_t* tot = ws.u32("dbl_tot", bigcap * 256);
   uint32_t* cnt = ws.u32("dbl_cnt", 64);
-  uint32_t* scratch = ws.u32("dbl_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(lcap, max_dtiles), T + 16)) + 64);
+  uint32_t* scratch = ws.u32z("dbl_scan", scan_scratch_words(std::max<size_t>(std::max<size_t>(lcap, max_dtiles), T + 16)) + 64);
   HIP_OK(hipMemcpyAsync(L, L0, sizeof(Grp) * nL0, hipMemcpyDeviceToDevice, st));
   // counters: 0 total(scan), 1 n_large, 2 n_small, 3 n_next(L'), 4 n_large2, 5 n_equal, 6 tiles
   uint32_t hc[8];

@@ -24,10 +24,12 @@ class Workspace {
   Workspace(const Workspace&) = delete;
   Workspace& operator=(const Workspace&) = delete;
 
-  void* get(const std::string& name, size_t bytes);
+  void* get(const std::string& name, size_t bytes, bool zero = false);
   uint8_t* u8(const std::string& name, size_t n) { return (uint8_t*)get(name, n); }
   uint16_t* u16(const std::string& name, size_t n) { return (uint16_t*)get(name, n * 2); }
   uint32_t* u32(const std::string& name, size_t n) { return (uint32_t*)get(name, n * 4); }
+  // the same, zeroed (on this workspace's stream) whenever it is (re)allocated: scan scratch
+  uint32_t* u32z(const std::string& name, size_t n) { return (uint32_t*)get(name, n * 4, true); }
   template <typename T>
   T* typed(const std::string& name, size_t n) { return (T*)get(name, n * sizeof(T)); }
 
@@ -48,11 +50,13 @@ class Workspace {
   // read instead of ~35 (profiles/r05_gaps_*).  Larger reads take hipMemcpyAsync + a stream
   // synchronisation.
   void read_small(void* dst, const void* dev_src, size_t bytes, hipStream_t st);
-  // the same for up to four pieces at once
+  // the same for up to four pieces at once; a piece with stride s > 1 reads the 32-bit words
+  // src[0], src[s], src[2 s], ... (bytes / 4 of them)
   struct SmallRead {
     void* dst;
     const void* src;
     size_t bytes;
+    uint32_t stride = 1;
   };
   void read_small(std::initializer_list<SmallRead> reads, hipStream_t st);
 
