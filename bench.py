@@ -376,6 +376,21 @@ def time_device(d, n, level, d_out, cap, steps, warmup=1):
     return (time.perf_counter() - t) * 1e3 / steps, nb, B.last_stats()
 
 
+def sequential_stages(d, n, level, d_out, cap):
+    """A multi-batch input's stage split with its batches one after another (one untimed step,
+    BZG_BATCH_PIPE=0): the pipelined run's stage figures are per-batch event spans that overlap
+    (a batch's MTF / tables / packing beside the next batch's sorts), so their sum exceeds the
+    step time."""
+    os.environ["BZG_BATCH_PIPE"] = "0"
+    try:
+        ms, _, st = time_device(d, n, level, d_out, cap, steps=1, warmup=0)
+    finally:
+        del os.environ["BZG_BATCH_PIPE"]
+    return {"ms": round(ms, 3), "stages_ms": {k: round(st[k + "_ms"], 3) for k in ("rle1", "bwt", "mtf", "code")},
+            "note": "one step with the batches one after another (BZG_BATCH_PIPE=0); stages_ms of the pipelined "
+                    "line above are overlapping per-batch spans"}
+
+
 def line_for(name, n, level, ms, nb, st, workload):
     rho = st["rle_bytes"] / n
     c = nb / n
@@ -510,6 +525,7 @@ def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False, nb_text=0):
     out = torch.empty(cap, dtype=torch.uint8, device="cuda")
     ms, nb, st = time_device(d, n4, level, out, cap, steps=2)
     res["single_byte_4gib"] = line_for("single", n4, level, ms, nb, st, "4 GiB of byte 0x61 (BASELINE config 4), -9")
+    res["single_byte_4gib"]["sequential"] = sequential_stages(d, n4, level, out, cap)
     res["single_byte_4gib"]["parity"] = sample_parity(d, 256 << 20, level, no_cpu)
     g = torch.Generator(device="cuda")
     g.manual_seed(0x5EED0005)
@@ -517,6 +533,7 @@ def extra_configs(a, d_text, d_out_text, cap_text, no_cpu=False, nb_text=0):
     ms, nb, st = time_device(d, n4, level, out, cap, steps=2)
     res["random_4gib"] = line_for("random", n4, level, ms, nb, st,
                                   "4 GiB of seeded PRNG bytes (torch Philox, seed 0x5EED0005; BASELINE config 5), -9")
+    res["random_4gib"]["sequential"] = sequential_stages(d, n4, level, out, cap)
     res["random_4gib"]["parity"] = sample_parity(d, 32 << 20, level, no_cpu)
     del d, out
     torch.cuda.empty_cache()

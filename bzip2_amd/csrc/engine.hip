@@ -31,8 +31,36 @@ namespace bzg {
 // ---------------------------------------------------------------- workspace
 Workspace::~Workspace() {
   release_all();
+  for (hipEvent_t& e : sev_)
+    if (e) (void)hipEventDestroy(e);
+  if (side_) (void)hipStreamDestroy(side_);
   if (handoff_) (void)hipEventDestroy(handoff_);
   if (mbox_) (void)hipHostFree(mbox_);
+}
+
+hipStream_t Workspace::side_stream() {
+  if (!side_) HIP_OK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  return side_;
+}
+
+hipEvent_t Workspace::side_event(int k) {
+  if (!sev_[k]) HIP_OK(hipEventCreateWithFlags(&sev_[k], hipEventDisableTiming));
+  return sev_[k];
+}
+
+void* Workspace::pinned(const std::string& name, size_t bytes) {
+  auto& b = pins_[name];
+  if (b.second >= bytes) return b.first;
+  if (b.first) {
+    if (side_) HIP_OK(hipStreamSynchronize(side_));
+    (void)hipHostFree(b.first);
+    b.first = nullptr;
+    b.second = 0;
+  }
+  const size_t grow = bytes + bytes / 4 + 64;
+  HIP_OK(hipHostMalloc(&b.first, grow, hipHostMallocDefault));
+  b.second = grow;
+  return b.first;
 }
 
 // read_small: the words of up to four pieces to pinned host memory, then the flag (release at
@@ -148,6 +176,12 @@ void Workspace::drop(Buf& b) {
 }
 
 void Workspace::release_all() {
+  if (!pins_.empty()) {
+    if (side_) (void)hipStreamSynchronize(side_);
+    for (auto& kv : pins_)
+      if (kv.second.first) (void)hipHostFree(kv.second.first);
+    pins_.clear();
+  }
   bool any_async = false;
   for (auto& kv : bufs_) {
     any_async |= kv.second.async && kv.second.p;
@@ -608,7 +642,7 @@ static void add_stats(bzg_stats& acc, const bzg_stats& one) {
 
 void Engine::compress(const uint8_t* d_in, uint64_t n, unsigned flags, bzg_stream_state* st, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* out_bytes, uint64_t* consumed, hipStream_t s, bzg_stats& last) {
-  static const bool pipe = cfg("BZG_BATCH_PIPE", 1, 0, 1) != 0;  // BZG_BATCH_PIPE=0: batches one after another
+  const bool pipe = cfg("BZG_BATCH_PIPE", 1, 0, 1) != 0;  // BZG_BATCH_PIPE=0: batches one after another (per call)
   const uint64_t batch_max = max_batch();
   if (pipe && n > batch_max) return compress_pipelined(d_in, n, flags, st, d_out, out_cap, out_bytes, consumed, s, last);
   ws.set_stream(s);

@@ -290,11 +290,13 @@ void copyrank_begin(Workspace& ws, const Rle1Result& r, const std::vector<uint32
   HIP_OK(hipGetLastError());
   // side stream: the device's answers and the root bytes to pinned memory, the host model for
   // what is left, the merged answers back
-  HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&job.pin_r), 4ull * (nb + 2), hipHostMallocDefault));
-  HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&job.pin_roots), total + 16, hipHostMallocDefault));
-  HIP_OK(hipStreamCreateWithFlags(&job.side, hipStreamNonBlocking));
-  HIP_OK(hipEventCreateWithFlags(&job.ev_cf, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&job.ev_done, hipEventDisableTiming));
+  // (the part workspace's side stream orders this batch's use of its pinned buffers after the
+  // previous batch's)
+  job.side = ws.side_stream();
+  job.pin_r = static_cast<int32_t*>(ws.pinned("copyrank_r", 4ull * (nb + 2)));
+  job.pin_roots = static_cast<uint8_t*>(ws.pinned("copyrank_roots", total + 16));
+  job.ev_cf = ws.side_event(0);
+  job.ev_done = ws.side_event(1);
   HIP_OK(hipEventRecord(job.ev_cf, st));
   HIP_OK(hipStreamWaitEvent(job.side, job.ev_cf, 0));
   HIP_OK(hipMemcpyAsync(job.pin_r, job.dev_r, 4ull * nb, hipMemcpyDeviceToHost, job.side));
@@ -323,12 +325,9 @@ void copyrank_check(const CopyRankJob& job) {
 }
 
 CopyRankJob::~CopyRankJob() {
+  // the host function on the side stream reads this job (the stream, events and pinned
+  // buffers belong to the part workspace)
   if (side) (void)hipStreamSynchronize(side);
-  if (ev_cf) (void)hipEventDestroy(ev_cf);
-  if (ev_done) (void)hipEventDestroy(ev_done);
-  if (side) (void)hipStreamDestroy(side);
-  if (pin_r) (void)hipHostFree(pin_r);
-  if (pin_roots) (void)hipHostFree(pin_roots);
 }
 
 }  // namespace bzg

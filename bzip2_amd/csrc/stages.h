@@ -33,6 +33,12 @@ class Workspace {
   template <typename T>
   T* typed(const std::string& name, size_t n) { return (T*)get(name, n * sizeof(T)); }
 
+  // Grow-only pinned host buffer, kept across calls (growth first waits for the side stream,
+  // the only user of these buffers), and the workspace's side stream and events, created once.
+  void* pinned(const std::string& name, size_t bytes);
+  hipStream_t side_stream();
+  hipEvent_t side_event(int k);  // k < 4
+
   const uint32_t* crc_table();   // 256 entries, MSB-first CRC-32 (poly 0x04C11DB7)
   const uint32_t* xpow2_table(); // 48 entries: x^(8*2^k) mod P
   size_t bytes_reserved() const { return total_; }
@@ -70,6 +76,9 @@ class Workspace {
   hipStream_t stream_ = nullptr;
   hipEvent_t handoff_ = nullptr;
   std::map<std::string, Buf> bufs_;
+  std::map<std::string, std::pair<void*, size_t>> pins_;
+  hipStream_t side_ = nullptr;
+  hipEvent_t sev_[4] = {};
   size_t total_ = 0;
   uint32_t* crc_ = nullptr;
   uint32_t* xp2_ = nullptr;
@@ -120,6 +129,7 @@ void seg_walk_stage(Workspace& ws, const uint8_t* d_in, uint64_t n, int level, u
 struct CopyRankJob {
   std::vector<uint32_t> need, per, len;  // blocks with such roots, their periods and lengths
   int32_t* dev_r = nullptr;              // per block: r (workspace buffer)
+  // the part workspace's pinned buffers, side stream and events (reused from batch to batch)
   int32_t* pin_r = nullptr;              // pinned: the device's answers, then the merged ones
   uint8_t* pin_roots = nullptr;          // pinned: the roots of `need`, concatenated
   hipStream_t side = nullptr;
