@@ -13,6 +13,11 @@ struct CopyRankFailure {};
 // Largest number of B* offsets per root the device closed form (origptr.hip k_copyrank_cf)
 // evaluates; copy_rank_distinct applies the same cap so that it reports what the device does.
 constexpr int32_t kCopyRankQMax = 1024;
+// ... and the bound on its class comparisons: a root of at most kCopyRankPMax bytes with
+// q * p <= kCopyRankCmpMax (a thread compares one class with the others, at most p bytes; a
+// workgroup at most q * p), longer roots go to the host model
+constexpr int32_t kCopyRankPMax = 16384;
+constexpr int64_t kCopyRankCmpMax = 1ll << 22;
 
 // B* structure of the cyclic root w (|w| = p >= 2, primitive): number of B* offsets q.
 int32_t root_bstar_count(const uint8_t* w, int32_t p);

@@ -64,7 +64,8 @@ int32_t copy_rank_distinct(const uint8_t* w, int32_t p, int32_t k) {
     if (w[t] < c) off.push_back(i);
   }
   const int32_t q = (int32_t)off.size();
-  if (q < 2 || q > kCopyRankQMax) return -1;  // (the device's cap, origptr.hip)
+  if (q < 2 || q > kCopyRankQMax) return -1;  // (the device's caps, origptr.hip)
+  if (p > kCopyRankPMax || (int64_t)q * p > kCopyRankCmpMax) return -1;
   const uint64_t m = (uint64_t)q * (uint64_t)k;
   if (m > 0x7fffffffull) return -1;
   std::vector<int32_t> bk(q), gap(q), ord(q), rk(q);

@@ -72,7 +72,8 @@ __global__ void __launch_bounds__(kCT) k_copyrank_cf(const uint8_t* __restrict__
   __shared__ unsigned long long work;
   const uint32_t b = list[blockIdx.x], lo = boff[b], n = boff[b + 1] - lo, p = period[b], q = bq[b];
   const uint32_t k = p ? n / p : 0;
-  if (q < 2 || q > kQMax || p < 2 || k < 2 || (uint64_t)q * k > 0x7fffffffull) {
+  if (q < 2 || q > kQMax || p < 2 || k < 2 || (uint64_t)q * k > 0x7fffffffull || p > (uint32_t)kCopyRankPMax ||
+      (int64_t)q * p > kCopyRankCmpMax) {  // (bounded comparisons: copyrank.h)
     if (threadIdx.x == 0) out[b] = -1;
     return;
   }
