@@ -37,8 +37,8 @@ HBM_PEAK_GBPS = 8000.0
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=3)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--bytes", type=int, default=1_000_000_000, help="input bytes per GPU (weak scaling)")
     p.add_argument("--total-bytes", type=int, default=0,
                    help="strong scaling: ONE stream of this many bytes split into N contiguous shards, one per "
