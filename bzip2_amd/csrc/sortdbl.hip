@@ -193,14 +193,18 @@ __global__ void __launch_bounds__(kT) k_dsingle(const Grp* __restrict__ G, uint3
 }
 
 // ---------------------------------------------------------------- small groups (LDS)
-// tile index of item i = P[i] / kWin; mark the first item of each tile and one past its last.
-__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_t* __restrict__ first,
+// tile index of item i = P[i] / kWin; mark the first item of each tile and one past its last,
+// and every tile of the ntiles that no item starts in (inside a large item, or after the last
+// one) empty, so that `first` needs no clearing.
+__global__ void k_tile_first(const uint32_t* __restrict__ P, uint32_t n, uint32_t ntiles, uint32_t* __restrict__ first,
                              uint32_t* __restrict__ last) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t t = P[i] / kWin;
   if (i == 0 || P[i - 1] / kWin != t) first[t] = i;
   if (i == n - 1 || P[i + 1] / kWin != t) last[t] = i + 1;
+  const uint32_t tn = i + 1 < n ? P[i + 1] / kWin : ntiles;
+  for (uint32_t e = t + 1; e < tn; e++) first[e] = 0xffffffffu;
 }
 
 struct TileLds {
@@ -599,12 +603,12 @@ void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0
       n_large = hc[4];
       std::swap(lg, lg2);
     }
-    HIP_OK(hipMemsetAsync(cnt + 3, 0, 4, st));
+    // (cnt + 3, the next list's count, was cleared with cnt + 1..7 at the top of the iteration:
+    // only k_tile_sort and k_equal below append to it)
     const uint32_t kbits = 20u;
     {  // groups of L small enough for LDS: tiles straight over L (P still holds L's prefix)
       const uint32_t ntiles = ceil_div(totalL, kWin);
-      HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
-      k_tile_first<<<grid(nL), kT, 0, st>>>(P, nL, first, last);
+      k_tile_first<<<grid(nL), kT, 0, st>>>(P, nL, ntiles, first, last);
       HIP_OK(hipGetLastError());
       k_tile_sort<false><<<ntiles, kT, tile_lds, st>>>(L, nL, first, last, kbits, B, Ln, cnt + 3, true, nullptr);
       HIP_OK(hipGetLastError());
@@ -619,8 +623,7 @@ void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0
       read_counters();
       const uint32_t tot_small = hc[0];
       const uint32_t ntiles = ceil_div(tot_small, kWin);
-      HIP_OK(hipMemsetAsync(first, 0xff, (size_t)ntiles * 4, st));
-      k_tile_first<<<grid(n_small), kT, 0, st>>>(P, n_small, first, last);
+      k_tile_first<<<grid(n_small), kT, 0, st>>>(P, n_small, ntiles, first, last);
       HIP_OK(hipGetLastError());
       k_tile_sort<false><<<ntiles, kT, tile_lds, st>>>(small, n_small, first, last, kbits, B, Ln, cnt + 3, false, nullptr);
       HIP_OK(hipGetLastError());
@@ -633,7 +636,7 @@ void doubling_sort(Workspace& ws, const SortBufs& B, const Grp* L0, uint32_t nL0
       k_equal<<<hc[6], kT, 0, st>>>(equal, n_equal, TP, B, Ln, cnt + 3);
       HIP_OK(hipGetLastError());
     }
-    read_counters();
+    if (n_small > 0 || n_equal > 0) read_counters();  // (else hc[3] is already the count)
     nL = hc[3];
     std::swap(L, Ln);
     h *= 2;
