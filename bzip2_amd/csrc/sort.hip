@@ -397,10 +397,13 @@ __global__ void __launch_bounds__(kT) k_s1_scatter(const TileRec* __restrict__ T
                                                    SortBufs B, SortOut O, const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ tot, const uint32_t* __restrict__ cscan,
                                                    uint32_t nTot, ClsLists C) {
-  // 20 KB of LDS, so that 8 workgroups fit a CU: the bucket counters (4 bank-spread copies per
-  // bucket, see k_s1_hist) and the reordered tile.  Once the tile is reordered the counter
-  // space holds each bucket's store base and flags (and the emission's wave counts); the scan
-  // scratch lives in the tile space before the tile is.
+  // 36 KB of LDS (4 workgroups per CU): the bucket counters (4 bank-spread copies per bucket,
+  // see k_s1_hist) and the reordered tile, rotations and key caches.  Once the tile is
+  // reordered the counter space holds each bucket's store base and flags (and the emission's
+  // wave counts); the scan scratch lives in the tile space before the tile is.  (Round 3 fitted
+  // 2048-rotation tiles in 20 KB for 8 workgroups; 4096-rotation tiles measured faster in round
+  // 4, and one shared 16 KB reorder array, or 7 waves per SIMD, gave nothing in round 6:
+  // profiles/r06_ab_s1_scatter.txt.)
   __shared__ uint32_t cnt[256 * 4];
   __shared__ uint32_t Lv[kDTile], Lk[kDTile];
   static_assert(kDTile == kPerT * kT, "one element per thread and round");
