@@ -131,6 +131,92 @@ __device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, i
   }
 }
 
+// The same BZ2_hbMakeCodeLengths run by one lane per table, kHuffLanes tables per wave, for
+// launches with many tables (the single-lane heap issues every instruction for the whole wave:
+// with thousands of tables per launch, BASELINE config 5, k_huff is VALU-bound, not
+// latency-bound).  Each lane keeps its table in its own LDS region (heap entries carrying
+// their weight, leaf weights, parents, depths) and runs the reference's loops as written:
+// UPHEAP / DOWNHEAP with strict '<' on weights, the rescale rounds, lengths as depths (nodes
+// are created in increasing order, so the depths fill top-down in one pass).
+constexpr int kHuffLanes = 8;
+struct HuffLane {  // 3,108 bytes: 8 lanes' regions in 24.9 KB, 6 workgroups per CU
+  uint64_t heap[kMaxAlpha + 1];
+  int16_t parent[2 * kMaxAlpha];  // then each node's depth, in place
+  uint32_t pad;                   // (regions of different lanes start in different banks)
+};
+// The leaf weights live in the table's frequency words in global memory (read at the start,
+// touched again only by a rescale), which are zeroed at the end when `reset` (ready for the
+// next iteration's counts).
+__device__ void hb_lane_lengths(HuffLane& H, uint32_t* __restrict__ wt, bool reset, int alpha, int max_len,
+                                uint8_t* __restrict__ lens) {
+  for (int i = 0; i < alpha; i++) {
+    const uint32_t f = wt[i];
+    wt[i] = (f == 0 ? 1u : f) << 8;
+  }
+  for (int round = 0; round < 64; round++) {
+    int nheap = 0, nodes = alpha;
+    H.heap[0] = 0;  // weight 0 sentinel above the root
+    for (int i = 1; i <= alpha; i++) {
+      H.parent[i] = -1;
+      const uint64_t tmp = ((uint64_t)wt[i - 1] << 32) | (uint32_t)i;
+      int z = ++nheap;
+      while (hb_wt(tmp) < hb_wt(H.heap[z >> 1])) {
+        H.heap[z] = H.heap[z >> 1];
+        z >>= 1;
+      }
+      H.heap[z] = tmp;
+    }
+    while (nheap > 1) {
+      uint64_t pick[2];
+      for (int k = 0; k < 2; k++) {
+        pick[k] = H.heap[1];
+        const uint64_t tmp = H.heap[nheap--];
+        int z = 1;
+        for (;;) {
+          int y = z << 1;
+          if (y > nheap) break;
+          uint64_t c = H.heap[y];
+          if (y < nheap) {
+            const uint64_t c2 = H.heap[y + 1];
+            if (hb_wt(c2) < hb_wt(c)) {
+              c = c2;
+              y++;
+            }
+          }
+          if (hb_wt(tmp) < hb_wt(c)) break;
+          H.heap[z] = c;
+          z = y;
+        }
+        H.heap[z] = tmp;
+      }
+      nodes++;
+      H.parent[(uint32_t)pick[0]] = H.parent[(uint32_t)pick[1]] = (int16_t)nodes;
+      const int32_t w0 = hb_wt(pick[0]), w1 = hb_wt(pick[1]);
+      const int32_t d0 = w0 & 0xff, d1 = w1 & 0xff;
+      const int32_t wn = (int32_t)(((uint32_t)w0 & 0xffffff00u) + ((uint32_t)w1 & 0xffffff00u)) | (1 + (d0 > d1 ? d0 : d1));
+      const uint64_t tmp = ((uint64_t)(uint32_t)wn << 32) | (uint32_t)nodes;
+      int z = ++nheap;
+      while (hb_wt(tmp) < hb_wt(H.heap[z >> 1])) {
+        H.heap[z] = H.heap[z >> 1];
+        z >>= 1;
+      }
+      H.heap[z] = tmp;
+    }
+    // depths top-down (a parent has a larger index than its children), in place of the parents
+    H.parent[nodes] = 0;
+    for (int k = nodes - 1; k >= 1; k--) H.parent[k] = (int16_t)(H.parent[H.parent[k]] + 1);
+    bool too_long = false;
+    for (int i = 1; i <= alpha; i++) {
+      lens[i - 1] = (uint8_t)H.parent[i];
+      too_long |= H.parent[i] > max_len;
+    }
+    if (!too_long) break;
+    for (int i = 0; i < alpha; i++) wt[i] = (1 + ((wt[i] >> 8) / 2)) << 8;
+  }
+  if (reset)
+    for (int i = 0; i < alpha; i++) wt[i] = 0;
+}
+
 __device__ __forceinline__ int n_groups(uint32_t nmtf) {  // compress.c:266-270
   return nmtf < 200 ? 2 : nmtf < 600 ? 3 : nmtf < 1200 ? 4 : nmtf < 2400 ? 5 : 6;
 }
@@ -147,6 +233,12 @@ __device__ __forceinline__ int n_groups(uint32_t nmtf) {  // compress.c:266-270
 // enough for about kSliceFill workgroups per launch, so that a call of few blocks (100 MB: 110
 // blocks, 55 per k_cf half) is not a chain of steps on a hundred workgroups.
 constexpr uint32_t kCfSlices = 2, kPackSlices = 1, kSliceMax = 8, kSliceFill = 768;
+// tables per launch from which k_huff_lanes (a lane per table) replaces k_huff (a wave per
+// table); BZG_HUFF_LANES_MIN overrides (A/B knob; 0 also routes the code-length test hook)
+inline uint32_t huff_lanes_min() {
+  static const uint32_t v = (uint32_t)std::max(0ll, env_ll("BZG_HUFF_LANES_MIN", 4096));
+  return v;
+}
 inline uint32_t slices_for(uint32_t nb, uint32_t lo) {
   return std::max(lo, std::min(kSliceMax, ceil_div(kSliceFill, std::max(nb, 1u))));
 }
@@ -337,6 +429,21 @@ __global__ void __launch_bounds__(64) k_huff(uint32_t b0, const uint32_t* __rest
   for (int v = threadIdx.x; v < alpha; v += 64) L[v] = len[v];
 }
 
+// k_huff with kHuffLanes tables per wave (one lane each): table tt = wave * kHuffLanes + lane of
+// the launch's n blocks (tt / kNGroups, tt % kNGroups).
+__global__ void __launch_bounds__(64) k_huff_lanes(uint32_t b0, uint32_t n, const uint32_t* __restrict__ nmtf_g,
+                                                   const uint32_t* __restrict__ ninuse, uint32_t* __restrict__ rf_g,
+                                                   uint8_t* __restrict__ lens_g) {
+  __shared__ HuffLane H[kHuffLanes];
+  const uint32_t lane = threadIdx.x, tt = blockIdx.x * kHuffLanes + lane;
+  if (lane >= (uint32_t)kHuffLanes || tt >= n * kNGroups) return;
+  const uint32_t b = b0 + tt / kNGroups, t = tt % kNGroups;
+  if ((int)t >= n_groups(nmtf_g[b])) return;
+  const int alpha = (int)ninuse[b] + 2;
+  hb_lane_lengths(H[lane], rf_g + ((size_t)b * kNGroups + t) * kMaxAlpha, true, alpha, kMaxCodeLen,
+                  lens_g + ((size_t)b * kNGroups + t) * kMaxAlpha);
+}
+
 // Test hook: code lengths of n tables (freq[t * kMaxAlpha ..], alpha[t], max_len) with the
 // same device routine as k_huff.
 __global__ void __launch_bounds__(64) k_code_lengths_test(const uint32_t* __restrict__ freq_g,
@@ -354,6 +461,16 @@ __global__ void __launch_bounds__(64) k_code_lengths_test(const uint32_t* __rest
   hb_code_lengths(len, fq, alpha, max_len, heap, weight, parent);
   __syncthreads();
   for (int v = threadIdx.x; v < alpha; v += 64) lens_g[(size_t)t * kMaxAlpha + v] = len[v];
+}
+
+__global__ void __launch_bounds__(64) k_code_lengths_lanes(const uint32_t* __restrict__ freq_g,
+                                                           const int32_t* __restrict__ alpha_g, uint32_t n, int max_len,
+                                                           uint8_t* __restrict__ lens_g) {
+  __shared__ HuffLane H[kHuffLanes];
+  const uint32_t lane = threadIdx.x, t = blockIdx.x * kHuffLanes + lane;
+  if (lane >= (uint32_t)kHuffLanes || t >= n) return;
+  hb_lane_lengths(H[lane], const_cast<uint32_t*>(freq_g) + (size_t)t * kMaxAlpha, false, alpha_g[t], max_len,
+                  lens_g + (size_t)t * kMaxAlpha);
 }
 
 // Canonical codes (huffman.c:152-166), selector MTF (compress.c:573-631), table bits
@@ -868,7 +985,10 @@ void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_
     for (int it = 0; it < kIters; it++) {
       k_cf<<<dim3(slices_for(n, kCfSlices), n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 0);
       HIP_OK(hipGetLastError());
-      k_huff<<<n * kNGroups, 64, 0, s>>>(b0, m.nmtf, r.ninuse, rf, t.lens);
+      if (n * (uint32_t)kNGroups >= huff_lanes_min())
+        k_huff_lanes<<<ceil_div(n * (uint32_t)kNGroups, (uint32_t)kHuffLanes), 64, 0, s>>>(b0, n, m.nmtf, r.ninuse, rf, t.lens);
+      else
+        k_huff<<<n * kNGroups, 64, 0, s>>>(b0, m.nmtf, r.ninuse, rf, t.lens);
       HIP_OK(hipGetLastError());
     }
     k_cf<<<dim3(slices_for(n, kCfSlices), n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 1);
@@ -946,7 +1066,11 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
 void code_lengths_test(const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len, uint8_t* d_lens,
                        hipStream_t st) {
   if (n == 0) return;
-  k_code_lengths_test<<<n, 64, 0, st>>>(d_freq, d_alpha, max_len, d_lens);
+  if (huff_lanes_min() == 0) {  // BZG_HUFF_LANES_MIN=0: the lane-per-table routine (its parity tests)
+    k_code_lengths_lanes<<<ceil_div(n, (uint32_t)kHuffLanes), 64, 0, st>>>(d_freq, d_alpha, n, max_len, d_lens);
+  } else {
+    k_code_lengths_test<<<n, 64, 0, st>>>(d_freq, d_alpha, max_len, d_lens);
+  }
   HIP_OK(hipGetLastError());
 }
 
