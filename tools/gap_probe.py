@@ -58,6 +58,13 @@ def report(path):
           f"{len(last)} kernels, {len(gaps)} gaps, idle {1e-6 * sum(g for g, _, _ in gaps):.3f} ms")
     for g, a, b in sorted(gaps, reverse=True)[:25]:
         print(f"  {g / 1e3:8.1f} us  after {a:40s} before {b}")
+    tot = {}
+    for s, e, n in last:
+        c, t = tot.get(n, (0, 0))
+        tot[n] = (c + 1, t + e - s)
+    print("per kernel in the last call (us, launches):")
+    for n, (c, t) in sorted(tot.items(), key=lambda kv: -kv[1][1]):
+        print(f"  {n:40s} {t / 1e3:9.1f} {c:5d}")
 
 
 if __name__ == "__main__":
