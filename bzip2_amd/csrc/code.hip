@@ -89,11 +89,18 @@ __device__ __forceinline__ void hb_sift_down(uint64_t* heap, int nheap, uint64_t
   heap[z] = item;
 }
 
-__device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, int max_len, uint64_t* heap,
-                                int32_t* weight, int32_t* parent) {
+// `rescales`: leaf weights halved that many times before the first round (the weights of
+// round 1 + rescales); at most kRounds rounds.  Returns whether the lengths fit max_len.
+template <int kRounds>
+__device__ bool hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, int max_len, uint64_t* heap,
+                                int32_t* weight, int32_t* parent, int rescales) {
   const int lane = (int)__lane_id();
-  for (int i = lane; i < alpha; i += 64) weight[i + 1] = (int32_t)((freq[i] == 0 ? 1u : freq[i]) << 8);
-  for (int round = 0; round < 64; round++) {  // converges in a few rounds for valid tables
+  for (int i = lane; i < alpha; i += 64) {
+    uint32_t f = freq[i] == 0 ? 1u : freq[i];
+    for (int k = 0; k < rescales; k++) f = 1 + f / 2;
+    weight[i + 1] = (int32_t)(f << 8);
+  }
+  for (int round = 0; round < kRounds; round++) {  // converges in a few rounds for valid tables
     for (int i = lane; i < 2 * alpha; i += 64) parent[i] = -1;
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
@@ -126,9 +133,61 @@ __device__ void hb_code_lengths(uint8_t* len, const uint32_t* freq, int alpha, i
       len[i - 1] = (uint8_t)d;
       if (d > max_len) too_long = true;
     }
-    if (__ballot(too_long) == 0) return;
+    if (__ballot(too_long) == 0) return true;
     for (int i = lane + 1; i <= alpha; i += 64) weight[i] = (1 + ((weight[i] >> 8) / 2)) << 8;
   }
+  return false;
+}
+
+struct HuffLds {  // one wave's table
+  alignas(16) uint64_t heap[kHeapCap];
+  int32_t weight[kMaxAlpha + 2];
+  int32_t parent[kMaxAlpha * 2];
+  uint32_t fq[kMaxAlpha];
+  uint8_t len[kMaxAlpha + 2];
+  uint32_t word;
+};
+
+// Rounds 1 and 2 of one table at once (k_huff_spec): workgroup r0 of the table runs round
+// 1 + r0 alone (its leaf weights halved r0 times: a round's weights depend only on the
+// frequencies, not on the previous round's tree).  Round 1's lengths, when they fit, go
+// straight to L; round 2's to the table's scratch.  The second workgroup to finish (one
+// atomic on the table's word: finish count in bits 0-1, "round 1 + r0 fits" in bit 2 + r0)
+// keeps the first round that fits -- or, when neither does, goes on from round 3 -- and
+// resets the word (and the frequencies, when `rf`).  The same lengths as the reference's
+// rounds one after another (huffman.c:63-148).  A table that needs one rescale (22 of 2,688
+// on the 100 MB bench text, in 6 of its 8 launches) then costs one round of latency instead
+// of two; but the round-1 waves run slower beside the round-2 ones (a launch of 336 tables:
+// 115-135 us for one round alone, 175-200 with the speculation, 210-225 for two rounds), so
+// the gain is 60-80 us per 100 MB call (profiles/r06_ab_huff_spec.txt).
+__device__ void hb_spec_table(HuffLds& S, int alpha, int max_len, uint32_t r0, uint32_t* word, uint8_t* scratch,
+                              uint8_t* L, uint32_t* rf) {
+  const bool ok = hb_code_lengths<1>(S.len, S.fq, alpha, max_len, S.heap, S.weight, S.parent, (int)r0);
+  if (ok) {
+    uint8_t* dst = r0 == 0 ? L : scratch;
+    for (int v = threadIdx.x; v < alpha; v += 64) dst[v] = S.len[v];
+  }
+  const uint32_t mine = 1u | ((ok ? 1u : 0u) << (2 + r0));
+  if (threadIdx.x == 0) {
+    __threadfence();  // the lengths before the count
+    S.word = atomicAdd(word, mine) + mine;
+    __threadfence();
+  }
+  __syncthreads();
+  const uint32_t w = S.word;
+  if ((w & 3u) != 2u) return;  // the other workgroup finishes the table
+  if (!(w & 4u)) {
+    const uint8_t* src = S.len;
+    if (w & 8u) {
+      if (r0 == 0) src = scratch;  // round 2 ran in the other workgroup
+    } else {
+      (void)hb_code_lengths<62>(S.len, S.fq, alpha, max_len, S.heap, S.weight, S.parent, 2);
+    }
+    for (int v = threadIdx.x; v < alpha; v += 64) L[v] = src[v];
+  }
+  if (rf)
+    for (int v = threadIdx.x; v < alpha; v += 64) rf[v] = 0;  // ready for the next iteration
+  if (threadIdx.x == 0) *word = 0;
 }
 
 // The same BZ2_hbMakeCodeLengths run by one lane per table, kHuffLanes tables per wave, for
@@ -239,6 +298,11 @@ inline uint32_t huff_lanes_min() {
   static const uint32_t v = (uint32_t)std::max(0ll, env_ll("BZG_HUFF_LANES_MIN", 4096));
   return v;
 }
+// tables per launch up to which k_huff_spec tries rounds 1 and 2 at once (the launch's latency
+// is its slowest table's; above it the extra waves cost throughput: 1 GB +2 ms with 8192);
+// BZG_HUFF_SPEC_MAX overrides (read per call: A/B knob, and 0 lets the code-length test take
+// the one-round-at-a-time path)
+inline uint32_t huff_spec_max() { return (uint32_t)std::max(0ll, env_ll("BZG_HUFF_SPEC_MAX", 2048)); }
 inline uint32_t slices_for(uint32_t nb, uint32_t lo) {
   return std::max(lo, std::min(kSliceMax, ceil_div(kSliceFill, std::max(nb, 1u))));
 }
@@ -408,25 +472,39 @@ __global__ void __launch_bounds__(kT) k_cf(uint32_t b0, const uint16_t* __restri
 // BZ2_hbMakeCodeLengths for table t of block b (one wave; the heap work is sequential).
 __global__ void __launch_bounds__(64) k_huff(uint32_t b0, const uint32_t* __restrict__ nmtf_g, const uint32_t* __restrict__ ninuse,
                                              uint32_t* __restrict__ rf_g, uint8_t* __restrict__ lens_g) {
-  __shared__ alignas(16) uint64_t heap[kHeapCap];
-  __shared__ int32_t weight[kMaxAlpha + 2];
-  __shared__ int32_t parent[kMaxAlpha * 2];
-  __shared__ uint32_t fq[kMaxAlpha];
-  __shared__ uint8_t len[kMaxAlpha + 2];
+  __shared__ HuffLds S;
   const uint32_t b = b0 + blockIdx.x / kNGroups, t = blockIdx.x % kNGroups;
   const int ng = n_groups(nmtf_g[b]);
   if ((int)t >= ng) return;
   const int alpha = (int)ninuse[b] + 2;
   uint32_t* rf = rf_g + ((size_t)b * kNGroups + t) * kMaxAlpha;
   for (int v = threadIdx.x; v < alpha; v += 64) {
-    fq[v] = rf[v];
+    S.fq[v] = rf[v];
     rf[v] = 0;  // ready for the next iteration
   }
   __syncthreads();
-  hb_code_lengths(len, fq, alpha, kMaxCodeLen, heap, weight, parent);
+  (void)hb_code_lengths<64>(S.len, S.fq, alpha, kMaxCodeLen, S.heap, S.weight, S.parent, 0);
   __syncthreads();
   uint8_t* L = lens_g + ((size_t)b * kNGroups + t) * kMaxAlpha;
-  for (int v = threadIdx.x; v < alpha; v += 64) L[v] = len[v];
+  for (int v = threadIdx.x; v < alpha; v += 64) L[v] = S.len[v];
+}
+
+// k_huff with rounds 1 and 2 of every table at once (hb_spec_table): workgroup g runs round
+// 1 + g / nt of table g % nt of the launch's nt = n * kNGroups tables.
+__global__ void __launch_bounds__(64) k_huff_spec(uint32_t b0, uint32_t nt, const uint32_t* __restrict__ nmtf_g,
+                                                  const uint32_t* __restrict__ ninuse, uint32_t* __restrict__ rf_g,
+                                                  uint8_t* __restrict__ lens_g, uint32_t* __restrict__ word_g,
+                                                  uint8_t* __restrict__ scratch_g) {
+  __shared__ HuffLds S;
+  const uint32_t r0 = blockIdx.x >= nt ? 1u : 0u, tt = blockIdx.x - r0 * nt;
+  const uint32_t b = b0 + tt / kNGroups, t = tt % kNGroups;
+  if ((int)t >= n_groups(nmtf_g[b])) return;
+  const int alpha = (int)ninuse[b] + 2;
+  const size_t g = (size_t)b * kNGroups + t;
+  uint32_t* rf = rf_g + g * kMaxAlpha;
+  for (int v = threadIdx.x; v < alpha; v += 64) S.fq[v] = rf[v];
+  __syncthreads();
+  hb_spec_table(S, alpha, kMaxCodeLen, r0, word_g + g, scratch_g + g * kMaxAlpha, lens_g + g * kMaxAlpha, rf);
 }
 
 // k_huff with kHuffLanes tables per wave (one lane each): table tt = wave * kHuffLanes + lane of
@@ -444,23 +522,32 @@ __global__ void __launch_bounds__(64) k_huff_lanes(uint32_t b0, uint32_t n, cons
                   lens_g + ((size_t)b * kNGroups + t) * kMaxAlpha);
 }
 
-// Test hook: code lengths of n tables (freq[t * kMaxAlpha ..], alpha[t], max_len) with the
-// same device routine as k_huff.
+// Test hooks: code lengths of n tables (freq[t * kMaxAlpha ..], alpha[t], max_len) with the
+// same device routines as k_huff and k_huff_spec.
 __global__ void __launch_bounds__(64) k_code_lengths_test(const uint32_t* __restrict__ freq_g,
                                                           const int32_t* __restrict__ alpha_g, int max_len,
                                                           uint8_t* __restrict__ lens_g) {
-  __shared__ alignas(16) uint64_t heap[kHeapCap];
-  __shared__ int32_t weight[kMaxAlpha + 2];
-  __shared__ int32_t parent[kMaxAlpha * 2];
-  __shared__ uint32_t fq[kMaxAlpha];
-  __shared__ uint8_t len[kMaxAlpha + 2];
+  __shared__ HuffLds S;
   const uint32_t t = blockIdx.x;
   const int alpha = alpha_g[t];
-  for (int v = threadIdx.x; v < alpha; v += 64) fq[v] = freq_g[(size_t)t * kMaxAlpha + v];
+  for (int v = threadIdx.x; v < alpha; v += 64) S.fq[v] = freq_g[(size_t)t * kMaxAlpha + v];
   __syncthreads();
-  hb_code_lengths(len, fq, alpha, max_len, heap, weight, parent);
+  (void)hb_code_lengths<64>(S.len, S.fq, alpha, max_len, S.heap, S.weight, S.parent, 0);
   __syncthreads();
-  for (int v = threadIdx.x; v < alpha; v += 64) lens_g[(size_t)t * kMaxAlpha + v] = len[v];
+  for (int v = threadIdx.x; v < alpha; v += 64) lens_g[(size_t)t * kMaxAlpha + v] = S.len[v];
+}
+
+__global__ void __launch_bounds__(64) k_code_lengths_spec(const uint32_t* __restrict__ freq_g,
+                                                          const int32_t* __restrict__ alpha_g, uint32_t n, int max_len,
+                                                          uint8_t* __restrict__ lens_g, uint32_t* __restrict__ word_g,
+                                                          uint8_t* __restrict__ scratch_g) {
+  __shared__ HuffLds S;
+  const uint32_t r0 = blockIdx.x >= n ? 1u : 0u, t = blockIdx.x - r0 * n;
+  const int alpha = alpha_g[t];
+  for (int v = threadIdx.x; v < alpha; v += 64) S.fq[v] = freq_g[(size_t)t * kMaxAlpha + v];
+  __syncthreads();
+  hb_spec_table(S, alpha, max_len, r0, word_g + t, scratch_g + (size_t)t * kMaxAlpha, lens_g + (size_t)t * kMaxAlpha,
+                nullptr);
 }
 
 __global__ void __launch_bounds__(64) k_code_lengths_lanes(const uint32_t* __restrict__ freq_g,
@@ -963,6 +1050,10 @@ void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_
   t.info = ws.u32("code_info", nbx * 8);
   t.bbits = ws.typed<uint64_t>("code_bbits", nbx + 2);
   uint32_t* rf = ws.u32("code_rf", nbx * kNGroups * kMaxAlpha);
+  // k_huff_spec: per-table words (zero between launches: the last workgroup of a table resets
+  // its word) and round-2 lengths
+  uint32_t* hword = ws.u32z("code_hword", nbx * kNGroups);
+  uint8_t* hscratch = ws.u8("code_hscratch", nbx * kNGroups * kMaxAlpha);
   if (nb == 0) return;
   HIP_OK(hipMemsetAsync(t.info, 0, nbx * 8 * 4, st));
   // Blocks are independent, and k_huff is a latency chain with a small grid that leaves the
@@ -980,15 +1071,19 @@ void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_
   for (int h = 0; h < (split ? 2 : 1); h++) {
     const uint32_t b0 = h ? half : 0, n = h ? nb - half : half;
     hipStream_t s = h ? st2 : st;
+    const uint32_t nt = n * (uint32_t)kNGroups;
+    const bool spec = nt <= huff_spec_max();
     k_init_tables<<<n, 64, 0, s>>>(b0, m.nmtf, m.freq, r.ninuse, t.lens, rf);
     HIP_OK(hipGetLastError());
     for (int it = 0; it < kIters; it++) {
       k_cf<<<dim3(slices_for(n, kCfSlices), n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 0);
       HIP_OK(hipGetLastError());
-      if (n * (uint32_t)kNGroups >= huff_lanes_min())
-        k_huff_lanes<<<ceil_div(n * (uint32_t)kNGroups, (uint32_t)kHuffLanes), 64, 0, s>>>(b0, n, m.nmtf, r.ninuse, rf, t.lens);
+      if (nt >= huff_lanes_min())
+        k_huff_lanes<<<ceil_div(nt, (uint32_t)kHuffLanes), 64, 0, s>>>(b0, n, m.nmtf, r.ninuse, rf, t.lens);
+      else if (spec)
+        k_huff_spec<<<2 * nt, 64, 0, s>>>(b0, nt, m.nmtf, r.ninuse, rf, t.lens, hword, hscratch);
       else
-        k_huff<<<n * kNGroups, 64, 0, s>>>(b0, m.nmtf, r.ninuse, rf, t.lens);
+        k_huff<<<nt, 64, 0, s>>>(b0, m.nmtf, r.ninuse, rf, t.lens);
       HIP_OK(hipGetLastError());
     }
     k_cf<<<dim3(slices_for(n, kCfSlices), n), kT, 0, s>>>(b0, m.mtfv, m.mtf_off, m.nmtf, t.lens, t.sel, rf, t.gbits, t.info, 1);
@@ -1063,11 +1158,15 @@ uint64_t code_stage(Workspace& ws, const Rle1Result& r, const MtfResult& m, cons
   return code_emit(ws, parts, level, final_batch, carry, out, out_cap, st);
 }
 
-void code_lengths_test(const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len, uint8_t* d_lens,
-                       hipStream_t st) {
+void code_lengths_test(Workspace& ws, const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len,
+                       uint8_t* d_lens, hipStream_t st) {
   if (n == 0) return;
+  uint32_t* word = ws.u32z("test_hword", n);
+  uint8_t* scratch = ws.u8("test_hscratch", (size_t)n * kMaxAlpha);
   if (huff_lanes_min() == 0) {  // BZG_HUFF_LANES_MIN=0: the lane-per-table routine (its parity tests)
     k_code_lengths_lanes<<<ceil_div(n, (uint32_t)kHuffLanes), 64, 0, st>>>(d_freq, d_alpha, n, max_len, d_lens);
+  } else if (n <= huff_spec_max()) {
+    k_code_lengths_spec<<<2 * n, 64, 0, st>>>(d_freq, d_alpha, n, max_len, d_lens, word, scratch);
   } else {
     k_code_lengths_test<<<n, 64, 0, st>>>(d_freq, d_alpha, max_len, d_lens);
   }

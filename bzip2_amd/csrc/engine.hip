@@ -1883,7 +1883,7 @@ int bzg_stage_code_lengths(const uint32_t* freq, const int32_t* alpha, uint32_t 
     uint8_t* d_lens = e.ws.u8("test_lens", nf);
     stage_copy(e, d_freq, freq, 4 * nf, hipMemcpyHostToDevice);
     stage_copy(e, d_alpha, alpha, 4 * (size_t)ntables, hipMemcpyHostToDevice);
-    code_lengths_test(d_freq, d_alpha, ntables, max_len, d_lens, e.stream);
+    code_lengths_test(e.ws, d_freq, d_alpha, ntables, max_len, d_lens, e.stream);
     HIP_OK(hipStreamSynchronize(e.stream));
     stage_copy(e, lens, d_lens, nf, hipMemcpyDeviceToHost);
     return BZ_OK;

@@ -185,8 +185,8 @@ struct StreamCarry {
 // Encodes all blocks into `out` (device), starting with the carried partial byte; when
 // `final_batch` appends the stream trailer.  Returns bytes fully written; updates carry.
 // Test hook: BZ2_hbMakeCodeLengths on n tables (kMaxAlpha frequencies each) on the GPU.
-void code_lengths_test(const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len, uint8_t* d_lens,
-                       hipStream_t st);
+void code_lengths_test(Workspace& ws, const uint32_t* d_freq, const int32_t* d_alpha, uint32_t n, int max_len,
+                       uint8_t* d_lens, hipStream_t st);
 // The per-block tables of nb blocks (selectors, code lengths, canonical codes, bit counts).
 struct CodeTables {
   uint8_t* lens = nullptr;
