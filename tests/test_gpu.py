@@ -109,6 +109,20 @@ def test_code_lengths_vs_reference(spec_max, monkeypatch):
     assert max(got[1]) == 17 and max(got[2]) <= 17  # table 2 needed rescale rounds (depth 27 unscaled)
 
 
+def test_huff_spec_stream_equals_serial(monkeypatch):
+    """k_huff_spec in a whole stream: the first 20 MB of the bench text (seed of bench.py's rank
+    0) has 5 of its 552 table runs needing a second Huffman round (blocks 6, 15, 17: iterations
+    0-3).  Rounds 1 and 2 at once (forced on every launch) and one after another give the same
+    stream, the reference's."""
+    data = datagen.text(20_000_000, 0x5EED0001)
+    monkeypatch.setenv("BZG_HUFF_SPEC_MAX", "100000")
+    spec = B.buff_to_buff_compress(data, 9)
+    monkeypatch.setenv("BZG_HUFF_SPEC_MAX", "0")
+    serial = B.buff_to_buff_compress(data, 9)
+    assert spec == serial
+    assert spec == expected(data, 9)
+
+
 RLE_CASES = {
     "text": lambda: datagen.text(2_500_000, 21),
     "random": lambda: datagen.random_bytes(700_000, 22),
