@@ -1063,9 +1063,9 @@ void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_
   // k_huff launches interleave (one half's selection beside the other half's Huffman).
   const bool split = st2 != nullptr && nb >= 64;
   hipEvent_t e_in = nullptr, e_out = nullptr;
-  if (split) {
-    HIP_OK(hipEventCreateWithFlags(&e_in, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&e_out, hipEventDisableTiming));
+  if (split) {  // (the workspace's events 2 and 3: no event created per call)
+    e_in = ws.side_event(2);
+    e_out = ws.side_event(3);
     HIP_OK(hipEventRecord(e_in, st));
     HIP_OK(hipStreamWaitEvent(st2, e_in, 0));
   }
@@ -1096,8 +1096,6 @@ void code_tables(Workspace& ws, const Rle1Result& r, const MtfResult& m, uint32_
   if (split) {
     HIP_OK(hipEventRecord(e_out, st2));
     HIP_OK(hipStreamWaitEvent(st, e_out, 0));
-    HIP_OK(hipEventDestroy(e_in));
-    HIP_OK(hipEventDestroy(e_out));
   }
 }
 

@@ -37,7 +37,7 @@ class Workspace {
   // the only user of these buffers), and the workspace's side stream and events, created once.
   void* pinned(const std::string& name, size_t bytes);
   hipStream_t side_stream();
-  hipEvent_t side_event(int k);  // k < 4
+  hipEvent_t side_event(int k);  // k < 4: 0, 1 the A5 copy-rank job, 2, 3 the table streams' fork / join
 
   const uint32_t* crc_table();   // 256 entries, MSB-first CRC-32 (poly 0x04C11DB7)
   const uint32_t* xpow2_table(); // 48 entries: x^(8*2^k) mod P
