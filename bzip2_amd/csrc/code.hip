@@ -23,68 +23,40 @@ constexpr int kT = 256;
 // max(freq,1) << 8 | 0, merge = sum of weights | (1 + max depth); heap moves use strict '<' on
 // weights only; rescale with w = 1 + w/2 while any length exceeds max_len.
 // The heap itself is sequential and runs on lane 0.  Heap entries carry their weight
-// (weight << 32 | node).  The chain of dependent LDS round trips is the cost, so a sift-down
-// loads the three levels below its node at once (2 + 4 + 8 entries, 16-byte reads) and walks
-// them in registers, and a sift-up loads three ancestors at once.  Lengths (parent-chain
-// walks) and the rescale run on all lanes.
-constexpr int kHeapCap = kMaxAlpha + 14;  // 272: the lookahead reads below a live node stay inside
+// (weight << 32 | node), so a DOWNHEAP level is one 16-byte read of the two children, and
+// UPHEAP reads one parent per level.  A heap wave is as much issue-bound as latency-bound:
+// loading two or three levels ahead (and three ancestors at once) cost more in selects than it
+// saved in round trips (profiles/r06_ab_heap_lookahead.txt: one heap 545 -> 415 us at 258
+// symbols).  Lengths (parent-chain walks) and the rescale run on all lanes.
+constexpr int kHeapCap = kMaxAlpha + 14;  // 272 entries (the 16-byte child reads stay inside)
 __device__ __forceinline__ int32_t hb_wt(uint64_t e) { return (int32_t)(e >> 32); }
 
 __device__ __forceinline__ void hb_sift_up(uint64_t* heap, int z, uint64_t item) {
-  while (z > 1) {  // heap[0] is the weight-0 sentinel above the root
-    const uint64_t p1 = heap[z >> 1], p2 = heap[z >> 2], p3 = heap[z >> 3];
-    if (!(hb_wt(item) < hb_wt(p1))) break;
-    heap[z] = p1;
-    z >>= 1;
-    if (!(hb_wt(item) < hb_wt(p2))) break;
-    heap[z] = p2;
-    z >>= 1;
-    if (!(hb_wt(item) < hb_wt(p3))) break;
-    heap[z] = p3;
+  while (hb_wt(item) < hb_wt(heap[z >> 1])) {  // heap[0]: the weight-0 sentinel stops at the root
+    heap[z] = heap[z >> 1];
     z >>= 1;
   }
   heap[z] = item;
 }
 
-// One level of the reference's DOWNHEAP (huffman.c:46-59) with the node's two children in
-// registers: returns false (stop) when item stays at z; otherwise moves the smaller child up
-// (the right one only when strictly smaller) and returns its side in k.
-__device__ __forceinline__ bool hb_down_step(uint64_t* heap, int& z, int nheap, uint64_t item, uint64_t l, uint64_t r,
-                                             int& k) {
-  const int y = 2 * z;
-  if (y > nheap) return false;
-  uint64_t c = l;
-  k = 0;
-  if (y < nheap && hb_wt(r) < hb_wt(l)) {
-    c = r;
-    k = 1;
-  }
-  if (hb_wt(item) < hb_wt(c)) return false;
-  heap[z] = c;
-  z = y + k;
-  return true;
-}
-
+// The reference's DOWNHEAP (huffman.c:46-59): at each level the smaller child (the right one
+// only when strictly smaller) moves up unless item is strictly lighter.
 __device__ __forceinline__ void hb_sift_down(uint64_t* heap, int nheap, uint64_t item) {
-  const uint4* h4 = reinterpret_cast<const uint4*>(heap);
-  constexpr int kQ = kHeapCap / 2;  // 16-byte words in the heap
-  auto lo = [](uint4 q) { return ((uint64_t)q.y << 32) | q.x; };
-  auto hi = [](uint4 q) { return ((uint64_t)q.w << 32) | q.z; };
+  const uint4* h4 = reinterpret_cast<const uint4*>(heap);  // h4[z] = heap[2z], heap[2z + 1]
   int z = 1;
   for (;;) {
-    if (2 * z > nheap) break;
-    // heap[2z..2z+1], heap[4z..4z+3], heap[8z..8z+7]; past the live heap the words are clamped
-    // inside the array and never used
-    const uint4 a = h4[z];
-    const uint4 b0 = h4[min(2 * z, kQ - 2)], b1 = h4[min(2 * z, kQ - 2) + 1];
-    const int ci = min(4 * z, kQ - 4);
-    const uint4 c0 = h4[ci], c1 = h4[ci + 1], c2 = h4[ci + 2], c3 = h4[ci + 3];
-    int k1, k2, k3;
-    if (!hb_down_step(heap, z, nheap, item, lo(a), hi(a), k1)) break;
-    const uint4 b = k1 ? b1 : b0;
-    if (!hb_down_step(heap, z, nheap, item, lo(b), hi(b), k2)) break;
-    const uint4 c = k1 ? (k2 ? c3 : c2) : (k2 ? c1 : c0);
-    if (!hb_down_step(heap, z, nheap, item, lo(c), hi(c), k3)) break;
+    const int y = 2 * z;
+    if (y > nheap) break;
+    const uint4 q = h4[z];
+    uint64_t c = ((uint64_t)q.y << 32) | q.x;
+    int k = 0;
+    if (y < nheap && (int32_t)q.w < (int32_t)q.y) {
+      c = ((uint64_t)q.w << 32) | q.z;
+      k = 1;
+    }
+    if (hb_wt(item) < hb_wt(c)) break;
+    heap[z] = c;
+    z = y + k;
   }
   heap[z] = item;
 }
