@@ -272,11 +272,11 @@ inline uint32_t huff_lanes_min() {
 }
 // tables per launch up to which k_huff_spec tries rounds 1 and 2 at once (the launch's latency
 // is its slowest table's; above it the extra waves cost throughput: code stage per call with
-// and without, 336 tables per launch (100 MB): -0.06..-0.08 ms, 834 (250 MB): even, 1,668
-// (500 MB): +1.0 ms, 3,336 (1 GB): +2 ms);
+// and without, 336 tables per launch (100 MB): -0.23 ms, 834 (250 MB): -0.07 ms, 1,668
+// (500 MB, measured with the round-5 heap): +1.0 ms, 3,336 (1 GB): +2 ms);
 // BZG_HUFF_SPEC_MAX overrides (read per call: A/B knob, and 0 lets the code-length test take
 // the one-round-at-a-time path)
-inline uint32_t huff_spec_max() { return (uint32_t)std::max(0ll, env_ll("BZG_HUFF_SPEC_MAX", 512)); }
+inline uint32_t huff_spec_max() { return (uint32_t)std::max(0ll, env_ll("BZG_HUFF_SPEC_MAX", 1024)); }
 inline uint32_t slices_for(uint32_t nb, uint32_t lo) {
   return std::max(lo, std::min(kSliceMax, ceil_div(kSliceFill, std::max(nb, 1u))));
 }
